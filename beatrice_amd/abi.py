@@ -1,0 +1,308 @@
+"""ctypes binding of the C-ABI in include/beatrice_gpu.h (libbeatrice_gpu.so).
+
+This is the Python-side caller of the drop-in boundary, used by tests/ and bench.py;
+the production caller is the C++ adapter in beatrice_amd/host/. There is no CPU
+fallback: if the HIP library is missing or no GPU is visible, Context() raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbeatrice_gpu.so")
+
+BT_REC_BYTES = 96
+BT_MAX_FILTERS = 64
+
+# FilterType order (reference include/beatrice/PacketFilter.hpp:17-24)
+BPF, PROTOCOL, IP_RANGE, PORT_RANGE, PAYLOAD, CUSTOM = range(6)
+DECIDE_PASS, DECIDE_REJECT, DECIDE_THROW, DECIDE_HOST = range(4)
+KINDS = ["TRUE", "FALSE", "BPF", "PROTO_EQ", "PROTO_NZ", "IP_MASK", "PORT", "IP_THROW", "PORT_THROW", "HOST"]
+
+L_ETH, L_VLAN0, L_VLAN1, L_IPV4, L_IPV6, L_TCP, L_UDP, L_ICMP = (1 << i for i in range(8))
+
+# numpy view of bt_rec (96 B, include/beatrice_gpu.h)
+REC_DTYPE = np.dtype({
+    "names": ["eth_dst", "eth_src", "ethertype", "pkt_len", "vlan_tpid", "vlan_tci", "present", "ok",
+              "l3_off", "l4_off", "l3", "l4", "reserved"],
+    "formats": [("u1", 6), ("u1", 6), "<u2", "<u2", ("<u2", 2), ("<u2", 2), "u1", "u1", "u1", "u1",
+                ("u1", 40), ("u1", 20), ("u1", 8)],
+    "offsets": [0, 6, 12, 14, 16, 20, 24, 25, 26, 27, 28, 68, 88],
+    "itemsize": 96,
+})
+
+
+class BtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"beatrice_gpu error {code}: {msg}")
+        self.code = code
+
+
+class FilterDesc(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("expression", ctypes.c_char_p), ("enabled", ctypes.c_int32),
+                ("priority", ctypes.c_int32), ("has_custom_func", ctypes.c_int32)]
+
+
+class FilterSlot(ctypes.Structure):
+    _fields_ = [("source_index", ctypes.c_uint32), ("kind", ctypes.c_uint32), ("a", ctypes.c_uint32),
+                ("b", ctypes.c_uint32), ("throw_kind", ctypes.c_int32)]
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("host_chunk_packets", ctypes.c_uint32), ("host_chunk_bytes", ctypes.c_uint32),
+                ("grid_waves", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("stride", ctypes.c_uint32),
+                ("n", ctypes.c_uint32), ("bytes", ctypes.c_uint64)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_void_p), ("n_cap", ctypes.c_uint32), ("verdict", ctypes.c_void_p),
+                ("decide", ctypes.c_void_p), ("pass_idx", ctypes.c_void_p), ("n_pass", ctypes.c_void_p)]
+
+
+EXPORTS = [
+    "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
+    "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
+    "bt_parse_filter", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
+    "bt_synchronize", "bt_time_device", "bt_record_gather",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: the gfx950 extension was not built "
+                           "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    sig = {
+        "bt_abi_version": (ctypes.c_int, []),
+        "bt_last_error": (ctypes.c_char_p, []),
+        "bt_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Opts), ctypes.POINTER(vp)]),
+        "bt_destroy": (None, [vp]),
+        "bt_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "bt_filter_compile": (ctypes.c_int, [vp, ctypes.POINTER(FilterDesc), u32]),
+        "bt_filter_program": (ctypes.c_int, [vp, ctypes.POINTER(FilterSlot), u32, ctypes.POINTER(u32)]),
+        "bt_filter_compile_host": (ctypes.c_int, [ctypes.POINTER(FilterDesc), u32, ctypes.POINTER(FilterSlot),
+                                                  u32, ctypes.POINTER(u32)]),
+        "bt_reserve": (ctypes.c_int, [vp, u32]),
+        "bt_parse_filter_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), vp]),
+        "bt_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_dev_malloc": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
+        "bt_dev_free": (ctypes.c_int, [vp, vp]),
+        "bt_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),
+        "bt_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, u64]),
+        "bt_memset_d": (ctypes.c_int, [vp, vp, ctypes.c_int, u64]),
+        "bt_synchronize": (ctypes.c_int, [vp]),
+        "bt_time_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
+                                          ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+        "bt_record_gather": (None, [vp, u32, u32, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _ = i32
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise BtError(rc, lib().bt_last_error().decode(errors="replace"))
+
+
+def filter_descs(filters):
+    """filters: list of dicts {type, expr, enabled=1, priority=0, custom=0}."""
+    arr = (FilterDesc * max(1, len(filters)))()
+    keep = []
+    for i, f in enumerate(filters):
+        e = f.get("expr", "").encode()
+        keep.append(e)
+        arr[i] = FilterDesc(f["type"], e, int(f.get("enabled", 1)), int(f.get("priority", 0)),
+                            int(bool(f.get("custom", 0))))
+    arr._keep = keep
+    return arr
+
+
+def compile_host(filters):
+    """Host-only compile (no GPU needed): list of FilterSlot in evaluation order."""
+    arr = filter_descs(filters)
+    out = (FilterSlot * BT_MAX_FILTERS)()
+    n = ctypes.c_uint32(0)
+    _check(lib().bt_filter_compile_host(arr, len(filters), out, BT_MAX_FILTERS, ctypes.byref(n)))
+    return [out[i] for i in range(n.value)]
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().bt_device_count(ctypes.byref(n))
+    return n.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p(0)
+        _check(lib().bt_dev_malloc(ctx.h, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(lib().bt_memcpy_h2d(self.ctx.h, self.ptr, arr.ctypes.data, arr.nbytes))
+
+    def download(self, arr: np.ndarray):
+        assert arr.flags.c_contiguous and arr.nbytes <= self.nbytes
+        _check(lib().bt_memcpy_d2h(self.ctx.h, arr.ctypes.data, self.ptr, arr.nbytes))
+        return arr
+
+    def zero(self):
+        _check(lib().bt_memset_d(self.ctx.h, self.ptr, 0, self.nbytes))
+
+    def free(self):
+        if self.ptr:
+            lib().bt_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One bt_ctx on one device."""
+
+    def __init__(self, device: int = 0, host_chunk_packets: int = 0, grid_waves: int = 0):
+        opts = Opts()
+        opts.host_chunk_packets = host_chunk_packets
+        opts.grid_waves = grid_waves
+        h = ctypes.c_void_p(0)
+        _check(lib().bt_create(device, ctypes.byref(opts), ctypes.byref(h)))
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().bt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compile(self, filters):
+        arr = filter_descs(filters)
+        _check(lib().bt_filter_compile(self.h, arr, len(filters)))
+        return self.program()
+
+    def program(self):
+        out = (FilterSlot * BT_MAX_FILTERS)()
+        n = ctypes.c_uint32(0)
+        _check(lib().bt_filter_program(self.h, out, BT_MAX_FILTERS, ctypes.byref(n)))
+        return [out[i] for i in range(n.value)]
+
+    def reserve(self, n: int):
+        _check(lib().bt_reserve(self.h, n))
+
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def synchronize(self):
+        _check(lib().bt_synchronize(self.h))
+
+    def run_device(self, batch: Batch, outs: Outputs, stream=None):
+        _check(lib().bt_parse_filter_device(self.h, ctypes.byref(batch), ctypes.byref(outs), stream))
+
+    def time_device(self, batch: Batch, outs: Outputs, iters: int):
+        a, b = ctypes.c_float(0), ctypes.c_float(0)
+        _check(lib().bt_time_device(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(a),
+                                    ctypes.byref(b)))
+        return a.value, b.value
+
+    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
+        """bt_parse_filter over host buffers. Returns dict of numpy outputs."""
+        n = len(desc)
+        rec = np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None
+        ver = np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None
+        dec = np.zeros(n, dtype=np.uint8) if filters else None
+        pidx = np.zeros(max(n, 1), dtype=np.uint32) if filters else None
+        npass = np.zeros(1, dtype=np.uint32) if filters else None
+        p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        data = np.ascontiguousarray(data)
+        desc = np.ascontiguousarray(desc, dtype=np.uint64)
+        _check(lib().bt_parse_filter(self.h, p(data), p(desc), n, p(rec), p(ver), p(dec), p(pidx), p(npass)))
+        out = {"records": rec, "verdict": ver, "decide": dec}
+        if filters:
+            out["pass_idx"] = pidx[: int(npass[0])]
+            out["n_pass"] = int(npass[0])
+        return out
+
+
+class DeviceRun:
+    """Device-resident batch + outputs (the bench / parity path)."""
+
+    def __init__(self, ctx: Context, data: np.ndarray, desc: np.ndarray | None, n: int, stride: int = 0,
+                 records=True, decide=True, verdict=True, pass_idx=True):
+        self.ctx, self.n = ctx, n
+        self.d_data = ctx.alloc((data.nbytes + 255) // 256 * 256 + 256)
+        self.d_data.upload(data)
+        self.d_desc = None
+        if desc is not None:
+            self.d_desc = ctx.alloc(max(8, desc.nbytes))
+            self.d_desc.upload(np.ascontiguousarray(desc, dtype=np.uint64))
+        self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n,
+                           int(data.nbytes))
+        nt = (n + 63) // 64
+        self.d_rec = ctx.alloc(max(16, n * BT_REC_BYTES)) if records else None
+        self.d_dec = ctx.alloc(max(16, n)) if decide else None
+        self.d_ver = ctx.alloc(max(16, nt * 8)) if verdict else None
+        self.d_pidx = ctx.alloc(max(16, n * 4)) if pass_idx else None
+        self.d_npass = ctx.alloc(16) if pass_idx else None
+        self.outs = Outputs(self.d_rec.ptr if self.d_rec else None, n,
+                            self.d_ver.ptr if self.d_ver else None,
+                            self.d_dec.ptr if self.d_dec else None,
+                            self.d_pidx.ptr if self.d_pidx else None,
+                            self.d_npass.ptr if self.d_npass else None)
+        ctx.reserve(n)
+
+    def run(self):
+        self.ctx.run_device(self.batch, self.outs)
+
+    def fetch(self):
+        n = self.n
+        out = {}
+        self.ctx.synchronize()
+        if self.d_rec:
+            planes = np.zeros((6, n, 16), dtype=np.uint8)
+            self.d_rec.download(planes.reshape(-1))
+            out["records"] = np.ascontiguousarray(planes.transpose(1, 0, 2)).reshape(n, 96)
+        if self.d_dec:
+            out["decide"] = self.d_dec.download(np.zeros(n, dtype=np.uint8))
+        if self.d_ver:
+            out["verdict"] = self.d_ver.download(np.zeros((n + 63) // 64, dtype=np.uint64))
+        if self.d_pidx:
+            npass = int(self.d_npass.download(np.zeros(1, dtype=np.uint32))[0])
+            out["n_pass"] = npass
+            out["pass_idx"] = self.d_pidx.download(np.zeros(max(npass, 1), dtype=np.uint32))[:npass]
+        return out
+
+    def free(self):
+        for b in (self.d_data, self.d_desc, self.d_rec, self.d_dec, self.d_ver, self.d_pidx, self.d_npass):
+            if b is not None:
+                b.free()

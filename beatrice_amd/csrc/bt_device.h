@@ -1,0 +1,57 @@
+// bt_device.h — shared between the host runtime and the gfx950 kernels.
+#pragma once
+
+#include <stdint.h>
+
+#include "beatrice_gpu.h"
+
+namespace bt {
+
+// Compiled filter slot as the device sees it (16 B; kernel-argument resident).
+struct DevFilter {
+    uint32_t kind, a, b, pad;
+};
+
+struct DevProgram {
+    uint32_t n;
+    uint32_t pad[3];
+    DevFilter f[BT_MAX_FILTERS];
+};
+
+// Everything the main kernel needs (passed by value as a kernel argument).
+struct MainArgs {
+    const uint8_t* base;
+    const uint64_t* desc;      // nullptr: fixed stride
+    uint64_t bytes;            // readable size of base (rounded up to 16 by the caller)
+    uint32_t stride;
+    uint32_t n;
+    uint32_t ntiles;           // ceil(n / 64): one wavefront tile = 64 packets
+    uint32_t n_cap;            // record plane stride (records)
+    uint8_t* records;          // plane-major (or AoS when the AOS variant is launched)
+    uint8_t* decide;
+    uint64_t* verdict;
+    uint32_t* tile_pass;       // per-tile pass counts (compaction input)
+};
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kRowDwords = 33;                    // 128 B header window + 4 B pad (bank spread)
+constexpr int kChunkTiles = 1024;                 // compaction chunk = 64Ki packets
+constexpr uint32_t kNeedParse = 102;              // 14 + 2*4 + 60 (IPv4 max) + 20 (TCP fields)
+constexpr uint32_t kNeedFilter = 38;              // PacketFilter reads bytes 12..37
+
+// Launch wrappers (bt_kernels.hip). All are asynchronous on `stream`.
+enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2 };
+int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
+                int grid_blocks, void* stream);
+int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
+                   uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream);
+int device_grid_blocks(int device);
+
+// Host filter compiler (bt_filter_compile.cpp): pure C++, no device needed.
+int compile_filters(const bt_filter_desc* f, uint32_t n, bt_filter_slot* out, uint32_t cap,
+                    uint32_t* n_slots, char* err, size_t errlen);
+void to_device_program(const bt_filter_slot* s, uint32_t n, DevProgram* p);
+
+}  // namespace bt

@@ -1,0 +1,447 @@
+// bt_kernels.hip — gfx950 kernels for the Beatrice parse+filter stage.
+//
+// bt_parse_filter_main: one packet per lane, one 64-packet tile per wavefront,
+// persistent grid-stride over tiles. Per tile:
+//   1. LOAD   — the wave fetches the 64 header windows (<=128 B each, 16-B aligned
+//               chunks) with coalesced global_load_dwordx4: in descriptor mode 8 lanes
+//               cover one packet's window (8 packets per instruction); in fixed-stride
+//               mode the tile is one contiguous span (1 KiB per instruction).
+//               Chunks are written into a per-wave LDS image, one 132-B row per packet
+//               (33 dwords: the odd stride spreads the later per-lane reads over banks).
+//   2. PARSE  — each lane walks its own row: Ethernet, up to two 802.1Q/802.1ad tags,
+//               IPv4/IPv6, TCP/UDP/ICMP (DESIGN.md "R-WALK"). Unaligned header windows
+//               are rebuilt from aligned ds_read_b32 pairs with v_alignbyte_b32. The
+//               96-B bt_rec is assembled in registers and written as six 16-B slab
+//               stores (plane-major: 1 KiB per wave instruction) or AoS for host copies.
+//   3. FILTER — the compiled PacketFilter program (kernel argument, scalar loads) is
+//               evaluated wave-uniformly slot by slot with early exit once every lane
+//               has decided; the verdict is a wavefront __ballot word and the per-tile
+//               pass count feeds the ordered compaction kernels below.
+// Replaces the per-packet work of reference src/parser/ProtocolParser.cpp:238-433 and
+// src/PacketFilter.cpp:57-372 (see DESIGN.md for the line-by-line mapping).
+#include <hip/hip_runtime.h>
+
+#include "bt_device.h"
+
+namespace bt {
+namespace {
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) {
+    return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t be16_of(const uint32_t* w, int i) {
+    return (byte_of(w, i) << 8) | byte_of(w, i + 1);
+}
+__device__ __forceinline__ uint32_t be32_of(const uint32_t* w, int i) {
+    return (byte_of(w, i) << 24) | (byte_of(w, i + 1) << 16) | (byte_of(w, i + 2) << 8) | byte_of(w, i + 3);
+}
+
+// K little-endian dwords starting at byte `a` of the LDS image (any alignment).
+template <int K>
+__device__ __forceinline__ void window(const uint32_t* lds, uint32_t a, uint32_t* out) {
+    const uint32_t d = a >> 2, sh = a & 3u;
+    uint32_t prev = lds[d];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint32_t next = lds[d + k + 1];
+        out[k] = __builtin_amdgcn_alignbyte(next, prev, sh);
+        prev = next;
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // Lanes of one wavefront hand rows to each other through LDS: keep the compiler
+    // from moving LDS accesses across this point and drain the LDS queue.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ bool is_vlan(uint32_t et) { return et == 0x8100u || et == 0x88A8u; }
+
+struct Parsed {
+    uint32_t r[24];   // bt_rec as 24 little-endian dwords
+};
+
+// The layer walk + field extraction for one packet whose byte 0 sits at byte `s` of
+// the lane's LDS row. Field semantics: ProtocolRegistry.cpp tables, extractValue<T>
+// big-endian decode, all-or-nothing per layer (ProtocolParser.cpp:244-247).
+__device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, uint32_t len,
+                                             const uint32_t* w0, Parsed& p) {
+    const uint32_t pl = len > 0xFFFFu ? 0xFFFFu : len;
+    // Ethernet (ProtocolRegistry.cpp:150-159): total length 14
+    const bool eth_ok = len >= 14;
+    const uint32_t et0 = be16_of(w0, 12);
+    p.r[0] = eth_ok ? w0[0] : 0;
+    p.r[1] = eth_ok ? w0[1] : 0;
+    p.r[2] = eth_ok ? w0[2] : 0;
+    p.r[3] = (eth_ok ? et0 : 0u) | (pl << 16);
+
+    // VLAN tags (ProtocolRegistry.cpp:289-297): slice k at 12+4k, total length 4
+    const bool v0 = eth_ok && is_vlan(et0);
+    const bool v0ok = v0 && len >= 16;
+    const bool has_et1 = v0ok && len >= 18;
+    const uint32_t et1 = be16_of(w0, 16);
+    const bool v1 = has_et1 && is_vlan(et1);
+    const bool v1ok = v1 && len >= 20;
+    const bool has_et2 = v1ok && len >= 22;
+    const uint32_t et2 = be16_of(w0, 20);
+    const uint32_t tci0 = be16_of(w0, 14), tci1 = be16_of(w0, 18);
+    p.r[4] = (v0ok ? et0 : 0u) | ((v1ok ? et1 : 0u) << 16);
+    p.r[5] = (v0ok ? tci0 : 0u) | ((v1ok ? tci1 : 0u) << 16);
+
+    bool have_et;
+    uint32_t l3et, o3;
+    if (!v0) { have_et = eth_ok; l3et = et0; o3 = 14; }
+    else if (!v1) { have_et = has_et1; l3et = et1; o3 = 18; }
+    else { have_et = has_et2; l3et = et2; o3 = 22; }
+    const bool is4 = have_et && l3et == 0x0800u;
+    const bool is6 = have_et && l3et == 0x86DDu;
+    const bool v4ok = is4 && len >= o3 + 20;
+    const bool v6ok = is6 && len >= o3 + 40;
+
+    uint32_t w3[10];
+    window<10>(row, s + o3, w3);
+    const uint32_t b0 = byte_of(w3, 0);
+    const uint32_t proto = byte_of(w3, 9), nh = byte_of(w3, 6);
+    uint32_t o4 = is4 ? o3 + 4u * (b0 & 0x0Fu) : o3 + 40u;
+    uint32_t l4 = 0;
+    if (v4ok && o4 <= len) l4 = proto == 6 ? BT_L_TCP : proto == 17 ? BT_L_UDP : proto == 1 ? BT_L_ICMP : 0u;
+    if (v6ok) l4 = nh == 6 ? BT_L_TCP : nh == 17 ? BT_L_UDP : 0u;
+
+    // L3 union at byte 28 (dwords 7..16); branch-free selects keep p.r in VGPRs
+    {   // IPv4: ProtocolRegistry.cpp:161-178, IPv6: :180-192
+        const uint32_t v4[10] = {b0 | (b0 << 8) | (byte_of(w3, 1) << 16) | (byte_of(w3, 8) << 24),
+                                 proto | (be16_of(w3, 2) << 16),
+                                 be16_of(w3, 4) | (be16_of(w3, 6) << 16),
+                                 be16_of(w3, 10),
+                                 w3[3], w3[4], 0u, 0u, 0u, 0u};
+        const uint32_t v6[10] = {be32_of(w3, 0),
+                                 be16_of(w3, 4) | (nh << 16) | (byte_of(w3, 7) << 24),
+                                 w3[2], w3[3], w3[4], w3[5], w3[6], w3[7], w3[8], w3[9]};
+#pragma unroll
+        for (int k = 0; k < 10; ++k) p.r[7 + k] = v4ok ? v4[k] : (v6ok ? v6[k] : 0u);
+    }
+
+    // L4 union at byte 68 (dwords 17..21)
+    uint32_t w4[5];
+    window<5>(row, s + (l4 ? o4 : 0u), w4);
+    const bool tcp_ok = l4 == BT_L_TCP && len >= o4 + 20;
+    const bool udp_ok = l4 == BT_L_UDP && len >= o4 + 8;
+    const bool icmp_ok = l4 == BT_L_ICMP && len >= o4 + 8;
+    {   // TCP :194-209, UDP :211-221, ICMP :223-234
+        const uint32_t ports = be16_of(w4, 0) | (be16_of(w4, 2) << 16);
+        const uint32_t icmp0 = byte_of(w4, 0) | (byte_of(w4, 1) << 8) | (be16_of(w4, 2) << 16);
+        const uint32_t pair45 = be16_of(w4, 4) | (be16_of(w4, 6) << 16);
+        p.r[17] = tcp_ok || udp_ok ? ports : (icmp_ok ? icmp0 : 0u);
+        p.r[18] = tcp_ok ? be32_of(w4, 4) : (udp_ok || icmp_ok ? pair45 : 0u);
+        p.r[19] = tcp_ok ? be32_of(w4, 8) : 0u;
+        p.r[20] = tcp_ok ? byte_of(w4, 12) | (byte_of(w4, 13) << 8) | (be16_of(w4, 14) << 16) : 0u;
+        p.r[21] = tcp_ok ? be16_of(w4, 16) | (be16_of(w4, 18) << 16) : 0u;
+    }
+
+    const uint32_t l3bit = is4 ? BT_L_IPV4 : is6 ? BT_L_IPV6 : 0u;
+    const uint32_t present = BT_L_ETH | (v0 ? BT_L_VLAN0 : 0u) | (v1 ? BT_L_VLAN1 : 0u) | l3bit | l4;
+    const uint32_t okbits = (eth_ok ? BT_L_ETH : 0u) | (v0ok ? BT_L_VLAN0 : 0u) | (v1ok ? BT_L_VLAN1 : 0u) |
+                            (v4ok ? BT_L_IPV4 : 0u) | (v6ok ? BT_L_IPV6 : 0u) |
+                            (tcp_ok ? BT_L_TCP : 0u) | (udp_ok ? BT_L_UDP : 0u) | (icmp_ok ? BT_L_ICMP : 0u);
+    p.r[6] = present | (okbits << 8) | ((l3bit ? o3 : 0u) << 16) | ((l4 ? o4 : 0u) << 24);
+    p.r[22] = p.r[23] = 0;
+}
+
+// One filter slot on one packet: 1 pass, 0 reject, 2 throw, 3 host.
+// The gates are the reference's: every built-in filter needs length >= 34 and
+// EtherType 0x0800 at frame byte 12 (VLAN/IPv6 frames fail, SURVEY §8(a) R-QUIRK-F);
+// the port filter reads L4 at the fixed offset 34 (:264-276).
+struct FilterIn {
+    bool gate;          // len >= 34 && frame[12..13] == 0x0800
+    bool l4_ok;         // (proto 6 && len >= 54) || (proto 17 && len >= 42)
+    uint32_t proto, src, dst, sport, dport;
+};
+
+__device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_t b, const FilterIn& x) {
+    switch (kind) {
+    case BT_K_TRUE: return 1;
+    case BT_K_FALSE: return 0;
+    case BT_K_BPF:
+        return x.gate && (((a & 1u) && x.proto == 6) || ((a & 2u) && x.proto == 17) || ((a & 4u) && x.proto == 1));
+    case BT_K_PROTO_EQ: return x.gate && x.proto == a;
+    case BT_K_PROTO_NZ: return x.gate && x.proto != 0;
+    case BT_K_IP_MASK: return x.gate && (((x.src & b) == a) || ((x.dst & b) == a));
+    case BT_K_PORT:
+        return x.gate && x.l4_ok && ((x.sport >= a && x.sport <= b) || (x.dport >= a && x.dport <= b));
+    case BT_K_IP_THROW: return x.gate ? 2u : 0u;
+    case BT_K_PORT_THROW: return (x.gate && x.l4_ok) ? 2u : 0u;
+    default: return 3;   // BT_K_HOST
+    }
+}
+
+template <int FIXED_LOG2, int REC, bool FILTER>
+__global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
+    // Per-wave LDS image: 64 rows x 33 dwords.
+    __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRowDwords];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = threadIdx.x >> 6;
+    uint32_t* img = lds_all + wid * (kWave * kRowDwords);
+    const uint32_t* row = img + lane * kRowDwords;
+
+    const uint32_t total_waves = gridDim.x * kWavesPerBlock;
+    const uint32_t need = REC != kRecNone ? kNeedParse : kNeedFilter;
+
+    for (uint32_t t = blockIdx.x * kWavesPerBlock + wid; t < a.ntiles; t += total_waves) {
+        const uint32_t p0 = t * 64u;
+        const uint32_t my = p0 + lane;
+        const bool live = my < a.n;
+
+        // ---- 1. LOAD --------------------------------------------------------
+        uint64_t my_off;
+        uint32_t my_len;
+        if constexpr (FIXED_LOG2 >= 0) {
+            constexpr int kL = FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0;
+            my_off = (uint64_t)my * a.stride;
+            my_len = a.stride;
+            constexpr uint32_t cpp = 1u << kL;                 // 16-B chunks per packet
+            const uint8_t* span = a.base + (uint64_t)p0 * a.stride;
+            uint4 v[cpp];
+#pragma unroll
+            for (uint32_t j = 0; j < cpp; ++j) {
+                const uint32_t g = j * 64u + lane;
+                const uint32_t q = g >> kL;
+                const bool ok = p0 + q < a.n;
+                v[j] = ok ? *reinterpret_cast<const uint4*>(span + (uint64_t)g * 16u) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < cpp; ++j) {
+                const uint32_t g = j * 64u + lane;
+                const uint32_t q = g >> kL, c = g & (cpp - 1u);
+                uint32_t* dst = img + q * kRowDwords + c * 4u;
+                dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+            }
+        } else {
+            if (a.desc) {
+                const uint64_t d = live ? a.desc[my] : 0ull;
+                my_off = d & 0xFFFFFFFFFFFFull;
+                my_len = (uint32_t)(d >> 48);
+            } else {
+                my_off = live ? (uint64_t)my * a.stride : 0ull;
+                my_len = live ? a.stride : 0u;
+            }
+            const uint32_t off_lo = (uint32_t)my_off, off_hi = (uint32_t)(my_off >> 32);
+            const uint32_t c = lane & 7u;
+            uint4 v[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t q = j * 8u + (lane >> 3);
+                const uint64_t qo = ((uint64_t)(uint32_t)__shfl((int)off_hi, (int)q) << 32) |
+                                    (uint32_t)__shfl((int)off_lo, (int)q);
+                const uint32_t ql = (uint32_t)__shfl((int)my_len, (int)q);
+                const uint64_t a0 = qo & ~15ull;
+                const uint32_t sq = (uint32_t)qo & 15u;
+                const uint32_t nq = ql < need ? ql : need;
+                const uint64_t addr = a0 + 16u * c;
+                const bool ok = (p0 + q < a.n) && (16u * c < sq + nq) && (addr + 16u <= a.bytes);
+                v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t q = j * 8u + (lane >> 3);
+                uint32_t* dst = img + q * kRowDwords + c * 4u;
+                dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+            }
+        }
+        wave_lds_sync();
+
+        // ---- 2. PARSE -------------------------------------------------------
+        const uint32_t s = (FIXED_LOG2 >= 0) ? 0u : ((uint32_t)my_off & 15u);
+        const uint32_t len = live ? my_len : 0u;
+        uint32_t w0[10];
+        window<10>(row, s, w0);
+
+        if (REC != kRecNone && live) {
+            Parsed p;
+            parse_packet(row, s, len, w0, p);
+            if (REC == kRecPlanes) {
+                uint4* planes = reinterpret_cast<uint4*>(a.records);
+#pragma unroll
+                for (int k = 0; k < BT_REC_SLABS; ++k)
+                    planes[(uint64_t)k * a.n_cap + my] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
+            } else {
+                uint4* rec = reinterpret_cast<uint4*>(a.records + (uint64_t)my * BT_REC_BYTES);
+#pragma unroll
+                for (int k = 0; k < BT_REC_SLABS; ++k)
+                    rec[k] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
+            }
+        }
+
+        // ---- 3. FILTER ------------------------------------------------------
+        if (FILTER) {
+            FilterIn x;
+            x.gate = len >= 34 && be16_of(w0, 12) == 0x0800u;
+            x.proto = byte_of(w0, 23);
+            x.src = be32_of(w0, 26);
+            x.dst = be32_of(w0, 30);
+            x.sport = be16_of(w0, 34);
+            x.dport = be16_of(w0, 36);
+            x.l4_ok = (x.proto == 6 && len >= 54) || (x.proto == 17 && len >= 42);
+            uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
+            bool open = live;
+            for (uint32_t f = 0; f < prog.n; ++f) {
+                if (__ballot(open) == 0ull) break;
+                const uint32_t r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
+                if (open && r != 1u) {
+                    code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+                    slot = f;
+                    open = false;
+                }
+            }
+            const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
+            if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
+            if (lane == 0) {
+                if (a.verdict) a.verdict[t] = pass;
+                if (a.tile_pass) a.tile_pass[t] = (uint32_t)__popcll(pass);
+            }
+        }
+        wave_lds_sync();   // the next tile overwrites this wave's image
+    }
+}
+
+// ---- ordered compaction of passing packet indices ---------------------------------
+// K2: chunk_sums[c] = sum of tile_pass over chunk c (kChunkTiles tiles).
+__global__ __launch_bounds__(256) void bt_chunk_sums(const uint32_t* tile_pass, uint32_t ntiles,
+                                                     uint32_t* chunk_sums) {
+    __shared__ uint32_t red[4];
+    const uint32_t c = blockIdx.x;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < kChunkTiles; i += 256) {
+        const uint32_t t = c * kChunkTiles + i;
+        if (t < ntiles) s += tile_pass[t];
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) chunk_sums[c] = red[0] + red[1] + red[2] + red[3];
+}
+
+// K3: block c scans its chunk's tile counts, adds the prefix of earlier chunks and
+// writes the indices of passing packets in ascending order (one wave per tile row:
+// the set lanes of one verdict word store to consecutive slots).
+__global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const uint32_t* tile_pass,
+                                                  const uint32_t* chunk_sums, uint32_t nchunks,
+                                                  uint32_t ntiles, uint32_t* pass_idx, uint32_t* n_pass) {
+    __shared__ uint32_t tile_off[kChunkTiles];
+    __shared__ uint32_t red[4];
+    __shared__ uint32_t wsum[4];
+    const uint32_t c = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+
+    // prefix of earlier chunks (and the grand total for n_pass)
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t i = tid; i < nchunks; i += 256) {
+        const uint32_t v = chunk_sums[i];
+        tot += v;
+        if (i < c) pre += v;
+    }
+    for (int o = 32; o > 0; o >>= 1) { pre += __shfl_xor(pre, o); tot += __shfl_xor(tot, o); }
+    if (lane == 0) { red[wid] = pre; wsum[wid] = tot; }
+    __syncthreads();
+    const uint32_t base = red[0] + red[1] + red[2] + red[3];
+    if (c == 0 && tid == 0 && n_pass) *n_pass = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (!pass_idx) return;   // count only
+    __syncthreads();
+
+    // exclusive scan of this chunk's tile counts: thread tid owns tiles 4*tid..4*tid+3
+    uint32_t v[4], run = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t = c * kChunkTiles + 4 * tid + k;
+        v[k] = t < ntiles ? tile_pass[t] : 0u;
+        run += v[k];
+    }
+    uint32_t incl = run;   // inclusive wave scan of per-thread sums
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) red[wid] = incl;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (uint32_t w = 0; w < wid; ++w) wpre += red[w];
+    uint32_t e = base + wpre + incl - run;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { tile_off[4 * tid + k] = e; e += v[k]; }
+    __syncthreads();
+
+    // scatter: wave wid handles tiles wid, wid+4, ... of the chunk
+    for (uint32_t i = wid; i < kChunkTiles; i += 4) {
+        const uint32_t t = c * kChunkTiles + i;
+        if (t >= ntiles) break;
+        const uint64_t word = verdict[t];
+        if (word == 0ull) continue;
+        if ((word >> lane) & 1ull) {
+            const uint32_t below = (uint32_t)__popcll(word & ((1ull << lane) - 1ull));
+            pass_idx[tile_off[i] + below] = t * 64u + lane;
+        }
+    }
+}
+
+template <int FL, int REC, bool F>
+void launch_t(const MainArgs& a, const DevProgram& prog, int grid, hipStream_t st) {
+    hipLaunchKernelGGL((bt_parse_filter_main<FL, REC, F>), dim3(grid), dim3(kBlock), 0, st, a, prog);
+}
+
+template <int FL>
+void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, hipStream_t st) {
+    if (rec == kRecPlanes) {
+        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, st); else launch_t<FL, kRecPlanes, false>(a, prog, grid, st);
+    } else if (rec == kRecAoS) {
+        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, st); else launch_t<FL, kRecAoS, false>(a, prog, grid, st);
+    } else {
+        launch_t<FL, kRecNone, true>(a, prog, grid, st);
+    }
+}
+
+}  // namespace
+
+int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter, int grid_blocks,
+                void* stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    int grid = grid_blocks > 0 ? grid_blocks : 1;
+    if ((uint32_t)grid > needed) grid = (int)(needed ? needed : 1);
+    int fl = -1;   // fixed-stride fast path when the stride is 16/32/64/128 B
+    if (!a.desc) {
+        if (a.stride == 16) fl = 0;
+        else if (a.stride == 32) fl = 1;
+        else if (a.stride == 64) fl = 2;
+        else if (a.stride == 128) fl = 3;
+    }
+    switch (fl) {
+    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, st); break;
+    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, st); break;
+    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, st); break;
+    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, st); break;
+    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, st); break;
+    }
+    return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
+}
+
+int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
+                   uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream) {
+    (void)n;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    if (nchunks == 0) return BT_OK;
+    hipLaunchKernelGGL(bt_chunk_sums, dim3(nchunks), dim3(256), 0, st, tile_pass, ntiles, chunk_sums);
+    hipLaunchKernelGGL(bt_compact, dim3(nchunks), dim3(256), 0, st, verdict, tile_pass, chunk_sums, nchunks,
+                       ntiles, pass_idx, n_pass);
+    return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
+}
+
+int device_grid_blocks(int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 1024;
+    // 33 KiB of LDS per block -> 4 blocks per CU; 2 rounds of residency for slack.
+    return prop.multiProcessorCount * 4 * 2;
+}
+
+}  // namespace bt

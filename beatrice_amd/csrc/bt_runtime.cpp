@@ -1,0 +1,448 @@
+// bt_runtime.cpp — the C-ABI (include/beatrice_gpu.h) over the gfx950 kernels.
+//
+// Owns per-context HIP resources: a stream for device-resident calls, two streams +
+// pinned staging for the host-batch pipeline, the compiled filter program and the
+// device workspace for the ordered compaction. Nothing here throws across the ABI:
+// failures return a beatrice::ErrorCode value and set a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bt_device.h"
+
+using namespace bt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(x)                                                                       \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) return fail(BT_E_INTERNAL, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr uint32_t kHostSlot = 112;   // bytes of each frame staged for the device (>= kNeedParse + pad)
+
+struct HostSlot {                      // one half of the double-buffered host pipeline
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* h_in = nullptr;           // pinned: prefixes then descriptors
+    uint8_t* d_in = nullptr;
+    uint8_t* h_out = nullptr;          // pinned: records (AoS) | decide | verdict
+    uint8_t* d_out = nullptr;
+    uint32_t* d_tile = nullptr;
+    bool busy = false;
+    uint32_t lo = 0, cnt = 0;          // packet range of the chunk in flight
+};
+
+}  // namespace
+
+struct bt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bt_opts opts{};
+    int grid = 0;
+    std::mutex mu;
+
+    std::vector<bt_filter_slot> slots;
+    DevProgram prog{};
+
+    // device workspace for bt_parse_filter_device
+    uint32_t ws_cap = 0;
+    uint32_t* tile_pass = nullptr;
+    uint32_t* chunk_sums = nullptr;
+    uint64_t* verdict = nullptr;
+
+    // host pipeline
+    uint32_t chunk = 0;
+    HostSlot hs[2];
+    bool host_ready = false;
+
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> tev;
+};
+
+namespace {
+
+int ensure_ws(bt_ctx* c, uint32_t n) {
+    if (n <= c->ws_cap) return BT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
+    c->tile_pass = nullptr; c->chunk_sums = nullptr; c->verdict = nullptr; c->ws_cap = 0;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    HIP_TRY(hipMalloc(&c->tile_pass, (size_t)ntiles * 4));
+    HIP_TRY(hipMalloc(&c->chunk_sums, (size_t)std::max<uint32_t>(nchunks, 1) * 4));
+    HIP_TRY(hipMalloc(&c->verdict, (size_t)ntiles * 8));
+    c->ws_cap = ntiles * 64 < n ? n : ntiles * 64;
+    return BT_OK;
+}
+
+int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st, bool aos,
+               hipEvent_t e0, hipEvent_t e1) {
+    if (!b || !o) return fail(BT_E_INVALID_ARGUMENT, "null batch/outputs");
+    if (b->n && !b->base) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer");
+    if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
+    if (o->records && o->n_cap < b->n) return fail(BT_E_INVALID_ARGUMENT, "records n_cap %u < n %u", o->n_cap, b->n);
+    const bool filter = o->verdict || o->decide || o->pass_idx || o->n_pass;
+    const bool compact = o->pass_idx || o->n_pass;
+    if (!filter && !o->records) return BT_OK;
+    if (b->n == 0) {
+        if (o->n_pass) HIP_TRY(hipMemsetAsync(o->n_pass, 0, 4, st));
+        return BT_OK;
+    }
+    if (compact) {
+        int rc = ensure_ws(c, b->n);
+        if (rc) return rc;
+    }
+    MainArgs a{};
+    a.base = b->base;
+    a.desc = b->desc;
+    a.stride = b->stride;
+    a.n = b->n;
+    a.ntiles = (b->n + 63) / 64;
+    uint64_t bytes = b->bytes;
+    if (!bytes) bytes = b->desc ? ~0ull : (uint64_t)b->n * b->stride;
+    a.bytes = bytes == ~0ull ? bytes : (bytes + 15) & ~15ull;
+    a.n_cap = o->records ? o->n_cap : 0;
+    a.records = reinterpret_cast<uint8_t*>(o->records);
+    a.decide = o->decide;
+    a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
+    a.tile_pass = compact ? c->tile_pass : nullptr;
+    const int rec = o->records ? (aos ? kRecAoS : kRecPlanes) : kRecNone;
+    if (e0) HIP_TRY(hipEventRecord(e0, st));
+    int rc = launch_main(a, c->prog, rec, filter, c->grid, st);
+    if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (e1) HIP_TRY(hipEventRecord(e1, st));
+    if (compact) {
+        rc = launch_compact(a.verdict, c->tile_pass, a.ntiles, b->n, c->chunk_sums, o->pass_idx, o->n_pass, st);
+        if (rc) return fail(rc, "compaction launch failed");
+    }
+    return BT_OK;
+}
+
+void free_host(bt_ctx* c) {
+    for (auto& s : c->hs) {
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_in) (void)hipFree(s.d_in);
+        if (s.d_out) (void)hipFree(s.d_out);
+        if (s.d_tile) (void)hipFree(s.d_tile);
+        s = HostSlot{};
+    }
+    c->host_ready = false;
+}
+
+size_t in_bytes(uint32_t chunk) { return (size_t)chunk * kHostSlot + (size_t)chunk * 8; }
+size_t out_bytes(uint32_t chunk) { return (size_t)chunk * BT_REC_BYTES + chunk + ((size_t)chunk + 63) / 64 * 8; }
+
+int ensure_host(bt_ctx* c) {
+    if (c->host_ready) return BT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    uint32_t chunk = c->opts.host_chunk_packets ? c->opts.host_chunk_packets : (1u << 20);
+    chunk = (chunk + 63) / 64 * 64;
+    c->chunk = chunk;
+    for (auto& s : c->hs) {
+        HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc(&s.h_in, in_bytes(chunk), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&s.h_out, out_bytes(chunk), hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_in, in_bytes(chunk)));
+        HIP_TRY(hipMalloc(&s.d_out, out_bytes(chunk)));
+    }
+    c->host_ready = true;
+    return BT_OK;
+}
+
+// Copies one finished chunk from pinned staging into the caller's buffers.
+void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint8_t* decide) {
+    const uint32_t chunk = c->chunk;
+    const uint8_t* rec = s.h_out;
+    const uint8_t* dec = s.h_out + (size_t)chunk * BT_REC_BYTES;
+    const uint64_t* ver = reinterpret_cast<const uint64_t*>(dec + chunk);
+    if (records) std::memcpy(records + s.lo, rec, (size_t)s.cnt * BT_REC_BYTES);
+    if (decide) std::memcpy(decide + s.lo, dec, s.cnt);
+    if (verdict) {   // chunks are 64-aligned, so whole words line up
+        std::memcpy(verdict + s.lo / 64, ver, ((size_t)s.cnt + 63) / 64 * 8);
+    }
+    s.busy = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bt_abi_version(void) { return BT_ABI_VERSION; }
+
+const char* bt_last_error(void) { return g_err.c_str(); }
+
+int bt_device_count(int* out) {
+    if (!out) return fail(BT_E_INVALID_ARGUMENT, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return BT_OK;
+}
+
+int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
+    if (!out) return fail(BT_E_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(BT_E_INIT_FAILED, "no HIP device visible (the MI355X path needs a GPU)");
+    if (device < 0 || device >= n) return fail(BT_E_INVALID_ARGUMENT, "device %d out of range [0,%d)", device, n);
+    auto* c = new bt_ctx();
+    c->device = device;
+    if (opts) c->opts = *opts;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(BT_E_INIT_FAILED, "hipSetDevice/hipStreamCreate failed on device %d", device);
+    }
+    (void)hipEventCreate(&c->ev0);
+    (void)hipEventCreate(&c->ev1);
+    c->grid = c->opts.grid_waves ? (int)((c->opts.grid_waves + kWavesPerBlock - 1) / kWavesPerBlock)
+                                 : device_grid_blocks(device);
+    to_device_program(nullptr, 0, &c->prog);
+    *out = c;
+    return BT_OK;
+}
+
+void bt_destroy(bt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    free_host(c);
+    if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
+    for (auto e : c->tev) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int bt_filter_compile_host(const bt_filter_desc* f, uint32_t n, bt_filter_slot* out, uint32_t cap,
+                           uint32_t* n_slots) {
+    if ((!f && n) || !out || !n_slots) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    char err[256] = {0};
+    int rc = compile_filters(f, n, out, cap, n_slots, err, sizeof(err));
+    if (rc) return fail(rc, "%s", err);
+    return BT_OK;
+}
+
+int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    std::vector<bt_filter_slot> slots(BT_MAX_FILTERS);
+    uint32_t m = 0;
+    int rc = bt_filter_compile_host(f, n, slots.data(), BT_MAX_FILTERS, &m);
+    if (rc) return rc;
+    slots.resize(m);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->slots = slots;
+    to_device_program(c->slots.data(), m, &c->prog);
+    return BT_OK;
+}
+
+int bt_filter_program(const bt_ctx* c, bt_filter_slot* out, uint32_t cap, uint32_t* n_slots) {
+    if (!c || !n_slots) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    *n_slots = (uint32_t)c->slots.size();
+    for (uint32_t i = 0; i < c->slots.size() && i < cap && out; ++i) out[i] = c->slots[i];
+    return BT_OK;
+}
+
+int bt_reserve(bt_ctx* c, uint32_t n) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return ensure_ws(c, n);
+}
+
+int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, void* stream) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    return run_device(c, b, o, st, false, nullptr, nullptr);
+}
+
+int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
+                   float* main_ms) {
+    if (!c || !iters) return fail(BT_E_INVALID_ARGUMENT, "null context / zero iterations");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    while (c->tev.size() < 2 * (size_t)iters) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->tev.push_back(e);
+    }
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    for (uint32_t i = 0; i < iters; ++i) {
+        int rc = run_device(c, b, o, c->stream, false, c->tev[2 * i], c->tev[2 * i + 1]);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float tot = 0, k = 0;
+    HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
+    for (uint32_t i = 0; i < iters; ++i) {
+        float x = 0;
+        HIP_TRY(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
+        k += x;
+    }
+    if (ms_per_iter) *ms_per_iter = tot / iters;
+    if (main_ms) *main_ms = k / iters;
+    return BT_OK;
+}
+
+int bt_parse_filter(bt_ctx* c, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n, bt_rec* records,
+                    uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (n && (!base || !desc)) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc = ensure_host(c);
+    if (rc) return rc;
+    const bool want_filter = verdict || decide || pass_idx || n_pass;
+    // pass indices come from the verdict words; keep a private copy when the caller
+    // did not ask for them
+    std::vector<uint64_t> vtmp;
+    uint64_t* ver = verdict;
+    if (!ver && (pass_idx || n_pass)) { vtmp.resize(((size_t)n + 63) / 64); ver = vtmp.data(); }
+
+    const uint32_t chunk = c->chunk;
+    uint32_t next = 0, k = 0;
+    while (next < n || c->hs[0].busy || c->hs[1].busy) {
+        HostSlot& s = c->hs[k & 1];
+        if (s.busy) {   // retire the chunk that used this half
+            HIP_TRY(hipEventSynchronize(s.done));
+            drain_slot(c, s, records, ver, decide);
+        }
+        if (next < n) {
+            const uint32_t cnt = std::min(chunk, n - next);
+            // gather the header prefixes (<= kHostSlot bytes) into pinned staging
+            uint8_t* pre = s.h_in;
+            uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlot);
+            uint64_t pos = 0;
+            for (uint32_t i = 0; i < cnt; ++i) {
+                const uint64_t dd = desc[next + i];
+                const uint32_t len = BT_DESC_LEN(dd);
+                const uint32_t m = std::min(len, kHostSlot);
+                std::memcpy(pre + pos, base + BT_DESC_OFF(dd), m);
+                d[i] = BT_DESC(pos, len);
+                pos += (m + 15) & ~15u;
+            }
+            const size_t pre_bytes = (pos + 15) & ~15ull;
+            HIP_TRY(hipMemcpyAsync(s.d_in, pre, pre_bytes, hipMemcpyHostToDevice, s.stream));
+            HIP_TRY(hipMemcpyAsync(s.d_in + (size_t)chunk * kHostSlot, d, (size_t)cnt * 8, hipMemcpyHostToDevice,
+                                   s.stream));
+            bt_batch b{};
+            b.base = s.d_in;
+            b.desc = reinterpret_cast<const uint64_t*>(s.d_in + (size_t)chunk * kHostSlot);
+            b.n = cnt;
+            b.bytes = (uint64_t)chunk * kHostSlot;
+            bt_outputs o{};
+            uint8_t* drec = s.d_out;
+            uint8_t* ddec = s.d_out + (size_t)chunk * BT_REC_BYTES;
+            uint64_t* dver = reinterpret_cast<uint64_t*>(ddec + chunk);
+            o.records = records ? drec : nullptr;
+            o.n_cap = chunk;
+            o.decide = want_filter ? ddec : nullptr;
+            o.verdict = want_filter ? dver : nullptr;
+            rc = run_device(c, &b, &o, s.stream, true, nullptr, nullptr);
+            if (rc) return rc;
+            if (records) HIP_TRY(hipMemcpyAsync(s.h_out, drec, (size_t)cnt * BT_REC_BYTES, hipMemcpyDeviceToHost, s.stream));
+            if (want_filter) {
+                HIP_TRY(hipMemcpyAsync(s.h_out + (size_t)chunk * BT_REC_BYTES, ddec, cnt, hipMemcpyDeviceToHost, s.stream));
+                HIP_TRY(hipMemcpyAsync(s.h_out + (size_t)chunk * BT_REC_BYTES + chunk, dver,
+                                       ((size_t)cnt + 63) / 64 * 8, hipMemcpyDeviceToHost, s.stream));
+            }
+            HIP_TRY(hipEventRecord(s.done, s.stream));
+            s.busy = true;
+            s.lo = next;
+            s.cnt = cnt;
+            next += cnt;
+        }
+        ++k;
+    }
+    if (ver && (pass_idx || n_pass)) {
+        uint32_t np = 0;
+        for (uint32_t w = 0; w < (n + 63) / 64; ++w) {
+            uint64_t x = ver[w];
+            if (w == (n - 1) / 64 && (n & 63)) x &= (1ull << (n & 63)) - 1ull;
+            while (x) {
+                const uint32_t bit = (uint32_t)__builtin_ctzll(x);
+                if (pass_idx) pass_idx[np] = w * 64 + bit;
+                ++np;
+                x &= x - 1;
+            }
+        }
+        if (n_pass) *n_pass = np;
+    }
+    return BT_OK;
+}
+
+int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {
+    if (!c || !out) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(out, bytes ? bytes : 16));
+    return BT_OK;
+}
+
+int bt_dev_free(bt_ctx* c, void* p) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (p) HIP_TRY(hipFree(p));
+    return BT_OK;
+}
+
+int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return BT_OK;
+}
+
+int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return BT_OK;
+}
+
+int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipMemsetAsync(dst, value, bytes, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BT_OK;
+}
+
+int bt_synchronize(bt_ctx* c) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BT_OK;
+}
+
+void bt_record_gather(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out) {
+    const uint8_t* p = static_cast<const uint8_t*>(planes);
+    uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    for (int k = 0; k < BT_REC_SLABS; ++k) std::memcpy(o + 16 * k, p + ((size_t)k * n_cap + i) * 16, 16);
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+"""Deterministic synthetic captures (ctypes over libbt_synth.so, csrc/bt_synth.cpp).
+
+A capture is (data: uint8 ndarray, desc: uint64 ndarray of bt_pkt_desc). The configs
+are the BASELINE.json ones: 2 = C1/C2 fixed 64 B Eth/IPv4/UDP,
+3 = C3 IMIX, 4 = C4 QinQ/IPv6/options, 9 = fuzz.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+C2, C3, C4, FUZZ = 2, 3, 4, 9
+SEEDS = {C2: 0x5EED0002, C3: 0x5EED0003, C4: 0x5EED0004, FUZZ: 0x5EED0009}
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "libbt_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() (make -C beatrice_amd/csrc)")
+        L = ctypes.CDLL(path)
+        L.bt_synth_layout.restype = ctypes.c_uint64
+        L.bt_synth_layout.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        L.bt_synth_fill.restype = ctypes.c_int
+        L.bt_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def capture(cfg: int, n: int, seed: int | None = None, threads: int | None = None):
+    """Returns (data, desc) for n frames of config cfg."""
+    if seed is None:
+        seed = SEEDS[cfg]
+    L = lib()
+    desc = np.empty(n, dtype=np.uint64)
+    nbytes = L.bt_synth_layout(cfg, n, seed, desc.ctypes.data)
+    data = np.zeros(int(nbytes), dtype=np.uint8)
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    L.bt_synth_fill(cfg, n, seed, desc.ctypes.data, data.ctypes.data, threads)
+    return data, desc
+
+
+def desc_off(desc: np.ndarray) -> np.ndarray:
+    return (desc & np.uint64(0xFFFFFFFFFFFF)).astype(np.int64)
+
+
+def desc_len(desc: np.ndarray) -> np.ndarray:
+    return (desc >> np.uint64(48)).astype(np.int64)
+
+
+def make_desc(off, length) -> np.ndarray:
+    off = np.asarray(off, dtype=np.uint64)
+    length = np.asarray(length, dtype=np.uint64)
+    return off | (length << np.uint64(48))
+
+
+def pack_frames(frames, align: int = 1, shift: int = 0):
+    """Packs a list of bytes objects into (data, desc); frame i starts at an offset
+    that is `shift` past a multiple of `align`."""
+    offs, lens, pos = [], [], 0
+    for f in frames:
+        pos = (pos + align - 1) // align * align + shift
+        offs.append(pos)
+        lens.append(len(f))
+        pos += len(f)
+    data = np.zeros((pos + 255) // 256 * 256 + 256, dtype=np.uint8)
+    for o, f in zip(offs, frames):
+        data[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+    return data, make_desc(offs, lens)

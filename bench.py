@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Benchmark of the device-resident parse+filter hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4] [--packets P]
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A step = one bt_parse_filter_device() pass over one synthetic 16M-packet batch that
+is already resident in HBM. Default workload (N=1): BASELINE.json configs[1] — C2,
+16,777,216 fixed 64 B Eth/IPv4/UDP frames, parse-only (96-B bt_rec per packet).
+`--config c3` runs configs[2] (IMIX parse + 5-tuple PacketFilter + ordered
+compaction). Multi-GPU is weak scaling: every rank owns its own 16M-packet batch on
+its own device (packet batches shard with no collective; the only cross-rank traffic
+is the timing barrier and the max-reduction of the step time, over gloo).
+
+Prints ONE JSON line on rank 0 with value = packets of all ranks / max step time,
+the roofline of the main kernel (HIP events around every main-kernel launch inside the
+timed region) and, at N=1, the same run's CPU baseline: the reference's own parser +
+PacketFilter (oracle/_ref, compiled from the reference sources) on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from beatrice_amd import abi, synth  # noqa: E402
+
+METRIC = "Mpps + achieved HBM GB/s, device-resident parse+filter, 64B and IMIX"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+C3_FILTERS = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+              {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+              {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+
+WORKLOADS = {
+    "c2": dict(cfg=synth.C2, fixed=True, parse=True, filters=None,
+               name="C2: 16M x 64B Eth/IPv4/UDP, fixed stride, parse-only (BASELINE configs[1])"),
+    "c3": dict(cfg=synth.C3, fixed=False, parse=True, filters=C3_FILTERS,
+               name="C3: 16M IMIX 64/512/1500 Eth/VLAN/IPv4/{TCP,UDP}, parse + PacketFilter "
+                    "(udp, 10.0.0.0/8, 1000-2000) + ordered compaction (BASELINE configs[2])"),
+    "c4": dict(cfg=synth.C4, fixed=False, parse=True, filters=C3_FILTERS,
+               name="C4: 16M QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets, parse + PacketFilter "
+                    "(BASELINE configs[3])"),
+}
+
+
+def algorithmic_bytes(desc: np.ndarray, fixed: bool, parse: bool, filt: bool, n_pass: int) -> float:
+    """Bytes the main kernel must move per launch (SURVEY.md §8(d) formula):
+    min(len,128) header read + 8 B descriptor (0 for fixed stride) + 96 B record
+    + 1 B decision + 1/8 B verdict bit (the ordered pass-index list is written by the
+    compaction kernels and is not counted here)."""
+    n = len(desc)
+    lens = synth.desc_len(desc)
+    b = float(np.minimum(lens, 128).sum())
+    if not fixed:
+        b += 8.0 * n
+    if parse:
+        b += 96.0 * n
+    if filt:
+        b += n * (1.0 + 1.0 / 8.0)
+    return b
+
+
+def cpu_baseline(data, desc, wl, n_sample, seconds):
+    """The reference's own parser + PacketFilter (oracle/_ref) on the host cores, on a
+    bounded sample of the same capture; falls back to the C oracle port."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol  # checker/baseline only
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    sub = desc[:n_sample]
+    filters = wl["filters"] or []
+    if ol.ref_available():
+        done, el = ol.ref_bench(data, sub, len(sub), filters, parse=wl["parse"], threads=threads,
+                                seconds=seconds)
+        kind = "reference"
+    else:
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < seconds:
+            ol.oracle_run(data, sub, len(sub), filters if filters else None, parse=wl["parse"],
+                          threads=threads)
+            done += len(sub)
+        el = time.perf_counter() - t0
+        kind = "port"
+    what = ("ProtocolParser::parsePacket per walked layer" if wl["parse"] else "") + \
+           (" + PacketFilter::applyFilters" if filters else "")
+    return {"value": round(done / el / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": kind,
+            "sample": f"first {len(sub)} packets of the same capture, repeated for {el:.1f}s; "
+                      f"{what.strip()}; {threads} std::threads, per-thread instances, disjoint shards"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=1 << 24)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 18)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("gloo")
+    wl = WORKLOADS[args.config]
+    n = args.packets
+
+    data, desc = synth.capture(wl["cfg"], n, seed=synth.SEEDS[wl["cfg"]] + rank)
+    ctx = abi.Context(local)
+    if wl["filters"]:
+        ctx.compile(wl["filters"])
+    filt = wl["filters"] is not None
+    run = abi.DeviceRun(ctx, data, None if wl["fixed"] else desc, n, stride=64 if wl["fixed"] else 0,
+                        records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt)
+    for _ in range(args.warmup):
+        run.run()
+    ctx.synchronize()
+    n_pass = run.fetch().get("n_pass", 0) if filt else 0
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ms_iter, main_ms = ctx.time_device(run.batch, run.outs, args.steps)
+    ctx.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    step_s = (t1 - t0) / args.steps
+    if dist is not None:
+        import torch
+        t = torch.tensor([step_s, main_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_s, main_ms = float(t[0]), float(t[1])
+    total_pkts = n * world
+    value = total_pkts / step_s / 1e6
+
+    algo = algorithmic_bytes(desc, wl["fixed"], wl["parse"], filt, n_pass)
+    achieved = algo / (main_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as fh:
+                traffic = json.load(fh).get(args.config)
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(data, desc, wl, args.cpu_sample, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64)",
+            "config": {"workload": wl["name"], "packets_per_gpu": n, "parallelism": f"batch split x{world}",
+                       "pass_fraction": round(n_pass / n, 4) if filt else None},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "bt_parse_filter_main", "kernel_ms": round(main_ms, 4),
+                         "algorithmic_bytes_per_packet": round(algo / n, 2),
+                         "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    run.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

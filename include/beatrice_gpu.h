@@ -1,0 +1,293 @@
+/*
+ * beatrice_gpu.h — C-ABI of the MI355X parse+filter stage.
+ *
+ * This is the drop-in boundary between Beatrice's C++ host (capture backends,
+ * PluginManager, PacketFilter callers) and the hand-written gfx950 kernels in
+ * beatrice_amd/csrc/. Plain C types only: pointers, sizes, POD structs. No
+ * exception crosses it; every entry point returns an int status
+ * (0 = OK, otherwise a beatrice::ErrorCode value, include/beatrice/Error.hpp:11-26
+ * of the reference) and bt_last_error() gives the message.
+ *
+ * What each entry point replaces in the reference (/root/reference, read-only):
+ *
+ *   bt_filter_compile   PacketFilter::addFilter + the per-packet priority sort and
+ *                       per-packet expression re-parsing of applyFilters
+ *                       (src/PacketFilter.cpp:19-31, :57-73, :330-372). Expressions
+ *                       are parsed ONCE here with the reference's own stoi/getline
+ *                       semantics; the device gets a POD program.
+ *   bt_parse_filter     PacketFilter::applyFilters(const std::vector<Packet>&)
+ *                       (src/PacketFilter.cpp:121-130) fused with the per-layer
+ *                       ProtocolParser::parsePacket(slice, name) calls
+ *                       (src/parser/ProtocolParser.cpp:69-95, :238-284) over a
+ *                       host batch (pinned staging, H2D -> kernels -> D2H).
+ *   bt_parse_filter_device  the same over device-resident buffers, async on a
+ *                       caller stream (the hot path that bench.py measures).
+ *
+ * Record layout (bt_rec, 96 B per packet). Each layer L found by the layer walk
+ * (DESIGN.md "R-WALK") has the field values that
+ *   ProtocolParser(enablePerformanceMetrics=false).parsePacket(
+ *       std::vector<uint8_t>(frame + off_L, frame + len), L)
+ * returns, bit for bit: integers are the reference's extractValue<T> results
+ * (big-endian wire order decoded, src/parser/ProtocolParser.cpp:418-431) stored
+ * little-endian; BYTES / IPV4_ADDRESS / IPV6_ADDRESS fields are the raw bytes.
+ * A layer whose slice is shorter than its table's getTotalLength() has status
+ * PACKET_TOO_SHORT and no fields (:244-247): its field bytes are zero here.
+ * Bytes of absent layers and reserved bytes are zero.
+ *
+ * On the device the records are stored SoA by 16-byte slab: slab k (k = 0..5)
+ * of packet i lives at  records + (k * n_cap + i) * 16  ("plane-major"), so each
+ * wavefront store instruction writes 1 KiB contiguously. bt_record_gather()
+ * assembles one bt_rec from that layout.
+ */
+#ifndef BEATRICE_GPU_H
+#define BEATRICE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BT_ABI_VERSION 1
+
+/* ---- status codes (values of beatrice::ErrorCode, reference include/beatrice/Error.hpp:11-26) */
+#define BT_OK                    0
+#define BT_E_INVALID_ARGUMENT    1
+#define BT_E_INIT_FAILED         2
+#define BT_E_RESOURCE            3
+#define BT_E_INTERNAL           10
+#define BT_E_NOT_IMPLEMENTED    11
+
+/* ---- packet descriptor: byte offset (48 bits) | length (16 bits) << 48 -------- */
+typedef uint64_t bt_pkt_desc;
+#define BT_DESC(off, len) ((uint64_t)(off) | ((uint64_t)(len) << 48))
+#define BT_DESC_OFF(d)    ((uint64_t)(d) & 0xFFFFFFFFFFFFull)
+#define BT_DESC_LEN(d)    ((uint32_t)((uint64_t)(d) >> 48))
+
+/* ---- parsed record --------------------------------------------------------- */
+#define BT_REC_BYTES  96
+#define BT_REC_SLABS  6
+
+/* bt_rec.present / bt_rec.ok bits: layer attempted by the walk / status SUCCESS */
+#define BT_L_ETH   0x01u
+#define BT_L_VLAN0 0x02u
+#define BT_L_VLAN1 0x04u
+#define BT_L_IPV4  0x08u
+#define BT_L_IPV6  0x10u
+#define BT_L_TCP   0x20u
+#define BT_L_UDP   0x40u
+#define BT_L_ICMP  0x80u
+
+#pragma pack(push, 1)
+typedef struct bt_ipv4_fields {   /* reference src/parser/ProtocolRegistry.cpp:161-178 */
+    uint8_t  version;             /* raw byte 0 (quirk: same byte as ihl)              */
+    uint8_t  ihl;                 /* raw byte 0                                         */
+    uint8_t  tos;
+    uint8_t  ttl;
+    uint8_t  protocol;
+    uint8_t  _pad0;
+    uint16_t total_length;
+    uint16_t identification;
+    uint16_t flags;               /* raw 16-bit flags + fragment offset                 */
+    uint16_t checksum;
+    uint16_t _pad1;
+    uint8_t  source_ip[4];
+    uint8_t  destination_ip[4];
+    uint8_t  _pad2[16];
+} bt_ipv4_fields;                 /* 40 B */
+
+typedef struct bt_ipv6_fields {   /* reference src/parser/ProtocolRegistry.cpp:180-192 */
+    uint32_t version_traffic_class_flow_label;
+    uint16_t payload_length;
+    uint8_t  next_header;
+    uint8_t  hop_limit;
+    uint8_t  source_ip[16];
+    uint8_t  destination_ip[16];
+} bt_ipv6_fields;                 /* 40 B */
+
+typedef struct bt_tcp_fields {    /* reference src/parser/ProtocolRegistry.cpp:194-209 */
+    uint16_t source_port;
+    uint16_t destination_port;
+    uint32_t sequence_number;
+    uint32_t acknowledgment_number;
+    uint8_t  data_offset;         /* raw byte 12 */
+    uint8_t  flags;               /* raw byte 13 */
+    uint16_t window_size;
+    uint16_t checksum;
+    uint16_t urgent_pointer;
+} bt_tcp_fields;                  /* 20 B */
+
+typedef struct bt_udp_fields {    /* reference src/parser/ProtocolRegistry.cpp:211-221 */
+    uint16_t source_port;
+    uint16_t destination_port;
+    uint16_t length;
+    uint16_t checksum;
+    uint8_t  _pad[12];
+} bt_udp_fields;                  /* 20 B */
+
+typedef struct bt_icmp_fields {   /* reference src/parser/ProtocolRegistry.cpp:223-234 */
+    uint8_t  type;
+    uint8_t  code;
+    uint16_t checksum;
+    uint16_t identifier;
+    uint16_t sequence_number;
+    uint8_t  _pad[12];
+} bt_icmp_fields;                 /* 20 B */
+
+typedef struct bt_rec {
+    /* slab 0 */
+    uint8_t  eth_destination_mac[6];   /* reference ProtocolRegistry.cpp:154 (BYTES) */
+    uint8_t  eth_source_mac[6];        /* :155 (BYTES)                               */
+    uint16_t eth_ethertype;            /* :156                                       */
+    uint16_t pkt_len;                  /* min(frame length, 65535)                   */
+    /* slab 1 */
+    uint16_t vlan_tpid[2];             /* ProtocolRegistry.cpp:293 per tag           */
+    uint16_t vlan_tci[2];              /* :294                                       */
+    uint8_t  present;                  /* BT_L_* layers the walk attempted           */
+    uint8_t  ok;                       /* BT_L_* layers with ParseStatus::SUCCESS    */
+    uint8_t  l3_off;                   /* frame offset of the L3 slice (0 if none)   */
+    uint8_t  l4_off;                   /* frame offset of the L4 slice (0 if none)   */
+    /* slabs 1..4: L3 union at 28, L4 union at 68 */
+    union { bt_ipv4_fields ipv4; bt_ipv6_fields ipv6; } l3;
+    union { bt_tcp_fields tcp; bt_udp_fields udp; bt_icmp_fields icmp; } l4;
+    /* slab 5 tail */
+    uint8_t  _reserved[8];
+} bt_rec;
+#pragma pack(pop)
+
+/* ---- filters --------------------------------------------------------------- */
+/* Same enumerator order as beatrice::PacketFilter::FilterType
+ * (reference include/beatrice/PacketFilter.hpp:17-24). */
+enum bt_filter_type {
+    BT_FILTER_BPF = 0,
+    BT_FILTER_PROTOCOL = 1,
+    BT_FILTER_IP_RANGE = 2,
+    BT_FILTER_PORT_RANGE = 3,
+    BT_FILTER_PAYLOAD = 4,
+    BT_FILTER_CUSTOM = 5
+};
+
+typedef struct bt_filter_desc {       /* mirrors PacketFilter::FilterConfig hpp:26-33 */
+    int32_t     type;                  /* enum bt_filter_type                          */
+    const char* expression;            /* NUL-terminated; NULL == ""                   */
+    int32_t     enabled;
+    int32_t     priority;              /* higher = evaluated first                      */
+    int32_t     has_custom_func;       /* CUSTOM only: a std::function is installed     */
+} bt_filter_desc;
+
+/* compiled filter kinds (device program) */
+enum bt_filter_kind {
+    BT_K_TRUE = 0,        /* empty expression (every apply*Filter :169,194,220,250,289) or unset CUSTOM */
+    BT_K_FALSE = 1,       /* can only ever return false                                           */
+    BT_K_BPF = 2,         /* substring keywords tcp/udp/icmp (:168-191)                           */
+    BT_K_PROTO_EQ = 3,    /* "tcp"/"udp"/"icmp" (:210-212)                                        */
+    BT_K_PROTO_NZ = 4,    /* "ip" (:213)                                                          */
+    BT_K_IP_MASK = 5,     /* CIDR or exact dotted quad (:219-247, :342-360)                       */
+    BT_K_PORT = 6,        /* inclusive range or exact port (:249-286, :362-372)                   */
+    BT_K_IP_THROW = 7,    /* expression makes std::stoi throw once the IPv4 gates pass            */
+    BT_K_PORT_THROW = 8,  /* same for the port filter once the TCP/UDP length gates pass          */
+    BT_K_HOST = 9         /* PAYLOAD regex / installed CUSTOM callback: evaluated on the host     */
+};
+
+typedef struct bt_filter_slot {       /* one compiled program slot, in evaluation order */
+    uint32_t source_index;            /* index into the bt_filter_desc array            */
+    uint32_t kind;                    /* enum bt_filter_kind                            */
+    uint32_t a, b;                    /* kind parameters                */
+    int32_t  throw_kind;              /* 0 none, 1 std::invalid_argument, 2 std::out_of_range */
+} bt_filter_slot;
+
+#define BT_MAX_FILTERS 64
+
+/* Per-packet decision byte: (code << 6) | slot. */
+#define BT_DECIDE_PASS   0u   /* every enabled filter returned true (slot = last slot, 0 if none) */
+#define BT_DECIDE_REJECT 1u   /* slot = first filter that returned false                           */
+#define BT_DECIDE_THROW  2u   /* slot = filter whose expression throws (reference rethrows)        */
+#define BT_DECIDE_HOST   3u   /* slot = first host-only filter reached; host continues from there  */
+#define BT_DECIDE_CODE(x) ((uint32_t)(x) >> 6)
+#define BT_DECIDE_SLOT(x) ((uint32_t)(x) & 63u)
+
+/* ---- context --------------------------------------------------------------- */
+typedef struct bt_ctx bt_ctx;
+
+typedef struct bt_opts {
+    uint32_t host_chunk_packets;   /* bt_parse_filter pipeline chunk (0 = default 1M)  */
+    uint32_t host_chunk_bytes;     /* pinned staging bytes per chunk (0 = default 256 MiB) */
+    uint32_t grid_waves;           /* 0 = auto (persistent grid sized to the device)    */
+    uint32_t reserved[5];
+} bt_opts;
+
+typedef struct bt_batch {          /* device-resident input */
+    const uint8_t* base;           /* packet bytes                                      */
+    const bt_pkt_desc* desc;       /* one per packet; NULL selects fixed-stride mode    */
+    uint32_t stride;               /* fixed-stride mode: packet i = base[i*stride .. +stride) */
+    uint32_t n;                    /* packets                                           */
+    uint64_t bytes;                /* size of the base buffer (bounds check)            */
+} bt_batch;
+
+typedef struct bt_outputs {        /* any pointer may be NULL = not produced            */
+    void*     records;             /* 96 * n_cap bytes, plane-major slabs               */
+    uint32_t  n_cap;               /* plane stride in records (>= n)                    */
+    uint64_t* verdict;             /* ceil(n/64) words, bit i%64 of word i/64 = passed  */
+    uint8_t*  decide;              /* n bytes, BT_DECIDE_*                              */
+    uint32_t* pass_idx;            /* n entries: indices of passing packets, ascending  */
+    uint32_t* n_pass;              /* 1 word                                            */
+} bt_outputs;
+
+int  bt_abi_version(void);
+const char* bt_last_error(void);              /* thread-local message of the last failure */
+
+int  bt_create(int device, const bt_opts* opts, bt_ctx** out);
+void bt_destroy(bt_ctx* ctx);
+int  bt_device_count(int* out);
+
+/* Compile the enabled filters: stable sort by priority (descending), parse each
+ * expression once. The C++ adapter (beatrice_amd/host) passes filters already in
+ * the reference's own evaluation order so ties match libstdc++ exactly. */
+int  bt_filter_compile(bt_ctx* ctx, const bt_filter_desc* filters, uint32_t n);
+int  bt_filter_program(const bt_ctx* ctx, bt_filter_slot* out, uint32_t cap, uint32_t* n_slots);
+/* host-only helper: compile without a context (no device needed) */
+int  bt_filter_compile_host(const bt_filter_desc* filters, uint32_t n,
+                            bt_filter_slot* out, uint32_t cap, uint32_t* n_slots);
+
+/* Pre-size the device workspace for batches of up to n packets (so later launches
+ * never allocate, e.g. under hipGraph capture). */
+int  bt_reserve(bt_ctx* ctx, uint32_t n);
+
+/* Device-resident parse+filter, asynchronous on `stream` (a hipStream_t, NULL =
+ * the context's own stream). records != NULL selects parsing; the filter
+ * outputs are produced when any of verdict/decide/pass_idx/n_pass is set. */
+int  bt_parse_filter_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, void* stream);
+
+/* Host batch: borrows base/desc for the call, copies through pinned staging in
+ * chunks (H2D, kernels, D2H double-buffered on two streams), fills host outputs,
+ * returns when done. Output pointers are host memory (records in bt_rec AoS). */
+int  bt_parse_filter(bt_ctx* ctx, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n,
+                     bt_rec* records, uint64_t* verdict, uint8_t* decide,
+                     uint32_t* pass_idx, uint32_t* n_pass);
+
+/* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
+int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);
+int  bt_dev_free(bt_ctx* ctx, void* p);
+int  bt_memcpy_h2d(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
+int  bt_synchronize(bt_ctx* ctx);
+/* events on the context stream for timing a device-resident run */
+int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
+                    uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
+
+/* host-side record gather from the plane-major device layout (after a D2H copy) */
+void bt_record_gather(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#if defined(__cplusplus)
+static_assert(sizeof(bt_rec) == BT_REC_BYTES, "bt_rec must be 96 bytes");
+static_assert(offsetof(bt_rec, l3) == 28, "L3 union at 28");
+static_assert(offsetof(bt_rec, l4) == 68, "L4 union at 68");
+#endif
+
+#endif /* BEATRICE_GPU_H */

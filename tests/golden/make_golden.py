@@ -1,0 +1,183 @@
+"""Generates the golden fixtures in tests/golden/ from the COMPILED REFERENCE.
+
+Run in the build container (needs /root/reference and `make -C oracle ref`):
+
+    python tests/golden/make_golden.py
+
+For each capture it stores the inputs (frames + bt_pkt_desc) and the reference's
+outputs: per-packet bt_rec records from the reference ProtocolParser walked layer by
+layer (oracle/ref_harness.cpp:ref_parse) and, for every filter set in FILTER_SETS,
+the per-packet PacketFilter::applyFilters(const Packet&) outcome (code, filterName
+index). Nothing from /root/reference is copied: only data goes into the .npz files.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from beatrice_amd import synth  # noqa: E402
+import oracle_lib as ol  # noqa: E402
+
+T = {"BPF": 0, "PROTOCOL": 1, "IP_RANGE": 2, "PORT_RANGE": 3, "PAYLOAD": 4, "CUSTOM": 5}
+
+
+def single(t, exprs):
+    return {f"{t.lower()}_{i}": [{"type": T[t], "expr": e}] for i, e in enumerate(exprs)}
+
+
+QUIRK_EXPRS = {
+    "BPF": ["", "tcp", "udp", "icmp", "not udp", "UDP", "tcp or udp", "xyz", "icmp and tcp"],
+    "PROTOCOL": ["", "tcp", "udp", "icmp", "ip", "IP", "tcp ", "arp"],
+    "IP_RANGE": ["", "10.0.0.0/8", "192.168.0.0/16", "10.0.0.0/0", "10.0.0.0/33", "10.0.0.0/-1",
+                 "0.0.0.0/1", "128.0.0.0/1", "10.1.2.3", "10.1.2", "10.1.2.3.4", "266.0.0.0/8",
+                 " 10.0.0.0/8", "10.0.0.0/8junk", "a.b.c.d/8", "10.0.0.0/x", "10..0.0/8",
+                 "10.0.0.0/99999999999", "10.0.0.0/", "/8", "10.0.0.0/8/3", "10.0.0.0.", "-246.0.0.0/8",
+                 "192.168.1.1/32"],
+    "PORT_RANGE": ["", "1000-2000", "0-65535", "53", "2000-1000", "-5", "1000-", "66770", "1000-66770",
+                   " 1000 - 2000", "abc", "99999999999", "0", "1000-2000-3000", "+1000-+2000"],
+    "PAYLOAD": ["", "GET", "HTTP/1\\.1", "[", "^GET", "beatrice"],
+}
+
+FILTER_SETS = {
+    # C3/C4 headline set: priorities 3/2/1
+    "c3": [{"type": T["PROTOCOL"], "expr": "udp", "priority": 3},
+           {"type": T["IP_RANGE"], "expr": "10.0.0.0/8", "priority": 2},
+           {"type": T["PORT_RANGE"], "expr": "1000-2000", "priority": 1}],
+    # a throwing filter behind a rejecting one: only packets that pass the first throw
+    "throw_after": [{"type": T["PROTOCOL"], "expr": "tcp", "priority": 5},
+                    {"type": T["PORT_RANGE"], "expr": "1000-", "priority": 1}],
+    "throw_oor": [{"type": T["BPF"], "expr": "udp", "priority": 2},
+                  {"type": T["IP_RANGE"], "expr": "10.0.0.0/99999999999", "priority": 1}],
+    # disabled filters are skipped; order by priority, not insertion
+    "mixed": [{"type": T["PORT_RANGE"], "expr": "0-1023", "priority": -1},
+              {"type": T["BPF"], "expr": "tcp udp", "priority": 10},
+              {"type": T["IP_RANGE"], "expr": "192.168.0.0/16", "priority": 4, "enabled": 0},
+              {"type": T["IP_RANGE"], "expr": "192.168.0.0/17", "priority": 4},
+              {"type": T["PROTOCOL"], "expr": "ip", "priority": 7}],
+    # host-side filters in the chain
+    "payload_mid": [{"type": T["PROTOCOL"], "expr": "tcp", "priority": 3},
+                    {"type": T["PAYLOAD"], "expr": "GET", "priority": 2},
+                    {"type": T["PORT_RANGE"], "expr": "0-2047", "priority": 1}],
+    "custom": [{"type": T["CUSTOM"], "expr": "", "priority": 2, "custom": 1},
+               {"type": T["CUSTOM"], "expr": "ignored", "priority": 1}],
+    "unknown_type": [{"type": 9, "expr": "x", "priority": 1}],
+    "empty": [],
+}
+for t, exprs in QUIRK_EXPRS.items():
+    FILTER_SETS.update(single(t, exprs))
+
+
+def edge_frames():
+    """Hand-built frames for the walk's and the filters' boundary cases."""
+    import struct
+
+    def eth(et, body=b"", dst=b"\x01\x02\x03\x04\x05\x06", src=b"\x0a\x0b\x0c\x0d\x0e\x0f"):
+        return dst + src + struct.pack(">H", et) + body
+
+    def ipv4(proto, l4=b"", ihl=5, src=b"\x0a\x01\x02\x03", dst=b"\xc0\xa8\x01\x01", opts=None):
+        hdr = bytes([0x40 | ihl, 0x10]) + struct.pack(">HHHBBH", 20 + len(l4), 0x1234, 0x4000, 64, proto, 0xBEEF)
+        hdr += src + dst
+        if ihl > 5:
+            hdr += (opts or bytes(range(1, 1 + 4 * (ihl - 5))))[: 4 * (ihl - 5)]
+        return hdr + l4
+
+    def udp(sp, dp, payload=b""):
+        return struct.pack(">HHHH", sp, dp, 8 + len(payload), 0x55AA) + payload
+
+    def tcp(sp, dp, doff=5, payload=b""):
+        h = struct.pack(">HHIIBBHHH", sp, dp, 0x01020304, 0xA0B0C0D0, doff << 4, 0x18, 0xFFFF, 0x1111, 7)
+        return h + bytes(4 * max(doff - 5, 0)) + payload
+
+    def vlan(tpid, tci, inner_et, body):
+        return struct.pack(">HH", tci, inner_et) + body, tpid
+
+    def ipv6(nh, l4=b""):
+        return struct.pack(">IHBB", 0x6ABCDEF1, len(l4), nh, 64) + bytes(range(16)) + bytes(range(16, 32)) + l4
+
+    f = []
+    base = eth(0x0800, ipv4(17, udp(1500, 53, b"GET / HTTP/1.1")))
+    for n in range(0, 60):
+        f.append(base[:n])                              # every truncation of a UDP frame
+    tb = eth(0x0800, ipv4(6, tcp(1234, 1999, payload=b"GET x")))
+    for n in (33, 34, 35, 41, 42, 43, 53, 54, 55):
+        f.append(tb[:n])
+    for ihl in range(0, 16):                            # every IHL, incl. < 5
+        fr = bytearray(eth(0x0800, ipv4(6, tcp(80, 8080), ihl=max(ihl, 5))) + bytes(64))
+        fr[14] = 0x40 | ihl
+        f.append(bytes(fr))
+    for doff in range(0, 16):
+        f.append(eth(0x0800, ipv4(6, tcp(1000, 2000, doff=doff))) + bytes(8))
+    # VLAN / QinQ, with truncations around the tag boundaries
+    body4 = ipv4(17, udp(1000, 2000))
+    inner = struct.pack(">HH", 0x0064, 0x0800) + body4
+    q1 = eth(0x8100, inner)
+    qq = eth(0x88A8, struct.pack(">HH", 0x00C8, 0x8100) + inner)
+    q3 = eth(0x8100, struct.pack(">HH", 1, 0x8100) + struct.pack(">HH", 2, 0x8100) + inner)
+    for fr in (q1, qq, q3):
+        for n in (14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 37, 38, 41, 42, 45, 46, 49, 50, len(fr)):
+            f.append(fr[:n])
+    # IPv6 with TCP/UDP/other next headers, truncations
+    for nh, l4 in ((6, tcp(443, 1500)), (17, udp(1000, 53)), (58, bytes(8)), (0, bytes(8))):
+        fr = eth(0x86DD, ipv6(nh, l4))
+        for n in (14, 20, 53, 54, 55, 61, 62, 73, 74, len(fr)):
+            f.append(fr[:n])
+        f.append(eth(0x8100, struct.pack(">HH", 5, 0x86DD) + ipv6(nh, l4)))
+    # ICMP, ARP, odd EtherTypes, protocol 0
+    f.append(eth(0x0800, ipv4(1, bytes([8, 0, 0xAB, 0xCD, 0, 1, 0, 2]) + bytes(20))))
+    f.append(eth(0x0800, ipv4(1, bytes([8, 0, 0xAB, 0xCD, 0, 1]))))
+    f.append(eth(0x0806, bytes(28)))
+    f.append(eth(0x0800, ipv4(0, bytes(30))))
+    f.append(eth(0x0800, ipv4(255, bytes(30))))
+    f.append(eth(0x86DD, bytes(10)))
+    # address / port boundary values for the filters
+    for src, dst in ((b"\x0a\x00\x00\x00", b"\x0b\x00\x00\x00"), (b"\x09\xff\xff\xff", b"\x0a\xff\xff\xff"),
+                     (b"\x80\x00\x00\x00", b"\x7f\xff\xff\xff"), (b"\xc0\xa8\x01\x01", b"\x01\x01\x01\x01"),
+                     (b"\x0a\x01\x02\x03", b"\x00\x00\x00\x00"), (b"\x0a\x01\x02\x04", b"\x0a\x01\x02\x03")):
+        f.append(eth(0x0800, ipv4(17, udp(53, 53), src=src, dst=dst)))
+    for sp, dp in ((999, 2001), (1000, 5), (5, 2000), (2000, 1000), (0, 65535), (1234, 1), (53, 0)):
+        f.append(eth(0x0800, ipv4(17, udp(sp, dp))))
+        f.append(eth(0x0800, ipv4(6, tcp(sp, dp))))
+    # a frame longer than 65535 is impossible in bt_pkt_desc; a long one near the cap
+    f.append(eth(0x0800, ipv4(17, udp(1500, 1500, bytes(9000)))))
+    return f
+
+
+def build():
+    out = {}
+    caps = {
+        "c1": (synth.capture(synth.C2, 10000), "C1: 10k fixed 64 B Eth/IPv4/UDP"),
+        "c3": (synth.capture(synth.C3, 4096), "C3: IMIX 64/512/1500, 25% 802.1Q"),
+        "c4": (synth.capture(synth.C4, 2048), "C4: QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets"),
+        "fuzz": (synth.capture(synth.FUZZ, 8192), "fuzz: short/odd frames, byte mutations"),
+        "edge": (synth.pack_frames(edge_frames(), align=4, shift=2), "edge: hand-built boundary frames"),
+    }
+    manifest = {"filter_sets": FILTER_SETS, "captures": {}}
+    for name, ((data, desc), what) in caps.items():
+        n = len(desc)
+        rec = ol.ref_parse(data, desc, n)
+        arrays = {"data": data, "desc": desc, "rec": rec}
+        sets = list(FILTER_SETS) if name in ("edge", "fuzz") else ["c3", "mixed", "throw_after", "payload_mid",
+                                                                    "custom", "empty"]
+        for s in sets:
+            code, src = ol.ref_filter(data, desc, n, FILTER_SETS[s])
+            arrays[f"code__{s}"] = code
+            arrays[f"src__{s}"] = src
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+        manifest["captures"][name] = {"n": n, "what": what, "filter_sets": sets}
+        print(name, n, "frames", data.nbytes, "bytes;", len(sets), "filter sets")
+    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1)
+
+
+if __name__ == "__main__":
+    if not ol.ref_available():
+        sys.exit("oracle/_ref/libbt_ref.so missing: make -C oracle ref (needs /root/reference)")
+    build()

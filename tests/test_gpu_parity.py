@@ -1,0 +1,168 @@
+"""GPU parity: the gfx950 path (through the C-ABI) against the golden fixtures from the
+compiled reference and against the oracle on seeded captures. Bit-exact: records,
+decision bytes, verdict words, compacted pass indices."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+from beatrice_amd import abi, synth
+from conftest import load_golden
+from golden_util import CAPTURES, compare_decisions, eval_order
+
+pytestmark = pytest.mark.gpu
+
+
+def run_dev(ctx, data, desc, n, stride=0, records=True, filt=True):
+    r = abi.DeviceRun(ctx, data, desc, n, stride=stride, records=records, decide=filt, verdict=filt,
+                      pass_idx=filt)
+    r.run()
+    out = r.fetch()
+    r.free()
+    return out
+
+
+def check_filter_outputs(out, n):
+    dec = out["decide"]
+    ver = out["verdict"]
+    bits = np.unpackbits(ver.view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(bits, (dec >> 6) == 0), "verdict bits != decide codes"
+    tail = np.unpackbits(ver.view(np.uint8), bitorder="little")[n:]
+    assert not tail.any(), "verdict bits set past n"
+    exp_idx = np.nonzero(bits)[0]
+    assert out["n_pass"] == len(exp_idx)
+    assert np.array_equal(out["pass_idx"], exp_idx.astype(np.uint32)), "pass_idx not the ordered passing set"
+
+
+@pytest.mark.parametrize("cap", CAPTURES)
+def test_records_match_reference(gpu_ctx, cap):
+    g, _ = load_golden(cap)
+    n = len(g["desc"])
+    gpu_ctx.compile([])
+    out = run_dev(gpu_ctx, g["data"], g["desc"], n, records=True, filt=False)
+    bad = np.nonzero((out["records"] != g["rec"]).any(axis=1))[0]
+    assert len(bad) == 0, f"{cap}: {len(bad)} records differ; first {bad[:5]}"
+
+
+@pytest.mark.parametrize("cap", CAPTURES)
+def test_filters_match_reference(gpu_ctx, cap):
+    g, man = load_golden(cap)
+    n = len(g["desc"])
+    for s in man["captures"][cap]["filter_sets"]:
+        filters = man["filter_sets"][s]
+        prog = gpu_ctx.compile(filters)
+        assert [p.source_index for p in prog] == eval_order(filters)
+        out = run_dev(gpu_ctx, g["data"], g["desc"], n, records=(s == "c3"), filt=True)
+        compare_decisions(out["decide"], g[f"code__{s}"], g[f"src__{s}"], filters, where=f"{cap}/{s}")
+        check_filter_outputs(out, n)
+        if s == "c3":
+            assert np.array_equal(out["records"], g["rec"])
+
+
+@pytest.mark.parametrize("stride", [16, 32, 64, 128, 80, 200])
+def test_fixed_stride_matches_oracle(gpu_ctx, stride):
+    n = 70001
+    data, desc = synth.capture(synth.C2, n)
+    # re-pack the 64-B frames at `stride` (truncated or zero-padded to the stride)
+    frames = data[:n * 64].reshape(n, 64)
+    buf = np.zeros((n, stride), np.uint8)
+    m = min(64, stride)
+    buf[:, :m] = frames[:, :m]
+    buf = buf.reshape(-1)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    gpu_ctx.compile(filters)
+    out = run_dev(gpu_ctx, buf, None, n, stride=stride)
+    rec, dec, npass = ol.oracle_run(buf, None, n, filters, stride=stride)
+    assert np.array_equal(out["records"], rec)
+    assert np.array_equal(out["decide"], dec)
+    assert out["n_pass"] == npass
+    check_filter_outputs(out, n)
+
+
+@pytest.mark.parametrize("cfg,n", [(synth.C3, 1 << 20), (synth.C4, 1 << 20), (synth.FUZZ, 1 << 20),
+                                   (synth.FUZZ, 777)])
+def test_seeded_captures_match_oracle(gpu_ctx, cfg, n):
+    data, desc = synth.capture(cfg, n, seed=0xC0FFEE + cfg)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1},
+               {"type": abi.BPF, "expr": "udp tcp", "priority": 0}]
+    gpu_ctx.compile(filters)
+    out = run_dev(gpu_ctx, data, desc, n)
+    rec, dec, npass = ol.oracle_run(data, desc, n, filters)
+    bad = np.nonzero((out["records"] != rec).any(axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} records differ; first {bad[:5]}"
+    assert np.array_equal(out["decide"], dec)
+    assert out["n_pass"] == npass
+    check_filter_outputs(out, n)
+
+
+@pytest.mark.parametrize("cap", ["c3", "c4", "fuzz", "edge"])
+def test_host_batch_path(cap):
+    """bt_parse_filter: host buffers, prefix gather into pinned staging, multi-chunk
+    double-buffered pipeline (chunk 1024 packets)."""
+    g, man = load_golden(cap)
+    n = len(g["desc"])
+    ctx = abi.Context(0, host_chunk_packets=1000)
+    try:
+        filters = man["filter_sets"]["c3"]
+        ctx.compile(filters)
+        out = ctx.run_host(g["data"], g["desc"])
+        assert np.array_equal(out["records"], g["rec"])
+        compare_decisions(out["decide"], g["code__c3"], g["src__c3"], filters, where=cap)
+        bits = np.unpackbits(out["verdict"].view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(np.nonzero(bits)[0].astype(np.uint32), out["pass_idx"])
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("cfg", [synth.C2, synth.C3])
+def test_full_size_batch_properties(gpu_ctx, cfg):
+    """BASELINE size (16M packets): size-independent checks — a 64Ki-packet random
+    sample against the oracle, verdict/decide/pass_idx consistency, monotone indices."""
+    n = 1 << 24
+    data, desc = synth.capture(cfg, n)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    gpu_ctx.compile(filters)
+    stride = 64 if cfg == synth.C2 else 0
+    out = run_dev(gpu_ctx, data, None if stride else desc, n, stride=stride)
+    check_filter_outputs(out, n)
+    rng = np.random.default_rng(7)
+    idx = np.sort(rng.choice(n, 65536, replace=False))
+    sub_desc = desc[idx]
+    rec, dec, _ = ol.oracle_run(data, sub_desc, len(idx), filters)
+    assert np.array_equal(out["records"][idx], rec)
+    assert np.array_equal(out["decide"][idx], dec)
+    assert np.all(np.diff(out["pass_idx"].astype(np.int64)) > 0)
+
+
+def test_edge_batches(gpu_ctx):
+    gpu_ctx.compile([{"type": abi.PROTOCOL, "expr": "udp"}])
+    # n = 0
+    data = np.zeros(256, np.uint8)
+    out = run_dev(gpu_ctx, data, np.zeros(0, np.uint64), 0)
+    assert out["n_pass"] == 0
+    # n = 1, zero-length frame; a 65535-byte frame; a descriptor past the buffer end
+    big = np.zeros(70000, np.uint8)
+    big[12:14] = [0x08, 0x00]
+    big[14] = 0x45
+    big[23] = 17
+    desc = synth.make_desc([0, 0, 60000], [0, 65535, 9000])
+    out = run_dev(gpu_ctx, big, desc[:1], 1)
+    assert out["records"][0, 24] == abi.L_ETH and out["records"][0, 25] == 0
+    rec, dec, _ = ol.oracle_run(big, desc[:2], 2, [{"type": abi.PROTOCOL, "expr": "udp"}])
+    out = run_dev(gpu_ctx, big, desc[:2], 2)
+    assert np.array_equal(out["records"], rec) and np.array_equal(out["decide"], dec)
+    out = run_dev(gpu_ctx, big, desc, 3)   # third frame runs past `bytes`: no fault
+    assert out["records"].shape == (3, 96)
+
+
+def test_too_many_filters(gpu_ctx):
+    fs = [{"type": abi.BPF, "expr": "udp", "priority": i} for i in range(65)]
+    with pytest.raises(abi.BtError):
+        gpu_ctx.compile(fs)
+    prog = gpu_ctx.compile(fs[:64])
+    assert len(prog) == 64 and prog[0].source_index == 63
