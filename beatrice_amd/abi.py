@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbeatrice_gpu.so")
+LIB_PATH = os.environ.get("BT_LIB_PATH") or os.path.join(HERE, "libbeatrice_gpu.so")
 
 BT_REC_BYTES = 96
 BT_MAX_FILTERS = 64
@@ -53,7 +53,12 @@ class FilterSlot(ctypes.Structure):
 
 class Opts(ctypes.Structure):
     _fields_ = [("host_chunk_packets", ctypes.c_uint32), ("host_chunk_bytes", ctypes.c_uint32),
-                ("grid_waves", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+                ("grid_waves", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 4)]
+
+
+OPT_NO_PREFETCH = 0x1
+OPT_TILE_BLOCKED = 0x2
+OPT_RECORDS_AOS = 0x4
 
 
 class Batch(ctypes.Structure):
@@ -186,10 +191,11 @@ class DeviceBuffer:
 class Context:
     """One bt_ctx on one device."""
 
-    def __init__(self, device: int = 0, host_chunk_packets: int = 0, grid_waves: int = 0):
+    def __init__(self, device: int = 0, host_chunk_packets: int = 0, grid_waves: int = 0, flags: int = 0):
         opts = Opts()
         opts.host_chunk_packets = host_chunk_packets
         opts.grid_waves = grid_waves
+        opts.flags = flags
         h = ctypes.c_void_p(0)
         _check(lib().bt_create(device, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h.value

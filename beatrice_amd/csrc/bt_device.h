@@ -31,6 +31,7 @@ struct MainArgs {
     uint8_t* decide;
     uint64_t* verdict;
     uint32_t* tile_pass;       // per-tile pass counts (compaction input)
+    uint32_t blocked;          // tile order: 0 cyclic, 1 one contiguous range per wavefront
 };
 
 constexpr int kWave = 64;
@@ -44,7 +45,7 @@ constexpr uint32_t kNeedFilter = 38;              // PacketFilter reads bytes 12
 // Launch wrappers (bt_kernels.hip). All are asynchronous on `stream`.
 enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2 };
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
-                int grid_blocks, void* stream);
+                int grid_blocks, bool prefetch, void* stream);
 int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
                    uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream);
 int device_grid_blocks(int device);

@@ -176,7 +176,121 @@ __device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_
     }
 }
 
-template <int FIXED_LOG2, int REC, bool FILTER>
+// Header windows of one 64-packet tile in flight in registers (LOAD stage).
+//  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
+//  descriptors:  round A = the first 64 B (chunks 0..3) of every packet's 16-B-aligned
+//                window, 4 lanes per packet, 16 packets per wave instruction.
+template <int FIXED_LOG2>
+struct Stage {
+    static constexpr int kV = FIXED_LOG2 >= 0 ? (1 << (FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0)) : 4;
+    uint4 v[kV];
+    uint64_t qa0[FIXED_LOG2 >= 0 ? 1 : 4];   // aligned window base of packet j*16 + lane/4
+    uint64_t off;                             // this lane's own packet
+    uint32_t len;
+};
+
+template <int FIXED_LOG2>
+__device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint32_t lane, Stage<FIXED_LOG2>& st) {
+    const uint32_t p0 = t * 64u;
+    const uint32_t my = p0 + lane;
+    const bool live = my < a.n;
+    if constexpr (FIXED_LOG2 >= 0) {
+        constexpr int kL = FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0;
+        constexpr uint32_t cpp = 1u << kL;
+        st.off = (uint64_t)my * a.stride;
+        st.len = a.stride;
+        const uint8_t* span = a.base + (uint64_t)p0 * a.stride;
+#pragma unroll
+        for (uint32_t j = 0; j < cpp; ++j) {
+            const uint32_t g = j * 64u + lane;
+            const bool ok = p0 + (g >> kL) < a.n;
+            st.v[j] = ok ? *reinterpret_cast<const uint4*>(span + (uint64_t)g * 16u) : make_uint4(0, 0, 0, 0);
+        }
+    } else {
+        if (a.desc) {
+            const uint64_t d = live ? a.desc[my] : 0ull;
+            st.off = d & 0xFFFFFFFFFFFFull;
+            st.len = (uint32_t)(d >> 48);
+        } else {
+            st.off = live ? (uint64_t)my * a.stride : 0ull;
+            st.len = live ? a.stride : 0u;
+        }
+        const uint32_t off_lo = (uint32_t)st.off, off_hi = (uint32_t)(st.off >> 32);
+        const uint32_t c = lane & 3u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t q = j * 16u + (lane >> 2);
+            const uint64_t qo = ((uint64_t)(uint32_t)__shfl((int)off_hi, (int)q) << 32) |
+                                (uint32_t)__shfl((int)off_lo, (int)q);
+            const uint32_t ql = (uint32_t)__shfl((int)st.len, (int)q);
+            const uint64_t a0 = qo & ~15ull;
+            const uint64_t addr = a0 + 16u * c;
+            st.qa0[j] = a0;
+            const bool ok = (p0 + q < a.n) && (16u * c < ((uint32_t)qo & 15u) + ql) && (addr + 16u <= a.bytes);
+            st.v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+        }
+    }
+}
+
+template <int FIXED_LOG2>
+__device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32_t* img, uint32_t lane) {
+    if constexpr (FIXED_LOG2 >= 0) {
+        constexpr int kL = FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0;
+        constexpr uint32_t cpp = 1u << kL;
+#pragma unroll
+        for (uint32_t j = 0; j < cpp; ++j) {
+            const uint32_t g = j * 64u + lane;
+            uint32_t* dst = img + (g >> kL) * kRowDwords + (g & (cpp - 1u)) * 4u;
+            dst[0] = st.v[j].x; dst[1] = st.v[j].y; dst[2] = st.v[j].z; dst[3] = st.v[j].w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + (lane & 3u) * 4u;
+            dst[0] = st.v[j].x; dst[1] = st.v[j].y; dst[2] = st.v[j].z; dst[3] = st.v[j].w;
+        }
+    }
+}
+
+// Upper bound of the frame bytes the walk + filters will read, from round A's 64 B
+// (everything it looks at — EtherTypes at 12/16/20, IHL at L3+0 — sits below byte 49).
+__device__ __forceinline__ uint32_t header_end(const uint32_t* row, uint32_t s, uint32_t len, uint32_t floor_) {
+    uint32_t w[6];
+    window<6>(row, s, w);
+    const uint32_t et0 = be16_of(w, 12), et1 = be16_of(w, 16), et2 = be16_of(w, 20);
+    uint32_t o3 = 14, et = et0;
+    if (is_vlan(et0)) { o3 = 18; et = et1; if (is_vlan(et1)) { o3 = 22; et = et2; } }
+    const uint32_t a = s + o3;
+    const uint32_t ihl = (row[a >> 2] >> (8 * (a & 3u))) & 0x0Fu;
+    uint32_t end = o3;
+    if (et == 0x0800u) end = o3 + 20u + (ihl > 5 ? 4u * ihl - 20u : 0u) + 20u;
+    else if (et == 0x86DDu) end = o3 + 60u;
+    end = end > floor_ ? end : floor_;
+    return end < len ? end : len;
+}
+
+// Round B: chunks 4..7 for the packets whose headers run past round A's 64 B.
+template <int FIXED_LOG2>
+__device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint32_t lane, const uint64_t* qa0,
+                                             uint32_t my_need, uint32_t* img) {
+    const uint32_t c = 4u + (lane & 3u);
+    uint4 v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t q = j * 16u + (lane >> 2);
+        const uint32_t qn = (uint32_t)__shfl((int)my_need, (int)q);   // bytes of q's window needed
+        const uint64_t addr = qa0[j] + 16u * c;
+        const bool ok = (t * 64u + q < a.n) && (16u * c < qn) && (addr + 16u <= a.bytes);
+        v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + c * 4u;
+        dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+    }
+}
+
+template <int FIXED_LOG2, int REC, bool FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
     __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRowDwords];
@@ -186,70 +300,49 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     const uint32_t* row = img + lane * kRowDwords;
 
     const uint32_t total_waves = gridDim.x * kWavesPerBlock;
-    const uint32_t need = REC != kRecNone ? kNeedParse : kNeedFilter;
 
-    for (uint32_t t = blockIdx.x * kWavesPerBlock + wid; t < a.ntiles; t += total_waves) {
+    // Tile order: cyclic (wave w takes w, w+W, ...) or blocked (wave w takes one
+    // contiguous range, so concurrent accesses spread over the whole buffer).
+    const uint32_t gw = blockIdx.x * kWavesPerBlock + wid;
+    uint32_t t, t_end, step;
+    if (a.blocked) {
+        const uint32_t per = (a.ntiles + total_waves - 1) / total_waves;
+        t = gw * per;
+        t_end = min(a.ntiles, t + per);
+        step = 1;
+    } else {
+        t = gw;
+        t_end = a.ntiles;
+        step = total_waves;
+    }
+    Stage<FIXED_LOG2> st;
+    if (PREFETCH && t < t_end) issue_loads<FIXED_LOG2>(a, t, lane, st);
+    for (; t < t_end; t += step) {
         const uint32_t p0 = t * 64u;
         const uint32_t my = p0 + lane;
         const bool live = my < a.n;
 
-        // ---- 1. LOAD --------------------------------------------------------
-        uint64_t my_off;
-        uint32_t my_len;
-        if constexpr (FIXED_LOG2 >= 0) {
-            constexpr int kL = FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0;
-            my_off = (uint64_t)my * a.stride;
-            my_len = a.stride;
-            constexpr uint32_t cpp = 1u << kL;                 // 16-B chunks per packet
-            const uint8_t* span = a.base + (uint64_t)p0 * a.stride;
-            uint4 v[cpp];
+        // ---- 1. LOAD (this tile's windows -> LDS; next tile's loads go in flight) ----
+        if (!PREFETCH) issue_loads<FIXED_LOG2>(a, t, lane, st);
+        stage_to_lds<FIXED_LOG2>(st, img, lane);
+        const uint64_t my_off = st.off;
+        const uint32_t my_len = st.len;
+        uint64_t qa0[FIXED_LOG2 >= 0 ? 1 : 4];
 #pragma unroll
-            for (uint32_t j = 0; j < cpp; ++j) {
-                const uint32_t g = j * 64u + lane;
-                const uint32_t q = g >> kL;
-                const bool ok = p0 + q < a.n;
-                v[j] = ok ? *reinterpret_cast<const uint4*>(span + (uint64_t)g * 16u) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < cpp; ++j) {
-                const uint32_t g = j * 64u + lane;
-                const uint32_t q = g >> kL, c = g & (cpp - 1u);
-                uint32_t* dst = img + q * kRowDwords + c * 4u;
-                dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
-            }
-        } else {
-            if (a.desc) {
-                const uint64_t d = live ? a.desc[my] : 0ull;
-                my_off = d & 0xFFFFFFFFFFFFull;
-                my_len = (uint32_t)(d >> 48);
-            } else {
-                my_off = live ? (uint64_t)my * a.stride : 0ull;
-                my_len = live ? a.stride : 0u;
-            }
-            const uint32_t off_lo = (uint32_t)my_off, off_hi = (uint32_t)(my_off >> 32);
-            const uint32_t c = lane & 7u;
-            uint4 v[8];
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) {
-                const uint32_t q = j * 8u + (lane >> 3);
-                const uint64_t qo = ((uint64_t)(uint32_t)__shfl((int)off_hi, (int)q) << 32) |
-                                    (uint32_t)__shfl((int)off_lo, (int)q);
-                const uint32_t ql = (uint32_t)__shfl((int)my_len, (int)q);
-                const uint64_t a0 = qo & ~15ull;
-                const uint32_t sq = (uint32_t)qo & 15u;
-                const uint32_t nq = ql < need ? ql : need;
-                const uint64_t addr = a0 + 16u * c;
-                const bool ok = (p0 + q < a.n) && (16u * c < sq + nq) && (addr + 16u <= a.bytes);
-                v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) {
-                const uint32_t q = j * 8u + (lane >> 3);
-                uint32_t* dst = img + q * kRowDwords + c * 4u;
-                dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+        for (int j = 0; j < (FIXED_LOG2 >= 0 ? 1 : 4); ++j) qa0[j] = st.qa0[j];
+        wave_lds_sync();
+        if (PREFETCH && t + step < t_end) issue_loads<FIXED_LOG2>(a, t + step, lane, st);
+        if constexpr (FIXED_LOG2 < 0) {
+            if (REC != kRecNone) {   // filter-only needs <= 38 B: round A always suffices
+                const uint32_t s0 = (uint32_t)my_off & 15u;
+                const uint32_t end = live ? s0 + header_end(row, s0, my_len, FILTER ? kNeedFilter : 0u) : 0u;
+                const uint32_t my_need = end > 64u ? end : 0u;
+                if (__ballot(my_need != 0u) != 0ull) {
+                    load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_need, img);
+                    wave_lds_sync();
+                }
             }
         }
-        wave_lds_sync();
 
         // ---- 2. PARSE -------------------------------------------------------
         const uint32_t s = (FIXED_LOG2 >= 0) ? 0u : ((uint32_t)my_off & 15u);
@@ -323,12 +416,14 @@ __global__ __launch_bounds__(256) void bt_chunk_sums(const uint32_t* tile_pass, 
 }
 
 // K3: block c scans its chunk's tile counts, adds the prefix of earlier chunks and
-// writes the indices of passing packets in ascending order (one wave per tile row:
-// the set lanes of one verdict word store to consecutive slots).
+// writes the indices of passing packets in ascending order. The chunk's verdict
+// words are staged in LDS first (one coalesced pass), so the per-tile scatter loop
+// reads LDS, not HBM; the set lanes of one verdict word store to consecutive slots.
 __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const uint32_t* tile_pass,
                                                   const uint32_t* chunk_sums, uint32_t nchunks,
                                                   uint32_t ntiles, uint32_t* pass_idx, uint32_t* n_pass) {
     __shared__ uint32_t tile_off[kChunkTiles];
+    __shared__ uint64_t words[kChunkTiles];
     __shared__ uint32_t red[4];
     __shared__ uint32_t wsum[4];
     const uint32_t c = blockIdx.x;
@@ -349,13 +444,16 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
     if (!pass_idx) return;   // count only
     __syncthreads();
 
-    // exclusive scan of this chunk's tile counts: thread tid owns tiles 4*tid..4*tid+3
+    // exclusive scan of this chunk's tile counts: thread tid owns tiles 4*tid..4*tid+3;
+    // the verdict words go to LDS in the same pass (coalesced)
     uint32_t v[4], run = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t t = c * kChunkTiles + 4 * tid + k;
         v[k] = t < ntiles ? tile_pass[t] : 0u;
         run += v[k];
+        const uint32_t tw = c * kChunkTiles + k * 256 + tid;
+        words[k * 256 + tid] = tw < ntiles ? verdict[tw] : 0ull;
     }
     uint32_t incl = run;   // inclusive wave scan of per-thread sums
     for (int o = 1; o < 64; o <<= 1) {
@@ -372,42 +470,59 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
     __syncthreads();
 
     // scatter: wave wid handles tiles wid, wid+4, ... of the chunk
+    const uint64_t below_mask = (1ull << lane) - 1ull;
     for (uint32_t i = wid; i < kChunkTiles; i += 4) {
-        const uint32_t t = c * kChunkTiles + i;
-        if (t >= ntiles) break;
-        const uint64_t word = verdict[t];
-        if (word == 0ull) continue;
-        if ((word >> lane) & 1ull) {
-            const uint32_t below = (uint32_t)__popcll(word & ((1ull << lane) - 1ull));
-            pass_idx[tile_off[i] + below] = t * 64u + lane;
-        }
+        const uint64_t word = words[i];
+        if ((word >> lane) & 1ull)
+            pass_idx[tile_off[i] + (uint32_t)__popcll(word & below_mask)] = (c * kChunkTiles + i) * 64u + lane;
     }
 }
 
+// One residency wave of blocks: the persistent grid-stride loop then has no tail of
+// late blocks (measured: 2x residency cost C3 11 %).
+template <class K>
+int resident_grid(K kernel) {
+    static int blocks = 0;   // per kernel instantiation
+    if (!blocks) {
+        int dev = 0, per_cu = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu < 1)
+            return 1024;
+        blocks = prop.multiProcessorCount * per_cu;
+    }
+    return blocks;
+}
+
 template <int FL, int REC, bool F>
-void launch_t(const MainArgs& a, const DevProgram& prog, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((bt_parse_filter_main<FL, REC, F>), dim3(grid), dim3(kBlock), 0, st, a, prog);
+void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st) {
+    const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    auto go = [&](auto kernel) {
+        int g = grid > 0 ? grid : resident_grid(kernel);
+        if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
+        hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), 0, st, a, prog);
+    };
+    if (pf) go(bt_parse_filter_main<FL, REC, F, true>);
+    else go(bt_parse_filter_main<FL, REC, F, false>);
 }
 
 template <int FL>
-void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, hipStream_t st) {
+void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, bool pf, hipStream_t st) {
     if (rec == kRecPlanes) {
-        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, st); else launch_t<FL, kRecPlanes, false>(a, prog, grid, st);
+        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, pf, st); else launch_t<FL, kRecPlanes, false>(a, prog, grid, pf, st);
     } else if (rec == kRecAoS) {
-        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, st); else launch_t<FL, kRecAoS, false>(a, prog, grid, st);
+        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, pf, st); else launch_t<FL, kRecAoS, false>(a, prog, grid, pf, st);
     } else {
-        launch_t<FL, kRecNone, true>(a, prog, grid, st);
+        launch_t<FL, kRecNone, true>(a, prog, grid, pf, st);
     }
 }
 
 }  // namespace
 
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter, int grid_blocks,
-                void* stream) {
+                bool prefetch, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    int grid = grid_blocks > 0 ? grid_blocks : 1;
-    if ((uint32_t)grid > needed) grid = (int)(needed ? needed : 1);
+    const int grid = grid_blocks;   // <= 0: one residency wave of the chosen variant
     int fl = -1;   // fixed-stride fast path when the stride is 16/32/64/128 B
     if (!a.desc) {
         if (a.stride == 16) fl = 0;
@@ -415,12 +530,15 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
         else if (a.stride == 64) fl = 2;
         else if (a.stride == 128) fl = 3;
     }
+    // Next-tile prefetch pays for descriptor mode (+3 % C3) but not for fixed stride
+    // (-16 % C2: the early loads interleave with the record stores).
+    prefetch = prefetch && fl < 0;
     switch (fl) {
-    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, st); break;
-    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, st); break;
-    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, st); break;
-    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, st); break;
-    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, st); break;
+    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, prefetch, st); break;
+    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, prefetch, st); break;
+    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, prefetch, st); break;
+    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, prefetch, st); break;
+    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, prefetch, st); break;
     }
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }
@@ -438,10 +556,8 @@ int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t 
 }
 
 int device_grid_blocks(int device) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 1024;
-    // 33 KiB of LDS per block -> 4 blocks per CU; 2 rounds of residency for slack.
-    return prop.multiProcessorCount * 4 * 2;
+    (void)device;
+    return 0;   // auto: one residency wave per kernel variant (resident_grid)
 }
 
 }  // namespace bt

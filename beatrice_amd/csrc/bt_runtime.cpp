@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -128,9 +129,10 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.decide = o->decide;
     a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
     a.tile_pass = compact ? c->tile_pass : nullptr;
-    const int rec = o->records ? (aos ? kRecAoS : kRecPlanes) : kRecNone;
+    a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
+    const int rec = o->records ? ((aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) ? kRecAoS : kRecPlanes) : kRecNone;
     if (e0) HIP_TRY(hipEventRecord(e0, st));
-    int rc = launch_main(a, c->prog, rec, filter, c->grid, st);
+    int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (e1) HIP_TRY(hipEventRecord(e1, st));
     if (compact) {
@@ -402,7 +404,12 @@ int bt_parse_filter(bt_ctx* c, const uint8_t* base, const bt_pkt_desc* desc, uin
 int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {
     if (!c || !out) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMalloc(out, bytes ? bytes : 16));
+    static const unsigned flags = [] {
+        const char* e = getenv("BT_MALLOC_FLAGS");   // experiments: 4 = hipDeviceMallocContiguous
+        return e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
+    }();
+    if (flags) HIP_TRY(hipExtMallocWithFlags(out, bytes ? bytes : 16, flags));
+    else HIP_TRY(hipMalloc(out, bytes ? bytes : 16));
     return BT_OK;
 }
 

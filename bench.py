@@ -111,6 +111,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 18)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--grid-waves", type=int, default=0, help="persistent grid size in wavefronts (0 = auto)")
+    ap.add_argument("--no-prefetch", action="store_true", help="A/B: disable the next-tile load prefetch")
+    ap.add_argument("--flags", type=int, default=None, help="raw bt_opts.flags (A/B experiments)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -126,7 +129,8 @@ def main():
     n = args.packets
 
     data, desc = synth.capture(wl["cfg"], n, seed=synth.SEEDS[wl["cfg"]] + rank)
-    ctx = abi.Context(local)
+    flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
+    ctx = abi.Context(local, grid_waves=args.grid_waves, flags=flags)
     if wl["filters"]:
         ctx.compile(wl["filters"])
     filt = wl["filters"] is not None
@@ -134,6 +138,7 @@ def main():
                         records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt)
     for _ in range(args.warmup):
         run.run()
+    ctx.time_device(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
     ctx.synchronize()
     n_pass = run.fetch().get("n_pass", 0) if filt else 0
 
@@ -159,11 +164,14 @@ def main():
 
     algo = algorithmic_bytes(desc, wl["fixed"], wl["parse"], filt, n_pass)
     achieved = algo / (main_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
+    traffic, traffic_src = None, None
+    if os.path.exists(args.traffic_json):   # rocprofv3 PMC passes of this kernel (tools/pmc_traffic.py)
         try:
             with open(args.traffic_json) as fh:
-                traffic = json.load(fh).get(args.config)
+                rec = json.load(fh).get(args.config)
+            if rec and rec.get("packets") == n:
+                traffic = rec["traffic"]
+                traffic_src = os.path.relpath(args.traffic_json, ROOT)
         except Exception:
             traffic = None
 
@@ -189,9 +197,11 @@ def main():
                        "pass_fraction": round(n_pass / n, 4) if filt else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "bt_parse_filter_main", "kernel_ms": round(main_ms, 4),
                          "algorithmic_bytes_per_packet": round(algo / n, 2),
-                         "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1)},
+                         "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),
+                         "gpu_span_ms_per_step": round(ms_iter, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

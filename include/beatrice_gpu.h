@@ -214,8 +214,13 @@ typedef struct bt_opts {
     uint32_t host_chunk_packets;   /* bt_parse_filter pipeline chunk (0 = default 1M)  */
     uint32_t host_chunk_bytes;     /* pinned staging bytes per chunk (0 = default 256 MiB) */
     uint32_t grid_waves;           /* 0 = auto (persistent grid sized to the device)    */
-    uint32_t reserved[5];
+    uint32_t flags;                /* BT_OPT_*                                          */
+    uint32_t reserved[4];
 } bt_opts;
+
+#define BT_OPT_NO_PREFETCH 0x1u    /* disable the next-tile load prefetch (A/B only)    */
+#define BT_OPT_TILE_BLOCKED 0x2u   /* one contiguous tile range per wavefront           */
+#define BT_OPT_RECORDS_AOS 0x4u    /* device records as bt_rec AoS instead of planes    */
 
 typedef struct bt_batch {          /* device-resident input */
     const uint8_t* base;           /* packet bytes                                      */
