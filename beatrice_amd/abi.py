@@ -59,6 +59,7 @@ class Opts(ctypes.Structure):
 OPT_NO_PREFETCH = 0x1
 OPT_TILE_BLOCKED = 0x2
 OPT_RECORDS_AOS = 0x4
+OPT_GRAPH = 0x8
 
 
 class Batch(ctypes.Structure):
@@ -74,7 +75,7 @@ class Outputs(ctypes.Structure):
 EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
-    "bt_parse_filter", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
+    "bt_parse_filter", "bt_parse_filter_ptrs", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather",
 ]
 
@@ -103,6 +104,7 @@ def lib() -> ctypes.CDLL:
         "bt_reserve": (ctypes.c_int, [vp, u32]),
         "bt_parse_filter_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), vp]),
         "bt_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_dev_malloc": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
         "bt_dev_free": (ctypes.c_int, [vp, vp]),
         "bt_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),

@@ -1,0 +1,280 @@
+// GpuPacketFilter.cpp — see GpuPacketFilter.hpp. Reference behaviour cited as
+// src/PacketFilter.cpp:<line> (Open-Sentra/beatrice).
+#include "GpuPacketFilter.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <regex>
+#include <stdexcept>
+
+namespace beatrice {
+namespace gpu {
+
+namespace {
+
+uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+uint32_t be32(const uint8_t* p) { return (be16(p) << 16) | be16(p + 2); }
+
+// The device's eval_slot (bt_kernels.hip) for one packet: used only to continue a
+// packet whose chain the device handed to the host at a PAYLOAD/CUSTOM slot.
+// 1 pass, 0 reject, 2 throw.
+int eval_builtin(const bt_filter_slot& s, const uint8_t* d, size_t len) {
+    const bool gate = len >= 34 && be16(d + 12) == 0x0800;
+    const uint32_t proto = gate ? d[23] : 0;
+    const bool l4ok = gate && ((proto == 6 && len >= 54) || (proto == 17 && len >= 42));
+    switch (s.kind) {
+    case BT_K_TRUE: return 1;
+    case BT_K_FALSE: return 0;
+    case BT_K_BPF:
+        return gate && (((s.a & 1) && proto == 6) || ((s.a & 2) && proto == 17) || ((s.a & 4) && proto == 1));
+    case BT_K_PROTO_EQ: return gate && proto == s.a;
+    case BT_K_PROTO_NZ: return gate && proto != 0;
+    case BT_K_IP_MASK:
+        return gate && (((be32(d + 26) & s.b) == s.a) || ((be32(d + 30) & s.b) == s.a));
+    case BT_K_PORT: {
+        if (!l4ok) return 0;
+        const uint32_t sp = be16(d + 34), dp = be16(d + 36);
+        return (sp >= s.a && sp <= s.b) || (dp >= s.a && dp <= s.b);
+    }
+    case BT_K_IP_THROW: return gate ? 2 : 0;
+    case BT_K_PORT_THROW: return l4ok ? 2 : 0;
+    default: return 1;
+    }
+}
+
+// applyPayloadFilter (src/PacketFilter.cpp:288-321) for a non-empty, valid regex.
+bool payload_match(const std::regex& re, const uint8_t* d, size_t len) {
+    if (len < 34) return false;
+    if (be16(d + 12) != 0x0800) return false;
+    const size_t payloadOffset = 14 + (size_t)(d[14] & 0x0F) * 4;
+    if (len <= payloadOffset) return false;
+    std::string payload(reinterpret_cast<const char*>(d + payloadOffset), std::min(len - payloadOffset, size_t(100)));
+    try {
+        return std::regex_search(payload, re);
+    } catch (const std::regex_error&) {
+        return false;
+    }
+}
+
+}  // namespace
+
+GpuPacketFilter::GpuPacketFilter(int device, const bt_opts* opts) {
+    if (bt_create(device, opts, &ctx_) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+}
+
+GpuPacketFilter::~GpuPacketFilter() { bt_destroy(ctx_); }
+
+Result<void> GpuPacketFilter::addFilter(const std::string& name, const FilterConfig& config) {
+    std::lock_guard<std::mutex> lock(filtersMutex_);   // :19-31
+    if (filters_.find(name) != filters_.end())
+        return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter already exists: " + name);
+    FilterEntry entry;
+    entry.config = config;
+    filters_[name] = entry;
+    dirty_ = true;
+    return Result<void>::success();
+}
+
+Result<void> GpuPacketFilter::removeFilter(const std::string& name) {
+    std::lock_guard<std::mutex> lock(filtersMutex_);   // :33-43
+    auto it = filters_.find(name);
+    if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
+    filters_.erase(it);
+    dirty_ = true;
+    return Result<void>::success();
+}
+
+Result<void> GpuPacketFilter::setFilterEnabled(const std::string& name, bool enabled) {
+    std::lock_guard<std::mutex> lock(filtersMutex_);   // :45-55
+    auto it = filters_.find(name);
+    if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
+    it->second.config.enabled = enabled;
+    dirty_ = true;
+    return Result<void>::success();
+}
+
+Result<void> GpuPacketFilter::setCustomFilter(const std::string& name, std::function<bool(const Packet&)> filterFunc) {
+    std::lock_guard<std::mutex> lock(filtersMutex_);   // :155-166
+    auto it = filters_.find(name);
+    if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
+    it->second.customFunc = std::move(filterFunc);
+    dirty_ = true;
+    return Result<void>::success();
+}
+
+std::vector<std::string> GpuPacketFilter::getActiveFilters() const {
+    std::lock_guard<std::mutex> lock(filtersMutex_);   // :132-143
+    std::vector<std::string> active;
+    for (const auto& [name, entry] : filters_)
+        if (entry.config.enabled) active.push_back(name);
+    return active;
+}
+
+GpuPacketFilter::FilterStats GpuPacketFilter::getStats() const {
+    std::lock_guard<std::mutex> lock(statsMutex_);
+    return stats_;
+}
+
+void GpuPacketFilter::resetStats() {
+    std::lock_guard<std::mutex> lock(statsMutex_);
+    stats_ = FilterStats{};
+}
+
+void GpuPacketFilter::updateStats(const std::string& filterName, bool passed, std::chrono::microseconds t) {
+    std::lock_guard<std::mutex> lock(statsMutex_);   // :374-386
+    stats_.packetsProcessed++;
+    if (passed) stats_.packetsPassed++;
+    else stats_.packetsDropped++;
+    stats_.totalProcessingTime += t;
+    stats_.filterCounts[filterName]++;
+}
+
+void GpuPacketFilter::compileLocked() {
+    // The reference's own ordering (:63-73): enabled entries in unordered_map iteration
+    // order, then std::sort by priority (descending). Same container, same calls.
+    std::vector<std::pair<std::string, FilterEntry*>> sortedFilters;
+    for (auto& [name, entry] : filters_)
+        if (entry.config.enabled) sortedFilters.emplace_back(name, &entry);
+    std::sort(sortedFilters.begin(), sortedFilters.end(),
+              [](const auto& a, const auto& b) { return a.second->config.priority > b.second->config.priority; });
+    std::vector<bt_filter_desc> descs(sortedFilters.size());
+    for (size_t i = 0; i < sortedFilters.size(); ++i) {
+        const FilterConfig& c = sortedFilters[i].second->config;
+        descs[i].type = static_cast<int32_t>(c.type);
+        descs[i].expression = c.expression.c_str();
+        descs[i].enabled = 1;
+        descs[i].priority = c.priority;
+        descs[i].has_custom_func = sortedFilters[i].second->customFunc ? 1 : 0;
+    }
+    if (bt_filter_compile(ctx_, descs.data(), (uint32_t)descs.size()) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    std::vector<bt_filter_slot> slots(BT_MAX_FILTERS);
+    uint32_t m = 0;
+    bt_filter_program(ctx_, slots.data(), BT_MAX_FILTERS, &m);
+    program_.clear();
+    for (uint32_t k = 0; k < m; ++k) {
+        const auto& src = sortedFilters[slots[k].source_index];
+        program_.push_back(Slot{src.first, src.second, slots[k]});
+    }
+    dirty_ = false;
+}
+
+std::vector<std::string> GpuPacketFilter::evaluationOrder() {
+    std::lock_guard<std::mutex> lock(filtersMutex_);
+    if (dirty_) compileLocked();
+    std::vector<std::string> names;
+    for (const auto& s : program_) names.push_back(s.name);
+    return names;
+}
+
+void GpuPacketFilter::rethrow(const Slot& s) const {
+    // std::stoi's own exceptions (libstdc++: what() == "stoi")
+    if (s.compiled.throw_kind == 2) throw std::out_of_range("stoi");
+    throw std::invalid_argument("stoi");
+}
+
+uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
+    const uint8_t* d = p.data();
+    const size_t len = p.length();
+    for (uint32_t s = first; s < program_.size(); ++s) {
+        const Slot& sl = program_[s];
+        int r;
+        if (sl.compiled.kind != BT_K_HOST) {
+            r = eval_builtin(sl.compiled, d, len);
+        } else if (sl.entry->config.type == FilterType::CUSTOM) {
+            r = sl.entry->customFunc ? (sl.entry->customFunc(p) ? 1 : 0) : 1;   // :323-328
+        } else {
+            // PAYLOAD: the regex is valid (compile checked it); the reference constructs
+            // it per packet, which cannot change regex_search's result.
+            thread_local std::string last_expr;
+            thread_local std::shared_ptr<std::regex> re;
+            if (!re || last_expr != sl.entry->config.expression) {
+                last_expr = sl.entry->config.expression;
+                re = std::make_shared<std::regex>(last_expr);
+            }
+            r = payload_match(*re, d, len) ? 1 : 0;
+        }
+        if (r == 0) return (BT_DECIDE_REJECT << 6) | s;
+        if (r == 2) return (BT_DECIDE_THROW << 6) | s;
+    }
+    return (BT_DECIDE_PASS << 6) | (program_.empty() ? 0u : (uint32_t)program_.size() - 1);
+}
+
+void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide) {
+    const uint32_t n = (uint32_t)packets.size();
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<uint32_t> lens(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        ptrs[i] = packets[i].data();
+        lens[i] = (uint32_t)packets[i].length();
+    }
+    decide.assign(n, 0);
+    if (bt_parse_filter_ptrs(ctx_, ptrs.data(), lens.data(), n, nullptr, nullptr, decide.data(), nullptr,
+                             nullptr) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+}
+
+std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const std::vector<Packet>& packets) {
+    std::vector<FilterResult> results;
+    results.reserve(packets.size());
+    std::lock_guard<std::mutex> lock(filtersMutex_);
+    if (dirty_) compileLocked();
+    if (packets.empty()) return results;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> decide;
+    runBatch(packets, decide);
+    const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
+                     (int64_t)packets.size();
+    for (size_t i = 0; i < packets.size(); ++i) {
+        uint32_t d = decide[i];
+        if ((d >> 6) == BT_DECIDE_HOST) d = resolveHost(packets[i], d & 63u);
+        const uint32_t code = d >> 6, slot = d & 63u;
+        if (code == BT_DECIDE_THROW) rethrow(program_[slot]);   // earlier packets are already counted
+        FilterResult r;
+        r.passed = code == BT_DECIDE_PASS;
+        if (!program_.empty()) {   // :102-111
+            if (r.passed) {
+                r.filterName = program_.back().name;
+                r.reason = "Packet passed all filters";
+            } else {
+                r.filterName = program_[slot].name;
+                r.reason = "Filter " + r.filterName + " rejected packet";
+            }
+        }
+        r.processingTime = per;
+        updateStats(r.filterName, r.passed, per);
+        results.push_back(std::move(r));
+    }
+    return results;
+}
+
+GpuPacketFilter::FilterResult GpuPacketFilter::applyFilters(const Packet& packet) {
+    return applyFilters(std::vector<Packet>{packet}).front();
+}
+
+GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& packets) {
+    Verdicts v;
+    std::lock_guard<std::mutex> lock(filtersMutex_);
+    if (dirty_) compileLocked();
+    if (packets.empty()) return v;
+    const auto t0 = std::chrono::steady_clock::now();
+    runBatch(packets, v.decide);
+    const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
+                     (int64_t)packets.size();
+    const std::string none;
+    for (size_t i = 0; i < packets.size(); ++i) {
+        uint32_t d = v.decide[i];
+        if ((d >> 6) == BT_DECIDE_HOST) v.decide[i] = (uint8_t)(d = resolveHost(packets[i], d & 63u));
+        const uint32_t code = d >> 6, slot = d & 63u;
+        if (code == BT_DECIDE_THROW) rethrow(program_[slot]);
+        const bool passed = code == BT_DECIDE_PASS;
+        if (passed) v.pass_idx.push_back((uint32_t)i);
+        updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
+    }
+    return v;
+}
+
+}  // namespace gpu
+}  // namespace beatrice

@@ -1,0 +1,96 @@
+// GpuPacketFilter.hpp — drop-in replacement for beatrice::PacketFilter
+// (reference include/beatrice/PacketFilter.hpp:15-94) whose per-packet work runs on
+// the MI355X through the C-ABI in include/beatrice_gpu.h.
+//
+// Same public interface, same nested types (it re-uses the reference's own
+// FilterConfig / FilterResult / FilterStats / FilterType), same observable results:
+//   * filters live in an std::unordered_map<std::string, ...> updated with the same
+//     operations as the reference, and are ordered with the same std::sort call
+//     (src/PacketFilter.cpp:63-73), so ties on priority resolve exactly as there;
+//   * FilterResult.passed / filterName / reason match the reference (:102-111);
+//   * an expression the reference's std::stoi would reject rethrows the same
+//     std::invalid_argument / std::out_of_range at the same packet, after the stats
+//     of the packets before it were updated (:116);
+//   * PAYLOAD (std::regex) and CUSTOM (std::function) filters are evaluated here on
+//     the host, with the reference's semantics, for the packets that reach them.
+// processingTime is the amortised batch time (the reference's value is a wall clock).
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "beatrice/PacketFilter.hpp"
+#include "beatrice_gpu.h"
+
+namespace beatrice {
+namespace gpu {
+
+class GpuPacketFilter {
+public:
+    using FilterType = beatrice::PacketFilter::FilterType;
+    using FilterConfig = beatrice::PacketFilter::FilterConfig;
+    using FilterResult = beatrice::PacketFilter::FilterResult;
+    using FilterStats = beatrice::PacketFilter::FilterStats;
+
+    // Throws std::runtime_error when no MI355X is available (no CPU fallback).
+    explicit GpuPacketFilter(int device = 0, const bt_opts* opts = nullptr);
+    ~GpuPacketFilter();
+    GpuPacketFilter(const GpuPacketFilter&) = delete;
+    GpuPacketFilter& operator=(const GpuPacketFilter&) = delete;
+
+    Result<void> addFilter(const std::string& name, const FilterConfig& config);
+    Result<void> removeFilter(const std::string& name);
+    Result<void> setFilterEnabled(const std::string& name, bool enabled);
+    FilterResult applyFilters(const Packet& packet);
+    std::vector<FilterResult> applyFilters(const std::vector<Packet>& packets);
+    std::vector<std::string> getActiveFilters() const;
+    FilterStats getStats() const;
+    void resetStats();
+    Result<void> setCustomFilter(const std::string& name, std::function<bool(const Packet&)> filterFunc);
+
+    // GPU-native batch form: decision bytes (BT_DECIDE_*) with host-side filters already
+    // resolved, plus the ordered indices of passing packets. Updates stats like
+    // applyFilters; throws like it.
+    struct Verdicts {
+        std::vector<uint8_t> decide;     // (code << 6) | slot
+        std::vector<uint32_t> pass_idx;  // ascending
+    };
+    Verdicts classify(const std::vector<Packet>& packets);
+
+    // Evaluation order of the enabled filters (names), as applyFilters uses it.
+    std::vector<std::string> evaluationOrder();
+    bt_ctx* context() const { return ctx_; }
+
+private:
+    struct FilterEntry {
+        FilterConfig config;
+        std::function<bool(const Packet&)> customFunc;
+    };
+    struct Slot {
+        std::string name;
+        FilterEntry* entry;
+        bt_filter_slot compiled;
+    };
+
+    void compileLocked();
+    // host continuation for packets the device left at a PAYLOAD/CUSTOM slot
+    uint32_t resolveHost(const Packet& p, uint32_t first_slot);
+    [[noreturn]] void rethrow(const Slot& s) const;
+    void runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide);
+    void updateStats(const std::string& filterName, bool passed, std::chrono::microseconds t);
+
+    bt_ctx* ctx_ = nullptr;
+    std::unordered_map<std::string, FilterEntry> filters_;
+    mutable std::mutex filtersMutex_;
+    FilterStats stats_;
+    mutable std::mutex statsMutex_;
+    bool dirty_ = true;
+    std::vector<Slot> program_;
+};
+
+}  // namespace gpu
+}  // namespace beatrice

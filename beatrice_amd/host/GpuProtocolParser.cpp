@@ -1,0 +1,243 @@
+// GpuProtocolParser.cpp — see GpuProtocolParser.hpp. The per-protocol field lists
+// (names, order, types) follow the reference builtin tables
+// src/parser/ProtocolRegistry.cpp:150-234/289-297; FieldValue contents follow
+// src/parser/ProtocolParser.cpp:286-383 (rawHex, formatted addresses) and the
+// ParseResult header fields :238-284.
+#include "GpuProtocolParser.hpp"
+
+#include <cstring>
+#include <sstream>
+#include <stdexcept>
+
+namespace beatrice {
+namespace gpu {
+
+using parser::FieldValue;
+using parser::FieldValueType;
+using parser::ParseResult;
+using parser::ParseStatus;
+
+namespace {
+
+enum Kind { U8, U16, U32, BYTES, IPV4, IPV6 };
+
+struct Field {
+    const char* name;
+    Kind kind;
+    uint32_t rec_off;   // position in bt_rec
+    uint32_t len;       // field length (bytes)
+};
+
+struct Table {
+    const char* name;
+    const char* version;
+    uint32_t total;     // ProtocolDefinition::getTotalLength()
+    std::vector<Field> fields;
+};
+
+const Table kEth{"ethernet", "2.0", 14,
+                 {{"destination_mac", BYTES, 0, 6}, {"source_mac", BYTES, 6, 6}, {"ethertype", U16, 12, 2}}};
+const Table kVlan{"vlan", "1.0", 4, {{"tpid", U16, 16, 2}, {"tci", U16, 20, 2}}};
+const Table kIpv4{"ipv4", "4.0", 20,
+                  {{"version", U8, 28, 1}, {"ihl", U8, 29, 1}, {"tos", U8, 30, 1}, {"total_length", U16, 34, 2},
+                   {"identification", U16, 36, 2}, {"flags", U16, 38, 2}, {"ttl", U8, 31, 1},
+                   {"protocol", U8, 32, 1}, {"checksum", U16, 40, 2}, {"source_ip", IPV4, 44, 4},
+                   {"destination_ip", IPV4, 48, 4}}};
+const Table kIpv6{"ipv6", "6.0", 40,
+                  {{"version_traffic_class_flow_label", U32, 28, 4}, {"payload_length", U16, 32, 2},
+                   {"next_header", U8, 34, 1}, {"hop_limit", U8, 35, 1}, {"source_ip", IPV6, 36, 16},
+                   {"destination_ip", IPV6, 52, 16}}};
+const Table kTcp{"tcp", "1.0", 20,
+                 {{"source_port", U16, 68, 2}, {"destination_port", U16, 70, 2}, {"sequence_number", U32, 72, 4},
+                  {"acknowledgment_number", U32, 76, 4}, {"data_offset", U8, 80, 1}, {"flags", U8, 81, 1},
+                  {"window_size", U16, 82, 2}, {"checksum", U16, 84, 2}, {"urgent_pointer", U16, 86, 2}}};
+const Table kUdp{"udp", "1.0", 8,
+                 {{"source_port", U16, 68, 2}, {"destination_port", U16, 70, 2}, {"length", U16, 72, 2},
+                  {"checksum", U16, 74, 2}}};
+const Table kIcmp{"icmp", "1.0", 8,
+                  {{"type", U8, 68, 1}, {"code", U8, 69, 1}, {"checksum", U16, 70, 2}, {"identifier", U16, 72, 2},
+                   {"sequence_number", U16, 74, 2}}};
+
+std::string hex(const uint8_t* b, size_t n) {   // ProtocolParser::bytesToHex (:591-597)
+    static const char* d = "0123456789abcdef";
+    std::string s(2 * n, '0');
+    for (size_t i = 0; i < n; ++i) {
+        s[2 * i] = d[b[i] >> 4];
+        s[2 * i + 1] = d[b[i] & 15];
+    }
+    return s;
+}
+
+std::string fmt_ipv4(const uint8_t* b) {        // :610-619
+    return std::to_string(b[0]) + "." + std::to_string(b[1]) + "." + std::to_string(b[2]) + "." + std::to_string(b[3]);
+}
+
+std::string fmt_ipv6(const uint8_t* b) {        // :621-631
+    std::stringstream ss;
+    for (size_t i = 0; i < 16; i += 2) {
+        if (i > 0) ss << ":";
+        uint16_t v = (uint16_t)((b[i] << 8) | b[i + 1]);
+        ss << std::hex << v;
+    }
+    return ss.str();
+}
+
+FieldValue make_field(const bt_rec& r, const Field& f, uint32_t bias) {
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(&r) + f.rec_off + bias;
+    FieldValue v;
+    v.valid = true;
+    uint8_t wire[16];
+    switch (f.kind) {
+    case U8:
+        v.type = FieldValueType::UINT8;
+        v.value = rb[0];
+        wire[0] = rb[0];
+        break;
+    case U16: {
+        uint16_t x;
+        std::memcpy(&x, rb, 2);
+        v.type = FieldValueType::UINT16;
+        v.value = x;
+        wire[0] = (uint8_t)(x >> 8);
+        wire[1] = (uint8_t)x;
+        break;
+    }
+    case U32: {
+        uint32_t x;
+        std::memcpy(&x, rb, 4);
+        v.type = FieldValueType::UINT32;
+        v.value = x;
+        for (int k = 0; k < 4; ++k) wire[k] = (uint8_t)(x >> (24 - 8 * k));
+        break;
+    }
+    case BYTES:
+        v.type = FieldValueType::BYTES;
+        v.value = std::vector<uint8_t>(rb, rb + f.len);
+        std::memcpy(wire, rb, f.len);
+        break;
+    case IPV4:
+        v.type = FieldValueType::IPV4_ADDRESS;
+        v.value = std::vector<uint8_t>(rb, rb + 4);
+        v.formatted = fmt_ipv4(rb);
+        std::memcpy(wire, rb, 4);
+        break;
+    case IPV6:
+        v.type = FieldValueType::IPV6_ADDRESS;
+        v.value = std::vector<uint8_t>(rb, rb + 16);
+        v.formatted = fmt_ipv6(rb);
+        std::memcpy(wire, rb, 16);
+        break;
+    }
+    v.rawHex = hex(wire, f.len);
+    return v;
+}
+
+const Table* table_of(const std::string& name) {
+    if (name == "ethernet") return &kEth;
+    if (name == "vlan") return &kVlan;
+    if (name == "ipv4") return &kIpv4;
+    if (name == "ipv6") return &kIpv6;
+    if (name == "tcp") return &kTcp;
+    if (name == "udp") return &kUdp;
+    if (name == "icmp") return &kIcmp;
+    return nullptr;
+}
+
+uint32_t bit_of(const std::string& name, int tag) {
+    if (name == "ethernet") return BT_L_ETH;
+    if (name == "vlan") return tag == 1 ? BT_L_VLAN1 : BT_L_VLAN0;
+    if (name == "ipv4") return BT_L_IPV4;
+    if (name == "ipv6") return BT_L_IPV6;
+    if (name == "tcp") return BT_L_TCP;
+    if (name == "udp") return BT_L_UDP;
+    return BT_L_ICMP;
+}
+
+}  // namespace
+
+std::vector<WalkedLayer> GpuParsedBatch::layers(size_t i) const {
+    const bt_rec& r = recs_.at(i);
+    std::vector<WalkedLayer> out;
+    out.push_back({"ethernet", 0, -1});
+    if (r.present & BT_L_VLAN0) out.push_back({"vlan", 12, 0});
+    if (r.present & BT_L_VLAN1) out.push_back({"vlan", 16, 1});
+    if (r.present & BT_L_IPV4) out.push_back({"ipv4", r.l3_off, -1});
+    if (r.present & BT_L_IPV6) out.push_back({"ipv6", r.l3_off, -1});
+    if (r.present & BT_L_TCP) out.push_back({"tcp", r.l4_off, -1});
+    if (r.present & BT_L_UDP) out.push_back({"udp", r.l4_off, -1});
+    if (r.present & BT_L_ICMP) out.push_back({"icmp", r.l4_off, -1});
+    return out;
+}
+
+ParseResult GpuParsedBatch::layer(size_t i, size_t k) const {
+    const auto ls = layers(i);
+    const WalkedLayer& L = ls.at(k);
+    const Table& t = *table_of(L.name);
+    const bt_rec& r = recs_[i];
+    const uint8_t* f = frames_[i];
+    const size_t len = lens_[i];
+    ParseResult res;   // parsePacketInternal (:238-284)
+    res.protocolName = t.name;
+    res.protocolVersion = t.version;
+    res.rawData.assign(f + L.offset, f + len);
+    res.packetLength = len - L.offset;
+    res.parsedBytes = 0;
+    if (!(r.ok & bit_of(L.name, L.tag))) {
+        res.status = ParseStatus::PACKET_TOO_SHORT;
+        res.errorMessage = "Packet too short for protocol";
+        return res;
+    }
+    const uint32_t bias = L.tag == 1 ? 2u : 0u;
+    for (const Field& fd : t.fields) res.fields[fd.name] = make_field(r, fd, bias);
+    res.parsedBytes = t.total;
+    return res;
+}
+
+ParseResult GpuParsedBatch::layer(size_t i, const std::string& name) const {
+    const auto ls = layers(i);
+    for (size_t k = 0; k < ls.size(); ++k)
+        if (ls[k].name == name) return layer(i, k);
+    ParseResult res;   // parsePacket with an unknown / absent protocol (:76-81)
+    res.status = ParseStatus::PROTOCOL_NOT_FOUND;
+    res.errorMessage = "Protocol not found: " + name;
+    return res;
+}
+
+GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts) {
+    if (bt_create(device, opts, &ctx_) != BT_OK)
+        throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+}
+
+GpuProtocolParser::~GpuProtocolParser() { bt_destroy(ctx_); }
+
+void GpuProtocolParser::run(GpuParsedBatch& b) {
+    const uint32_t n = (uint32_t)b.frames_.size();
+    b.recs_.resize(n);
+    if (n && bt_parse_filter_ptrs(ctx_, b.frames_.data(), b.lens_.data(), n, b.recs_.data(), nullptr, nullptr,
+                                  nullptr, nullptr) != BT_OK)
+        throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+}
+
+GpuParsedBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets) {
+    GpuParsedBatch b;
+    b.keep_ = packets;
+    for (const auto& p : b.keep_) {
+        b.frames_.push_back(p.data());
+        b.lens_.push_back((uint32_t)p.length());
+    }
+    run(b);
+    return b;
+}
+
+GpuParsedBatch GpuProtocolParser::parseBatch(const uint8_t* base, const bt_pkt_desc* desc, uint32_t n) {
+    GpuParsedBatch b;
+    for (uint32_t i = 0; i < n; ++i) {
+        b.frames_.push_back(base + BT_DESC_OFF(desc[i]));
+        b.lens_.push_back(BT_DESC_LEN(desc[i]));
+    }
+    run(b);
+    return b;
+}
+
+}  // namespace gpu
+}  // namespace beatrice

@@ -1,0 +1,64 @@
+// GpuProtocolParser.hpp — batch front end of the MI355X parse stage for callers of
+// beatrice::parser::ProtocolParser (reference include/parser/ProtocolParser.hpp:67).
+//
+// parseBatch() runs the whole layer walk (Ethernet, up to two VLAN tags, IPv4/IPv6,
+// TCP/UDP/ICMP — DESIGN.md "R-WALK") for every packet on the GPU and keeps the 96-B
+// bt_rec per packet. layer(i, k) materialises, on demand, the reference ParseResult of
+// the k-th walked layer of packet i: identical to
+//     ProtocolParser(cfg with enablePerformanceMetrics=false)
+//         .parsePacket(std::vector<uint8_t>(frame + offset, frame + len), name)
+// in every member except the wall-clock timings (parseTime / totalParseTime = 0).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "beatrice/Packet.hpp"
+#include "beatrice_gpu.h"
+#include "parser/ParserResult.hpp"
+
+namespace beatrice {
+namespace gpu {
+
+struct WalkedLayer {
+    std::string name;   // "ethernet", "vlan", "ipv4", "ipv6", "tcp", "udp", "icmp"
+    size_t offset;      // slice start in the frame
+    int tag;            // VLAN tag index (0/1), -1 otherwise
+};
+
+class GpuParsedBatch {
+public:
+    size_t size() const { return recs_.size(); }
+    const bt_rec& record(size_t i) const { return recs_[i]; }
+    std::vector<WalkedLayer> layers(size_t i) const;
+    parser::ParseResult layer(size_t i, size_t k) const;
+    // first walked layer called `name` (PROTOCOL_NOT_FOUND result when absent)
+    parser::ParseResult layer(size_t i, const std::string& name) const;
+
+private:
+    friend class GpuProtocolParser;
+    std::vector<bt_rec> recs_;
+    std::vector<const uint8_t*> frames_;
+    std::vector<uint32_t> lens_;
+    std::vector<Packet> keep_;   // owns the frames of a vector<Packet> batch
+};
+
+class GpuProtocolParser {
+public:
+    explicit GpuProtocolParser(int device = 0, const bt_opts* opts = nullptr);
+    ~GpuProtocolParser();
+    GpuProtocolParser(const GpuProtocolParser&) = delete;
+    GpuProtocolParser& operator=(const GpuProtocolParser&) = delete;
+
+    GpuParsedBatch parseBatch(const std::vector<Packet>& packets);
+    // borrows `base` for the lifetime of the returned batch
+    GpuParsedBatch parseBatch(const uint8_t* base, const bt_pkt_desc* desc, uint32_t n);
+
+private:
+    void run(GpuParsedBatch& b);
+    bt_ctx* ctx_ = nullptr;
+};
+
+}  // namespace gpu
+}  // namespace beatrice

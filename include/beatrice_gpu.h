@@ -221,6 +221,7 @@ typedef struct bt_opts {
 #define BT_OPT_NO_PREFETCH 0x1u    /* disable the next-tile load prefetch (A/B only)    */
 #define BT_OPT_TILE_BLOCKED 0x2u   /* one contiguous tile range per wavefront           */
 #define BT_OPT_RECORDS_AOS 0x4u    /* device records as bt_rec AoS instead of planes    */
+#define BT_OPT_GRAPH 0x8u          /* bt_time_device: replay the steps as one hipGraph  */
 
 typedef struct bt_batch {          /* device-resident input */
     const uint8_t* base;           /* packet bytes                                      */
@@ -271,6 +272,13 @@ int  bt_parse_filter(bt_ctx* ctx, const uint8_t* base, const bt_pkt_desc* desc, 
                      bt_rec* records, uint64_t* verdict, uint8_t* decide,
                      uint32_t* pass_idx, uint32_t* n_pass);
 
+/* The same over a gather list — one pointer + length per frame, e.g. the buffers of a
+ * std::vector<beatrice::Packet> (reference include/beatrice/Packet.hpp:145-211). Only
+ * the first min(len, 112) bytes of each frame are staged for the device. */
+int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                          bt_rec* records, uint64_t* verdict, uint8_t* decide,
+                          uint32_t* pass_idx, uint32_t* n_pass);
+
 /* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
 int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);
 int  bt_dev_free(bt_ctx* ctx, void* p);
@@ -278,7 +286,11 @@ int  bt_memcpy_h2d(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
 int  bt_synchronize(bt_ctx* ctx);
-/* events on the context stream for timing a device-resident run */
+/* Timing of a device-resident run on the context stream: `iters` steps, each = the
+ * main kernel between an event pair + the compaction kernels; returns the event span
+ * per step and the mean main-kernel time. With BT_OPT_GRAPH the steps are captured
+ * once into a hipGraph (first call per (batch, outputs, iters)) and replayed, and
+ * main_ms is -1 (HIP does not time events recorded inside a graph). */
 int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
                     uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
 

@@ -1,0 +1,273 @@
+// test_adapter.cpp — GPU parity of the C++ drop-in layer against the reference itself.
+//
+// Links the reference's own parser + PacketFilter objects (oracle/_ref/obj, compiled
+// from the unmodified sources by oracle/Makefile — test infrastructure) next to
+// libbeatrice_gpu_host.so, and runs both on the same synthetic captures:
+//   filters  GpuPacketFilter vs beatrice::PacketFilter: every FilterResult (passed,
+//            filterName, reason), the stats, getActiveFilters, the exception thrown —
+//            including equal-priority ties, PAYLOAD regex, CUSTOM callbacks, removal.
+//   parser   GpuProtocolParser::layer(i, k) vs ProtocolParser::parsePacket(slice, name)
+//            for every walked layer: every ParseResult member but the wall-clock times,
+//            field iteration order included.
+//   plugin   dlopen of libgpu_parse_filter_plugin.so through createPlugin(), the
+//            IPacketPlugin lifecycle, pass count vs the reference.
+// Prints one line per check; exit status 0 = all passed.
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "beatrice/IPacketPlugin.hpp"
+#include "beatrice/PacketFilter.hpp"
+#include "parser/ProtocolParser.hpp"
+#include "parser/ProtocolRegistry.hpp"
+#include "../../beatrice_amd/host/GpuPacketFilter.hpp"
+#include "../../beatrice_amd/host/GpuProtocolParser.hpp"
+
+extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
+extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
+
+using beatrice::Packet;
+using beatrice::PacketFilter;
+using beatrice::gpu::GpuPacketFilter;
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                                  \
+    do {                                                                  \
+        if (!(cond)) {                                                    \
+            ++g_fail;                                                     \
+            std::printf("FAIL %s:%d: ", __FILE__, __LINE__);              \
+            std::printf(__VA_ARGS__);                                     \
+            std::printf("\n");                                            \
+            return false;                                                 \
+        }                                                                 \
+    } while (0)
+
+struct Capture {
+    std::vector<uint8_t> data;
+    std::vector<uint64_t> desc;
+    std::vector<Packet> packets;
+};
+
+static Capture capture(int cfg, uint32_t n, uint64_t seed) {
+    Capture c;
+    c.desc.resize(n);
+    c.data.resize(bt_synth_layout(cfg, n, seed, c.desc.data()));
+    bt_synth_fill(cfg, n, seed, c.desc.data(), c.data.data(), 8);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* f = c.data.data() + (c.desc[i] & 0xFFFFFFFFFFFFull);
+        c.packets.emplace_back(std::shared_ptr<const uint8_t[]>(f, [](const uint8_t*) {}), (size_t)(c.desc[i] >> 48));
+    }
+    return c;
+}
+
+struct Spec {
+    std::string name;
+    PacketFilter::FilterType type;
+    std::string expr;
+    int priority;
+    bool enabled;
+    int custom;   // 0 none, 1 len % 3 != 0, 2 len >= 100, 3 throws
+};
+
+static std::function<bool(const Packet&)> custom_fn(int id) {
+    switch (id) {
+    case 1: return [](const Packet& p) { return p.length() % 3 != 0; };
+    case 2: return [](const Packet& p) { return p.length() >= 100; };
+    default: return [](const Packet& p) -> bool {
+        if (p.length() == 777) throw std::runtime_error("custom boom");
+        return true;
+    };
+    }
+}
+
+template <class F>
+static void install(F& f, const std::vector<Spec>& specs) {
+    for (const auto& s : specs) {
+        PacketFilter::FilterConfig c;
+        c.type = s.type;
+        c.expression = s.expr;
+        c.priority = s.priority;
+        c.enabled = s.enabled;
+        f.addFilter(s.name, c);
+        if (s.custom) f.setCustomFilter(s.name, custom_fn(s.custom));
+    }
+}
+
+static std::string what_kind(const std::exception_ptr& e) {
+    try {
+        std::rethrow_exception(e);
+    } catch (const std::invalid_argument& x) {
+        return std::string("invalid_argument:") + x.what();
+    } catch (const std::out_of_range& x) {
+        return std::string("out_of_range:") + x.what();
+    } catch (const std::exception& x) {
+        return std::string("exception:") + x.what();
+    }
+}
+
+static bool filter_case(const char* label, const Capture& cap, const std::vector<Spec>& specs,
+                        const std::vector<std::string>& remove = {}) {
+    PacketFilter ref;
+    GpuPacketFilter gpu(0);
+    install(ref, specs);
+    install(gpu, specs);
+    for (const auto& r : remove) {
+        ref.removeFilter(r);
+        gpu.removeFilter(r);
+    }
+    CHECK(ref.getActiveFilters() == gpu.getActiveFilters(), "%s: active filter lists differ", label);
+    std::vector<PacketFilter::FilterResult> a, b;
+    std::exception_ptr ea, eb;
+    try { a = ref.applyFilters(cap.packets); } catch (...) { ea = std::current_exception(); }
+    try { b = gpu.applyFilters(cap.packets); } catch (...) { eb = std::current_exception(); }
+    CHECK((bool)ea == (bool)eb, "%s: exception mismatch ref=%d gpu=%d", label, (bool)ea, (bool)eb);
+    if (ea) {
+        CHECK(what_kind(ea) == what_kind(eb), "%s: %s vs %s", label, what_kind(ea).c_str(), what_kind(eb).c_str());
+    } else {
+        CHECK(a.size() == b.size(), "%s: result counts", label);
+        for (size_t i = 0; i < a.size(); ++i) {
+            CHECK(a[i].passed == b[i].passed && a[i].filterName == b[i].filterName && a[i].reason == b[i].reason,
+                  "%s: packet %zu ref=(%d,%s,%s) gpu=(%d,%s,%s)", label, i, a[i].passed, a[i].filterName.c_str(),
+                  a[i].reason.c_str(), b[i].passed, b[i].filterName.c_str(), b[i].reason.c_str());
+        }
+    }
+    auto sa = ref.getStats(), sb = gpu.getStats();
+    CHECK(sa.packetsProcessed == sb.packetsProcessed && sa.packetsPassed == sb.packetsPassed &&
+              sa.packetsDropped == sb.packetsDropped && sa.filterCounts == sb.filterCounts,
+          "%s: stats differ (processed %lu/%lu passed %lu/%lu)", label, (unsigned long)sa.packetsProcessed,
+          (unsigned long)sb.packetsProcessed, (unsigned long)sa.packetsPassed, (unsigned long)sb.packetsPassed);
+    std::printf("ok   filters %-22s %zu packets, %lu passed%s\n", label, cap.packets.size(),
+                (unsigned long)sa.packetsPassed, ea ? (" (threw " + what_kind(ea) + ")").c_str() : "");
+    return true;
+}
+
+static bool same_field(const beatrice::parser::FieldValue& x, const beatrice::parser::FieldValue& y) {
+    return x.value == y.value && x.type == y.type && x.rawHex == y.rawHex && x.formatted == y.formatted &&
+           x.valid == y.valid && x.errorMessage == y.errorMessage;
+}
+
+static bool parser_case(const char* label, const Capture& cap) {
+    using namespace beatrice::parser;
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    ProtocolParser ref(cfg);
+    for (auto p : {BuiltinProtocols::createEthernetProtocol(), BuiltinProtocols::createVLANProtocol(),
+                   BuiltinProtocols::createIPv4Protocol(), BuiltinProtocols::createIPv6Protocol(),
+                   BuiltinProtocols::createTCPProtocol(), BuiltinProtocols::createUDPProtocol(),
+                   BuiltinProtocols::createICMPProtocol()})
+        ref.registerProtocol(p);
+    beatrice::gpu::GpuProtocolParser gpu(0);
+    auto batch = gpu.parseBatch(cap.packets);
+    size_t nlayers = 0;
+    for (size_t i = 0; i < cap.packets.size(); ++i) {
+        const uint8_t* f = cap.packets[i].data();
+        const size_t len = cap.packets[i].length();
+        auto ls = batch.layers(i);
+        for (size_t k = 0; k < ls.size(); ++k) {
+            ParseResult want = ref.parsePacket(std::vector<uint8_t>(f + ls[k].offset, f + len), ls[k].name);
+            ParseResult got = batch.layer(i, k);
+            ++nlayers;
+            CHECK(want.status == got.status && want.protocolName == got.protocolName &&
+                      want.protocolVersion == got.protocolVersion && want.errorMessage == got.errorMessage &&
+                      want.packetLength == got.packetLength && want.parsedBytes == got.parsedBytes &&
+                      want.rawData == got.rawData && want.validationResults.size() == got.validationResults.size(),
+                  "%s: packet %zu layer %s header differs (status %d/%d)", label, i, ls[k].name.c_str(),
+                  (int)want.status, (int)got.status);
+            std::vector<std::string> ka, kb;
+            for (const auto& [n, v] : want.fields) ka.push_back(n);
+            for (const auto& [n, v] : got.fields) kb.push_back(n);
+            CHECK(ka == kb, "%s: packet %zu layer %s field order differs", label, i, ls[k].name.c_str());
+            for (const auto& [n, v] : want.fields)
+                CHECK(same_field(v, got.fields.at(n)), "%s: packet %zu %s.%s differs", label, i, ls[k].name.c_str(),
+                      n.c_str());
+        }
+    }
+    std::printf("ok   parser  %-22s %zu packets, %zu layer results\n", label, cap.packets.size(), nlayers);
+    return true;
+}
+
+static bool plugin_case(const Capture& cap, const char* so) {
+    setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|3|udp;net|IP_RANGE|2|10.0.0.0/8;ports|PORT_RANGE|1|1000-2000", 1);
+    setenv("BEATRICE_GPU_BATCH", "4096", 1);
+    setenv("BEATRICE_GPU_FLUSH_US", "100000000", 1);
+    void* h = dlopen(so, RTLD_LAZY);   // PluginManager::loadPlugin (src/PluginManager.cpp:57-79)
+    CHECK(h, "dlopen %s: %s", so, dlerror());
+    using CreateFunc = beatrice::IPacketPlugin* (*)();
+    auto create = reinterpret_cast<CreateFunc>(dlsym(h, "createPlugin"));
+    auto flush = reinterpret_cast<void (*)(beatrice::IPacketPlugin*)>(dlsym(h, "gpu_plugin_flush"));
+    auto passed = reinterpret_cast<uint64_t (*)(const beatrice::IPacketPlugin*)>(dlsym(h, "gpu_plugin_passed"));
+    CHECK(create && flush && passed, "plugin symbols missing");
+    std::unique_ptr<beatrice::IPacketPlugin> p(create());
+    p->onStart();
+    for (const auto& pk : cap.packets) p->onPacket(const_cast<Packet&>(pk));
+    flush(p.get());
+    PacketFilter ref;
+    install(ref, {{"proto", PacketFilter::FilterType::PROTOCOL, "udp", 3, true, 0},
+                  {"net", PacketFilter::FilterType::IP_RANGE, "10.0.0.0/8", 2, true, 0},
+                  {"ports", PacketFilter::FilterType::PORT_RANGE, "1000-2000", 1, true, 0}});
+    uint64_t want = 0;
+    for (const auto& pk : cap.packets) want += ref.applyFilters(pk).passed;
+    CHECK(p->getProcessedPacketCount() == cap.packets.size(), "plugin processed %lu",
+          (unsigned long)p->getProcessedPacketCount());
+    CHECK(passed(p.get()) == want, "plugin passed %lu, reference %lu", (unsigned long)passed(p.get()),
+          (unsigned long)want);
+    CHECK(p->getName() == "gpu_parse_filter" && p->getErrorCount() == 0, "plugin identity/errors");
+    p->onStop();
+    p.reset();
+    dlclose(h);
+    std::printf("ok   plugin  createPlugin/onStart/onPacket x%zu/onStop, %lu passed\n", cap.packets.size(),
+                (unsigned long)want);
+    return true;
+}
+
+int main(int argc, char** argv) {
+    const char* plugin_so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
+    using T = PacketFilter::FilterType;
+    Capture c3 = capture(3, 20000, 0x5EED0003), c4 = capture(4, 12000, 0x5EED0004), fz = capture(9, 30000, 0x5EED0009);
+    const std::vector<Spec> headline = {{"proto", T::PROTOCOL, "udp", 3, true, 0},
+                                        {"net", T::IP_RANGE, "10.0.0.0/8", 2, true, 0},
+                                        {"ports", T::PORT_RANGE, "1000-2000", 1, true, 0}};
+    // equal priorities: the order comes from unordered_map iteration + std::sort
+    const std::vector<Spec> ties = {{"a", T::PORT_RANGE, "0-1023", 1, true, 0},
+                                    {"zeta", T::BPF, "tcp", 1, true, 0},
+                                    {"m7", T::IP_RANGE, "10.0.0.0/9", 1, true, 0},
+                                    {"q", T::PROTOCOL, "ip", 1, true, 0},
+                                    {"beta", T::IP_RANGE, "192.168.0.0/17", 1, true, 0},
+                                    {"k2", T::PORT_RANGE, "0-30000", 1, true, 0},
+                                    {"off", T::BPF, "udp", 1, false, 0},
+                                    {"hi", T::BPF, "udp tcp", 5, true, 0}};
+    const std::vector<Spec> host_side = {{"tcp", T::PROTOCOL, "tcp", 3, true, 0},
+                                         {"get", T::PAYLOAD, "GET|HTTP", 2, true, 0},
+                                         {"cust", T::CUSTOM, "", 2, true, 1},
+                                         {"ports", T::PORT_RANGE, "0-2047", 1, true, 0},
+                                         {"nofn", T::CUSTOM, "x", 0, true, 0}};
+    const std::vector<Spec> throws = {{"udp", T::BPF, "udp", 2, true, 0}, {"bad", T::IP_RANGE, "10.0.0.0/x", 1, true, 0}};
+    const std::vector<Spec> throws_late = {{"tcp", T::PROTOCOL, "tcp", 9, true, 0},
+                                           {"p", T::PORT_RANGE, "1000-2000", 5, true, 0},
+                                           {"oor", T::PORT_RANGE, "99999999999", 1, true, 0}};
+    const std::vector<Spec> custom_throw = {{"c", T::CUSTOM, "", 1, true, 3}};
+    bool ok = true;
+    ok &= filter_case("c3/headline", c3, headline);
+    ok &= filter_case("c4/headline", c4, headline);
+    ok &= filter_case("fuzz/headline", fz, headline);
+    ok &= filter_case("fuzz/ties", fz, ties);
+    ok &= filter_case("c3/ties-removed", c3, ties, {"m7", "q"});
+    ok &= filter_case("fuzz/payload+custom", fz, host_side);
+    ok &= filter_case("c4/payload+custom", c4, host_side);
+    ok &= filter_case("fuzz/throw", fz, throws);
+    ok &= filter_case("c3/throw-late", c3, throws_late);
+    ok &= filter_case("c4/custom-throw", c4, custom_throw);
+    ok &= filter_case("c3/no-filters", c3, {});
+    ok &= parser_case("c3", c3);
+    ok &= parser_case("c4", c4);
+    ok &= parser_case("fuzz", fz);
+    ok &= plugin_case(c3, plugin_so);
+    std::printf("%s (%d failures)\n", ok && !g_fail ? "ALL OK" : "FAILED", g_fail);
+    return ok && !g_fail ? 0 : 1;
+}

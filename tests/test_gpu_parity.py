@@ -166,3 +166,25 @@ def test_too_many_filters(gpu_ctx):
         gpu_ctx.compile(fs)
     prog = gpu_ctx.compile(fs[:64])
     assert len(prog) == 64 and prog[0].source_index == 63
+
+
+def test_graph_replay_outputs(gpu_ctx):
+    """BT_OPT_GRAPH: the timed steps replayed as one hipGraph produce the same outputs."""
+    n = 200003
+    data, desc = synth.capture(synth.C3, n, seed=99)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    ctx = abi.Context(0, flags=abi.OPT_GRAPH)
+    try:
+        ctx.compile(filters)
+        r = abi.DeviceRun(ctx, data, desc, n)
+        span, main = ctx.time_device(r.batch, r.outs, 3)    # builds the graph
+        span2, main2 = ctx.time_device(r.batch, r.outs, 3)  # replays it
+        assert main == -1.0 and main2 == -1.0 and span2 > 0
+        out = r.fetch()
+        r.free()
+    finally:
+        ctx.close()
+    rec, dec, npass = ol.oracle_run(data, desc, n, filters)
+    assert np.array_equal(out["records"], rec) and np.array_equal(out["decide"], dec)
+    check_filter_outputs(out, n)
