@@ -53,13 +53,15 @@ class FilterSlot(ctypes.Structure):
 
 class Opts(ctypes.Structure):
     _fields_ = [("host_chunk_packets", ctypes.c_uint32), ("host_chunk_bytes", ctypes.c_uint32),
-                ("grid_waves", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 4)]
+                ("grid_waves", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("host_threads", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 3)]
 
 
 OPT_NO_PREFETCH = 0x1
 OPT_TILE_BLOCKED = 0x2
 OPT_RECORDS_AOS = 0x4
 OPT_GRAPH = 0x8
+OPT_RECORDS_PLANES = 0x10
 
 
 class Batch(ctypes.Structure):
@@ -76,7 +78,7 @@ EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_record_gather",
+    "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
 ]
 
 _lib = None
@@ -114,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "bt_time_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
+        "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -193,8 +196,10 @@ class DeviceBuffer:
 class Context:
     """One bt_ctx on one device."""
 
-    def __init__(self, device: int = 0, host_chunk_packets: int = 0, grid_waves: int = 0, flags: int = 0):
+    def __init__(self, device: int = 0, host_chunk_packets: int = 0, grid_waves: int = 0, flags: int = 0,
+                 host_threads: int = 0):
         opts = Opts()
+        opts.host_threads = host_threads
         opts.host_chunk_packets = host_chunk_packets
         opts.grid_waves = grid_waves
         opts.flags = flags
@@ -202,6 +207,7 @@ class Context:
         _check(lib().bt_create(device, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h.value
         self.device = device
+        self.flags = flags
 
     def close(self):
         if self.h:
@@ -262,6 +268,16 @@ class Context:
         return out
 
 
+def untile_records(buf: np.ndarray, n: int, planes: bool = False) -> np.ndarray:
+    """bt_rec[n] (AoS) from the device record layout (include/beatrice_gpu.h)."""
+    if planes:
+        p = buf[: 6 * n * 16].reshape(6, n, 16)
+        return np.ascontiguousarray(p.transpose(1, 0, 2)).reshape(n, 96)
+    nt = (n + 63) // 64
+    t = buf[: nt * 6144].reshape(nt, 6, 64, 16)
+    return np.ascontiguousarray(t.transpose(0, 2, 1, 3)).reshape(nt * 64, 96)[:n]
+
+
 class DeviceRun:
     """Device-resident batch + outputs (the bench / parity path)."""
 
@@ -277,7 +293,7 @@ class DeviceRun:
         self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n,
                            int(data.nbytes))
         nt = (n + 63) // 64
-        self.d_rec = ctx.alloc(max(16, n * BT_REC_BYTES)) if records else None
+        self.d_rec = ctx.alloc(max(16, nt * 64 * BT_REC_BYTES)) if records else None
         self.d_dec = ctx.alloc(max(16, n)) if decide else None
         self.d_ver = ctx.alloc(max(16, nt * 8)) if verdict else None
         self.d_pidx = ctx.alloc(max(16, n * 4)) if pass_idx else None
@@ -297,9 +313,8 @@ class DeviceRun:
         out = {}
         self.ctx.synchronize()
         if self.d_rec:
-            planes = np.zeros((6, n, 16), dtype=np.uint8)
-            self.d_rec.download(planes.reshape(-1))
-            out["records"] = np.ascontiguousarray(planes.transpose(1, 0, 2)).reshape(n, 96)
+            out["records"] = untile_records(self.d_rec.download(np.zeros(self.d_rec.nbytes, np.uint8)), n,
+                                            planes=bool(self.ctx.flags & OPT_RECORDS_PLANES))
         if self.d_dec:
             out["decide"] = self.d_dec.download(np.zeros(n, dtype=np.uint8))
         if self.d_ver:

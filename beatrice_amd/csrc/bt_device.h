@@ -43,7 +43,7 @@ constexpr uint32_t kNeedParse = 102;              // 14 + 2*4 + 60 (IPv4 max) + 
 constexpr uint32_t kNeedFilter = 38;              // PacketFilter reads bytes 12..37
 
 // Launch wrappers (bt_kernels.hip). All are asynchronous on `stream`.
-enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2 };
+enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2, kRecTiled = 3 };
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
                 int grid_blocks, bool prefetch, void* stream);
 int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,

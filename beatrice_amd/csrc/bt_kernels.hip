@@ -180,17 +180,22 @@ __device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_
 //  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
 //  descriptors:  round A = the first 64 B (chunks 0..3) of every packet's 16-B-aligned
 //                window, 4 lanes per packet, 16 packets per wave instruction.
+//                "wide" (wave-adaptive): chunks 4..7 in the same round, for waves whose
+//                previous tile mostly needed them (QinQ / IPv6 / IP options): one round
+//                trip, and no second fetch of lines L2 evicted between two rounds.
 template <int FIXED_LOG2>
 struct Stage {
-    static constexpr int kV = FIXED_LOG2 >= 0 ? (1 << (FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0)) : 4;
+    static constexpr int kV = FIXED_LOG2 >= 0 ? (1 << (FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0)) : 8;
     uint4 v[kV];
     uint64_t qa0[FIXED_LOG2 >= 0 ? 1 : 4];   // aligned window base of packet j*16 + lane/4
     uint64_t off;                             // this lane's own packet
     uint32_t len;
+    bool wide;
 };
 
 template <int FIXED_LOG2>
-__device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint32_t lane, Stage<FIXED_LOG2>& st) {
+__device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint32_t lane, Stage<FIXED_LOG2>& st,
+                                            bool wide, uint32_t need_max) {
     const uint32_t p0 = t * 64u;
     const uint32_t my = p0 + lane;
     const bool live = my < a.n;
@@ -217,6 +222,7 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
         }
         const uint32_t off_lo = (uint32_t)st.off, off_hi = (uint32_t)(st.off >> 32);
         const uint32_t c = lane & 3u;
+        st.wide = wide;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t q = j * 16u + (lane >> 2);
@@ -225,9 +231,16 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
             const uint32_t ql = (uint32_t)__shfl((int)st.len, (int)q);
             const uint64_t a0 = qo & ~15ull;
             const uint64_t addr = a0 + 16u * c;
+            const uint32_t sq = (uint32_t)qo & 15u;
             st.qa0[j] = a0;
-            const bool ok = (p0 + q < a.n) && (16u * c < ((uint32_t)qo & 15u) + ql) && (addr + 16u <= a.bytes);
+            const bool live_q = p0 + q < a.n;
+            const bool ok = live_q && (16u * c < sq + ql) && (addr + 16u <= a.bytes);
             st.v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+            if (wide) {   // chunks 4..7 up to the longest header the walk can read
+                const uint32_t nq = ql < need_max ? ql : need_max;
+                const bool okb = live_q && (16u * (c + 4u) < sq + nq) && (addr + 64u + 16u <= a.bytes);
+                st.v[4 + j] = okb ? *reinterpret_cast<const uint4*>(a.base + addr + 64u) : make_uint4(0, 0, 0, 0);
+            }
         }
     }
 }
@@ -248,6 +261,13 @@ __device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32
         for (uint32_t j = 0; j < 4; ++j) {
             uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + (lane & 3u) * 4u;
             dst[0] = st.v[j].x; dst[1] = st.v[j].y; dst[2] = st.v[j].z; dst[3] = st.v[j].w;
+        }
+        if (st.wide) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + 16u + (lane & 3u) * 4u;
+                dst[0] = st.v[4 + j].x; dst[1] = st.v[4 + j].y; dst[2] = st.v[4 + j].z; dst[3] = st.v[4 + j].w;
+            }
         }
     }
 }
@@ -315,15 +335,17 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         t_end = a.ntiles;
         step = total_waves;
     }
+    const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
+    bool wide = false;   // wave-uniform: previous tile mostly needed chunks 4..7
     Stage<FIXED_LOG2> st;
-    if (PREFETCH && t < t_end) issue_loads<FIXED_LOG2>(a, t, lane, st);
+    if (PREFETCH && t < t_end) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
     for (; t < t_end; t += step) {
         const uint32_t p0 = t * 64u;
         const uint32_t my = p0 + lane;
         const bool live = my < a.n;
 
         // ---- 1. LOAD (this tile's windows -> LDS; next tile's loads go in flight) ----
-        if (!PREFETCH) issue_loads<FIXED_LOG2>(a, t, lane, st);
+        if (!PREFETCH) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
         stage_to_lds<FIXED_LOG2>(st, img, lane);
         const uint64_t my_off = st.off;
         const uint32_t my_len = st.len;
@@ -331,16 +353,19 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 #pragma unroll
         for (int j = 0; j < (FIXED_LOG2 >= 0 ? 1 : 4); ++j) qa0[j] = st.qa0[j];
         wave_lds_sync();
-        if (PREFETCH && t + step < t_end) issue_loads<FIXED_LOG2>(a, t + step, lane, st);
+        const bool this_wide = FIXED_LOG2 < 0 && st.wide;
+        if (PREFETCH && t + step < t_end) issue_loads<FIXED_LOG2>(a, t + step, lane, st, wide, need_max);
         if constexpr (FIXED_LOG2 < 0) {
             if (REC != kRecNone) {   // filter-only needs <= 38 B: round A always suffices
                 const uint32_t s0 = (uint32_t)my_off & 15u;
                 const uint32_t end = live ? s0 + header_end(row, s0, my_len, FILTER ? kNeedFilter : 0u) : 0u;
                 const uint32_t my_need = end > 64u ? end : 0u;
-                if (__ballot(my_need != 0u) != 0ull) {
+                const uint64_t needs_b = __ballot(my_need != 0u);
+                if (!this_wide && needs_b != 0ull) {
                     load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_need, img);
                     wave_lds_sync();
                 }
+                wide = __popcll(needs_b) > 32;   // decides the wave's next issue
             }
         }
 
@@ -358,6 +383,12 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 #pragma unroll
                 for (int k = 0; k < BT_REC_SLABS; ++k)
                     planes[(uint64_t)k * a.n_cap + my] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
+            } else if (REC == kRecTiled) {
+                // [tile][slab][lane]: the tile's six 1-KiB slab stores land back to back
+                uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
+#pragma unroll
+                for (int k = 0; k < BT_REC_SLABS; ++k)
+                    tile[k * 64 + lane] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
             } else {
                 uint4* rec = reinterpret_cast<uint4*>(a.records + (uint64_t)my * BT_REC_BYTES);
 #pragma unroll
@@ -510,6 +541,8 @@ template <int FL>
 void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, bool pf, hipStream_t st) {
     if (rec == kRecPlanes) {
         if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, pf, st); else launch_t<FL, kRecPlanes, false>(a, prog, grid, pf, st);
+    } else if (rec == kRecTiled) {
+        if (f) launch_t<FL, kRecTiled, true>(a, prog, grid, pf, st); else launch_t<FL, kRecTiled, false>(a, prog, grid, pf, st);
     } else if (rec == kRecAoS) {
         if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, pf, st); else launch_t<FL, kRecAoS, false>(a, prog, grid, pf, st);
     } else {

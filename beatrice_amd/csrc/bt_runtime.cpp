@@ -8,6 +8,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -54,6 +57,67 @@ struct HostSlot {                      // one half of the double-buffered host p
     uint32_t lo = 0, cnt = 0;          // packet range of the chunk in flight
 };
 
+// Fixed pool of host threads for the host-batch pipeline's gather / drain copies.
+class HostPool {
+public:
+    explicit HostPool(unsigned n) {
+        for (unsigned i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+        nthreads_ = n ? n : 1;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned size() const { return nthreads_; }
+    // runs fn(worker) on every worker (the caller is worker 0) and waits
+    void run(const std::function<void(unsigned)>& fn) {
+        if (nthreads_ == 1) { fn(0); return; }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            pending_ = nthreads_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = fn_;
+            }
+            (*f)(id);
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    unsigned pending_ = 0, nthreads_ = 1;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 struct bt_ctx {
@@ -76,6 +140,7 @@ struct bt_ctx {
     uint32_t chunk = 0;
     HostSlot hs[2];
     bool host_ready = false;
+    std::unique_ptr<HostPool> pool;
 
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -135,7 +200,12 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
     a.tile_pass = compact ? c->tile_pass : nullptr;
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
-    const int rec = o->records ? ((aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) ? kRecAoS : kRecPlanes) : kRecNone;
+    int rec = kRecNone;
+    if (o->records) {
+        if (aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) rec = kRecAoS;
+        else if (c->opts.flags & BT_OPT_RECORDS_PLANES) rec = kRecPlanes;
+        else rec = kRecTiled;
+    }
     if (e0) HIP_TRY(hipEventRecord(e0, st));
     int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -170,6 +240,9 @@ int ensure_host(bt_ctx* c) {
     uint32_t chunk = c->opts.host_chunk_packets ? c->opts.host_chunk_packets : (1u << 20);
     chunk = (chunk + 63) / 64 * 64;
     c->chunk = chunk;
+    unsigned nt = c->opts.host_threads;
+    if (!nt) nt = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    c->pool = std::make_unique<HostPool>(std::min(nt, 16u));
     for (auto& s : c->hs) {
         HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -188,11 +261,17 @@ void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint
     const uint8_t* rec = s.h_out;
     const uint8_t* dec = s.h_out + (size_t)chunk * BT_REC_BYTES;
     const uint64_t* ver = reinterpret_cast<const uint64_t*>(dec + chunk);
-    if (records) std::memcpy(records + s.lo, rec, (size_t)s.cnt * BT_REC_BYTES);
-    if (decide) std::memcpy(decide + s.lo, dec, s.cnt);
-    if (verdict) {   // chunks are 64-aligned, so whole words line up
-        std::memcpy(verdict + s.lo / 64, ver, ((size_t)s.cnt + 63) / 64 * 8);
-    }
+    const unsigned T = c->pool->size();
+    const uint32_t lo = s.lo, cnt = s.cnt;
+    c->pool->run([&](unsigned w) {   // split on 64-packet boundaries
+        const uint32_t tiles = (cnt + 63) / 64;
+        const uint32_t t0 = (uint32_t)((uint64_t)tiles * w / T), t1 = (uint32_t)((uint64_t)tiles * (w + 1) / T);
+        const uint32_t a = t0 * 64, b = std::min(cnt, t1 * 64);
+        if (a >= b) return;
+        if (records) std::memcpy(records + lo + a, rec + (size_t)a * BT_REC_BYTES, (size_t)(b - a) * BT_REC_BYTES);
+        if (decide) std::memcpy(decide + lo + a, dec + a, b - a);
+        if (verdict) std::memcpy(verdict + (lo + a) / 64, ver + a / 64, (size_t)(t1 - t0) * 8);
+    });
     s.busy = false;
 }
 
@@ -241,6 +320,7 @@ void bt_destroy(bt_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     free_host(c);
+    c->pool.reset();
     if (c->tgraph) (void)hipGraphExecDestroy(c->tgraph);
     if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
     for (auto e : c->tev) (void)hipEventDestroy(e);
@@ -382,18 +462,37 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
         }
         if (next < n) {
             const uint32_t cnt = std::min(chunk, n - next);
-            // gather the header prefixes (<= kHostSlot bytes) into pinned staging
+            // gather the header prefixes (<= kHostSlot bytes) into pinned staging:
+            // per-worker byte counts, exclusive scan, then parallel copies
             uint8_t* pre = s.h_in;
             uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlot);
-            uint64_t pos = 0;
-            for (uint32_t i = 0; i < cnt; ++i) {
-                uint32_t len = 0;
-                const uint8_t* f = frame(next + i, &len);
-                const uint32_t m = std::min(len, kHostSlot);
-                if (m) std::memcpy(pre + pos, f, m);
-                d[i] = BT_DESC(pos, len);
-                pos += (m + 15) & ~15u;
-            }
+            const unsigned T = c->pool->size();
+            std::vector<uint64_t> part(T + 1, 0);
+            const uint32_t base_i = next;
+            c->pool->run([&](unsigned w) {
+                const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
+                uint64_t sum = 0;
+                for (uint32_t i = a; i < b; ++i) {
+                    uint32_t len = 0;
+                    (void)frame(base_i + i, &len);
+                    sum += (std::min(len, kHostSlot) + 15) & ~15u;
+                }
+                part[w + 1] = sum;
+            });
+            for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
+            c->pool->run([&](unsigned w) {
+                const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
+                uint64_t p = part[w];
+                for (uint32_t i = a; i < b; ++i) {
+                    uint32_t len = 0;
+                    const uint8_t* f = frame(base_i + i, &len);
+                    const uint32_t m = std::min(len, kHostSlot);
+                    if (m) std::memcpy(pre + p, f, m);
+                    d[i] = BT_DESC(p, len);
+                    p += (m + 15) & ~15u;
+                }
+            });
+            const uint64_t pos = part[T];
             const size_t pre_bytes = (pos + 15) & ~15ull;
             if (pre_bytes) HIP_TRY(hipMemcpyAsync(s.d_in, pre, pre_bytes, hipMemcpyHostToDevice, s.stream));
             HIP_TRY(hipMemcpyAsync(s.d_in + (size_t)chunk * kHostSlot, d, (size_t)cnt * 8, hipMemcpyHostToDevice,
@@ -523,7 +622,15 @@ int bt_synchronize(bt_ctx* c) {
     return BT_OK;
 }
 
-void bt_record_gather(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out) {
+void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out) {
+    const uint8_t* p = static_cast<const uint8_t*>(records);
+    uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    for (int k = 0; k < BT_REC_SLABS; ++k)
+        std::memcpy(o + 16 * k, p + (((size_t)(i / 64) * BT_REC_SLABS + k) * 64 + (i % 64)) * 16, 16);
+    (void)n_cap;
+}
+
+void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out) {
     const uint8_t* p = static_cast<const uint8_t*>(planes);
     uint8_t* o = reinterpret_cast<uint8_t*>(out);
     for (int k = 0; k < BT_REC_SLABS; ++k) std::memcpy(o + 16 * k, p + ((size_t)k * n_cap + i) * 16, 16);

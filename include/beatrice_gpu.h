@@ -34,10 +34,13 @@
  * PACKET_TOO_SHORT and no fields (:244-247): its field bytes are zero here.
  * Bytes of absent layers and reserved bytes are zero.
  *
- * On the device the records are stored SoA by 16-byte slab: slab k (k = 0..5)
- * of packet i lives at  records + (k * n_cap + i) * 16  ("plane-major"), so each
- * wavefront store instruction writes 1 KiB contiguously. bt_record_gather()
- * assembles one bt_rec from that layout.
+ * On the device the records are stored tiled by 64 packets (one wavefront tile),
+ * SoA by 16-byte slab inside the tile: slab k (k = 0..5) of packet i lives at
+ *     records + ((i / 64) * 6 + k) * 1024 + (i % 64) * 16
+ * so each wavefront store instruction writes 1 KiB contiguously and one tile's six
+ * slabs form one contiguous 6 KiB run (a single write stream). The buffer needs
+ * ceil(n / 64) * 6144 bytes. bt_record_gather() assembles one bt_rec from it.
+ * BT_OPT_RECORDS_PLANES selects plane-major slabs instead: (k * n_cap + i) * 16.
  */
 #ifndef BEATRICE_GPU_H
 #define BEATRICE_GPU_H
@@ -215,13 +218,15 @@ typedef struct bt_opts {
     uint32_t host_chunk_bytes;     /* pinned staging bytes per chunk (0 = default 256 MiB) */
     uint32_t grid_waves;           /* 0 = auto (persistent grid sized to the device)    */
     uint32_t flags;                /* BT_OPT_*                                          */
-    uint32_t reserved[4];
+    uint32_t host_threads;         /* host-path gather/drain threads (0 = auto, <= 16)  */
+    uint32_t reserved[3];
 } bt_opts;
 
 #define BT_OPT_NO_PREFETCH 0x1u    /* disable the next-tile load prefetch (A/B only)    */
 #define BT_OPT_TILE_BLOCKED 0x2u   /* one contiguous tile range per wavefront           */
 #define BT_OPT_RECORDS_AOS 0x4u    /* device records as bt_rec AoS instead of planes    */
 #define BT_OPT_GRAPH 0x8u          /* bt_time_device: replay the steps as one hipGraph  */
+#define BT_OPT_RECORDS_PLANES 0x10u /* device records plane-major (k * n_cap + i) * 16  */
 
 typedef struct bt_batch {          /* device-resident input */
     const uint8_t* base;           /* packet bytes                                      */
@@ -232,8 +237,8 @@ typedef struct bt_batch {          /* device-resident input */
 } bt_batch;
 
 typedef struct bt_outputs {        /* any pointer may be NULL = not produced            */
-    void*     records;             /* 96 * n_cap bytes, plane-major slabs               */
-    uint32_t  n_cap;               /* plane stride in records (>= n)                    */
+    void*     records;             /* ceil(n/64) * 6144 bytes, tiled slabs (see above)  */
+    uint32_t  n_cap;               /* records capacity (>= n); plane stride with PLANES */
     uint64_t* verdict;             /* ceil(n/64) words, bit i%64 of word i/64 = passed  */
     uint8_t*  decide;              /* n bytes, BT_DECIDE_*                              */
     uint32_t* pass_idx;            /* n entries: indices of passing packets, ascending  */
@@ -294,8 +299,9 @@ int  bt_synchronize(bt_ctx* ctx);
 int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
                     uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
 
-/* host-side record gather from the plane-major device layout (after a D2H copy) */
-void bt_record_gather(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out);
+/* host-side record gather from the device layout (after a D2H copy) */
+void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out);
+void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out);
 
 #ifdef __cplusplus
 }

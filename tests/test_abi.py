@@ -50,3 +50,21 @@ def test_compile_rejects_more_than_64_enabled_filters():
         abi.compile_host(fs)
     fs[3]["enabled"] = 0
     assert len(abi.compile_host(fs)) == 64
+
+
+def test_record_gather_matches_untile():
+    """bt_record_gather (C) and abi.untile_records (numpy) agree on the tiled layout."""
+    import numpy as np
+    n = 200
+    nt = (n + 63) // 64
+    buf = (np.arange(nt * 6144, dtype=np.uint32) * 2654435761 >> 13).astype(np.uint8)
+    aos = abi.untile_records(buf, n)
+    out = np.zeros(96, np.uint8)
+    for i in (0, 1, 63, 64, 130, 199):
+        abi.lib().bt_record_gather(buf.ctypes.data, n, i, out.ctypes.data)
+        assert np.array_equal(out, aos[i])
+    planes = buf[: 6 * n * 16]
+    aos_p = abi.untile_records(planes, n, planes=True)
+    for i in (0, 77, 199):
+        abi.lib().bt_record_gather_planes(planes.ctypes.data, n, i, out.ctypes.data)
+        assert np.array_equal(out, aos_p[i])

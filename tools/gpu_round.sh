@@ -10,4 +10,4 @@ for cfg in c2 c3 c4; do
   timeout -k 10 300 python bench.py --config $cfg > gpurun_out/bench_$cfg.json 2>gpurun_out/bench_$cfg.err || exit 3
   summ gpurun_out/bench_$cfg.json
 done
-for cfg in c2 c3; do timeout -k 10 300 python tools/e2e.py --config $cfg > gpurun_out/e2e_$cfg.json 2>&1 || exit 5; cat gpurun_out/e2e_$cfg.json; done
+for cfg in c2 c3 c4; do timeout -k 10 300 python tools/e2e.py --config $cfg > gpurun_out/e2e_$cfg.json 2>&1 || exit 5; cat gpurun_out/e2e_$cfg.json; done
