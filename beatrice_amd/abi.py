@@ -62,6 +62,10 @@ OPT_TILE_BLOCKED = 0x2
 OPT_RECORDS_AOS = 0x4
 OPT_GRAPH = 0x8
 OPT_RECORDS_PLANES = 0x10
+OPT_NT_STORES = 0x20
+OPT_NT_LOADS = 0x40
+OPT_CACHE_DEFAULT = 0x80
+OPT_SPIN_SYNC = 0x100
 
 
 class Batch(ctypes.Structure):

@@ -32,6 +32,7 @@ struct MainArgs {
     uint64_t* verdict;
     uint32_t* tile_pass;       // per-tile pass counts (compaction input)
     uint32_t blocked;          // tile order: 0 cyclic, 1 one contiguous range per wavefront
+    uint32_t nt;               // bit0 non-temporal record stores, bit1 non-temporal header loads
 };
 
 constexpr int kWave = 64;

@@ -59,6 +59,25 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ bool is_vlan(uint32_t et) { return et == 0x8100u || et == 0x88A8u; }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-B global load / store; `nt` selects the non-temporal (streaming) cache policy.
+__device__ __forceinline__ uint4 ld16(const uint8_t* p, bool nt) {
+    if (nt) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    }
+    return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void st16(uint4* p, uint4 v, bool nt) {
+    if (nt) {
+        const u32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 struct Parsed {
     uint32_t r[24];   // bt_rec as 24 little-endian dwords
 };
@@ -209,7 +228,7 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
         for (uint32_t j = 0; j < cpp; ++j) {
             const uint32_t g = j * 64u + lane;
             const bool ok = p0 + (g >> kL) < a.n;
-            st.v[j] = ok ? *reinterpret_cast<const uint4*>(span + (uint64_t)g * 16u) : make_uint4(0, 0, 0, 0);
+            st.v[j] = ok ? ld16(span + (uint64_t)g * 16u, a.nt & 2u) : make_uint4(0, 0, 0, 0);
         }
     } else {
         if (a.desc) {
@@ -235,11 +254,11 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
             st.qa0[j] = a0;
             const bool live_q = p0 + q < a.n;
             const bool ok = live_q && (16u * c < sq + ql) && (addr + 16u <= a.bytes);
-            st.v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+            st.v[j] = ok ? ld16(a.base + addr, a.nt & 2u) : make_uint4(0, 0, 0, 0);
             if (wide) {   // chunks 4..7 up to the longest header the walk can read
                 const uint32_t nq = ql < need_max ? ql : need_max;
                 const bool okb = live_q && (16u * (c + 4u) < sq + nq) && (addr + 64u + 16u <= a.bytes);
-                st.v[4 + j] = okb ? *reinterpret_cast<const uint4*>(a.base + addr + 64u) : make_uint4(0, 0, 0, 0);
+                st.v[4 + j] = okb ? ld16(a.base + addr + 64u, a.nt & 2u) : make_uint4(0, 0, 0, 0);
             }
         }
     }
@@ -301,7 +320,7 @@ __device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint
         const uint32_t qn = (uint32_t)__shfl((int)my_need, (int)q);   // bytes of q's window needed
         const uint64_t addr = qa0[j] + 16u * c;
         const bool ok = (t * 64u + q < a.n) && (16u * c < qn) && (addr + 16u <= a.bytes);
-        v[j] = ok ? *reinterpret_cast<const uint4*>(a.base + addr) : make_uint4(0, 0, 0, 0);
+        v[j] = ok ? ld16(a.base + addr, a.nt & 2u) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
@@ -382,13 +401,13 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                 uint4* planes = reinterpret_cast<uint4*>(a.records);
 #pragma unroll
                 for (int k = 0; k < BT_REC_SLABS; ++k)
-                    planes[(uint64_t)k * a.n_cap + my] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
+                    st16(planes + (uint64_t)k * a.n_cap + my, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
             } else if (REC == kRecTiled) {
                 // [tile][slab][lane]: the tile's six 1-KiB slab stores land back to back
                 uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
 #pragma unroll
                 for (int k = 0; k < BT_REC_SLABS; ++k)
-                    tile[k * 64 + lane] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
+                    st16(tile + k * 64 + lane, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
             } else {
                 uint4* rec = reinterpret_cast<uint4*>(a.records + (uint64_t)my * BT_REC_BYTES);
 #pragma unroll

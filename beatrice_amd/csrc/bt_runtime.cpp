@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <thread>
@@ -200,6 +201,13 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
     a.tile_pass = compact ? c->tile_pass : nullptr;
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
+    // Cache policy (measured, profiles/r01): non-temporal record stores everywhere
+    // (C2 +3..9 %), non-temporal header loads in descriptor mode (C3 +15 %, C4 +8 %;
+    // they cost C2 a little). BT_OPT_CACHE_DEFAULT turns both off, BT_OPT_NT_* force on.
+    if (c->opts.flags & BT_OPT_CACHE_DEFAULT) a.nt = 0;
+    else a.nt = 1u | (b->desc ? 2u : 0u);
+    if (c->opts.flags & BT_OPT_NT_STORES) a.nt |= 1u;
+    if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     int rec = kRecNone;
     if (o->records) {
         if (aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) rec = kRecAoS;
@@ -302,6 +310,12 @@ int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
     auto* c = new bt_ctx();
     c->device = device;
     if (opts) c->opts = *opts;
+    if (c->opts.flags & BT_OPT_SPIN_SYNC) {
+        // host waits spin instead of sleeping: no wake-up latency on a loaded host.
+        // Only possible before the process's first HIP context on this device.
+        (void)hipSetDevice(device);
+        (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+    }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(BT_E_INIT_FAILED, "hipSetDevice/hipStreamCreate failed on device %d", device);
@@ -409,6 +423,8 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
         c->tg_out = *o;
         c->tg_iters = iters;
     }
+    static const bool dbg = getenv("BT_DEBUG_TIMING") != nullptr;
+    const auto h0 = std::chrono::steady_clock::now();
     if (use_graph) {
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(hipGraphLaunch(c->tgraph, c->stream));
@@ -421,7 +437,9 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
         }
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
     }
+    const auto h1 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(c->ev1));
+    const auto h2 = std::chrono::steady_clock::now();
     float tot = 0, k = 0;
     HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
     for (uint32_t i = 0; !use_graph && i < iters; ++i) {
@@ -431,6 +449,12 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
     }
     if (ms_per_iter) *ms_per_iter = tot / iters;
     if (main_ms) *main_ms = use_graph ? -1.0f : k / iters;
+    if (dbg) {
+        const auto h3 = std::chrono::steady_clock::now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "[bt_time_device] enqueue %.3f ms, sync %.3f ms, elapsed-queries %.3f ms, gpu span %.3f ms\n",
+                ms(h0, h1), ms(h1, h2), ms(h2, h3), tot);
+    }
     return BT_OK;
 }
 

@@ -130,6 +130,7 @@ def main():
 
     data, desc = synth.capture(wl["cfg"], n, seed=synth.SEEDS[wl["cfg"]] + rank)
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
+    flags |= abi.OPT_SPIN_SYNC   # the timed region's end is not delayed by a sleeping host thread
     ctx = abi.Context(local, grid_waves=args.grid_waves, flags=flags)
     if wl["filters"]:
         ctx.compile(wl["filters"])
@@ -150,9 +151,12 @@ def main():
     ctx.synchronize()
     t0 = time.perf_counter()
     ms_iter, main_ms = ctx.time_device(run.batch, run.outs, args.steps)
+    ta = time.perf_counter()
     ctx.synchronize()
     barrier()
     t1 = time.perf_counter()
+    if os.environ.get("BT_DEBUG_TIMING"):
+        print(f"[bench] time_device {1e3 * (ta - t0):.3f} ms, sync+barrier {1e3 * (t1 - ta):.3f} ms", file=sys.stderr)
     step_s = (t1 - t0) / args.steps
     if dist is not None:
         import torch

@@ -227,6 +227,10 @@ typedef struct bt_opts {
 #define BT_OPT_RECORDS_AOS 0x4u    /* device records as bt_rec AoS instead of planes    */
 #define BT_OPT_GRAPH 0x8u          /* bt_time_device: replay the steps as one hipGraph  */
 #define BT_OPT_RECORDS_PLANES 0x10u /* device records plane-major (k * n_cap + i) * 16  */
+#define BT_OPT_NT_STORES 0x20u     /* force non-temporal record stores                   */
+#define BT_OPT_NT_LOADS 0x40u      /* force non-temporal header loads                    */
+#define BT_OPT_CACHE_DEFAULT 0x80u /* default cache policy everywhere (A/B only)         */
+#define BT_OPT_SPIN_SYNC 0x100u    /* spin-wait host synchronisation (bench / latency)   */
 
 typedef struct bt_batch {          /* device-resident input */
     const uint8_t* base;           /* packet bytes                                      */
