@@ -68,9 +68,13 @@ OPT_CACHE_DEFAULT = 0x80
 OPT_SPIN_SYNC = 0x100
 
 
+DESC_PACKED, DESC_XDP = 0, 1
+
+
 class Batch(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("stride", ctypes.c_uint32),
-                ("n", ctypes.c_uint32), ("bytes", ctypes.c_uint64)]
+                ("n", ctypes.c_uint32), ("bytes", ctypes.c_uint64), ("desc_format", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class Outputs(ctypes.Structure):
@@ -81,7 +85,7 @@ class Outputs(ctypes.Structure):
 EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
-    "bt_parse_filter", "bt_parse_filter_ptrs", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
+    "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
 ]
 
@@ -111,6 +115,8 @@ def lib() -> ctypes.CDLL:
         "bt_parse_filter_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), vp]),
         "bt_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_host_register": (ctypes.c_int, [vp, vp, u64, ctypes.POINTER(vp)]),
+        "bt_host_unregister": (ctypes.c_int, [vp, vp]),
         "bt_dev_malloc": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
         "bt_dev_free": (ctypes.c_int, [vp, vp]),
         "bt_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, u64]),
@@ -237,6 +243,15 @@ class Context:
 
     def reserve(self, n: int):
         _check(lib().bt_reserve(self.h, n))
+
+    def register(self, arr: np.ndarray) -> int:
+        """Page-lock + map a host array (zero-copy); returns its device alias."""
+        p = ctypes.c_void_p(0)
+        _check(lib().bt_host_register(self.h, arr.ctypes.data, arr.nbytes, ctypes.byref(p)))
+        return p.value
+
+    def unregister(self, arr: np.ndarray):
+        _check(lib().bt_host_unregister(self.h, arr.ctypes.data))
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)

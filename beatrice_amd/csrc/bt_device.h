@@ -22,6 +22,7 @@ struct DevProgram {
 struct MainArgs {
     const uint8_t* base;
     const uint64_t* desc;      // nullptr: fixed stride
+    uint32_t desc_words;       // descriptor stride in u64 words: 1 packed, 2 xdp_desc
     uint64_t bytes;            // readable size of base (rounded up to 16 by the caller)
     uint32_t stride;
     uint32_t n;

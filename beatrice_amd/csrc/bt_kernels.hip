@@ -232,9 +232,15 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
         }
     } else {
         if (a.desc) {
-            const uint64_t d = live ? a.desc[my] : 0ull;
-            st.off = d & 0xFFFFFFFFFFFFull;
-            st.len = (uint32_t)(d >> 48);
+            if (a.desc_words == 1) {   // bt_pkt_desc
+                const uint64_t d = live ? a.desc[my] : 0ull;
+                st.off = d & 0xFFFFFFFFFFFFull;
+                st.len = (uint32_t)(d >> 48);
+            } else {                   // xdp_desc {u64 addr; u32 len; u32 options}
+                const uint4 d = live ? *reinterpret_cast<const uint4*>(a.desc + 2ull * my) : make_uint4(0, 0, 0, 0);
+                st.off = ((uint64_t)d.y << 32) | d.x;
+                st.len = d.z > 0xFFFFu ? 0xFFFFu : d.z;
+            }
         } else {
             st.off = live ? (uint64_t)my * a.stride : 0ull;
             st.len = live ? a.stride : 0u;

@@ -186,9 +186,11 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
         int rc = ensure_ws(c, b->n);
         if (rc) return rc;
     }
+    if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
     MainArgs a{};
     a.base = b->base;
-    a.desc = b->desc;
+    a.desc = static_cast<const uint64_t*>(b->desc);
+    a.desc_words = b->desc_format == BT_DESC_XDP ? 2u : 1u;
     a.stride = b->stride;
     a.n = b->n;
     a.ntiles = (b->n + 63) / 64;
@@ -599,6 +601,26 @@ int bt_parse_filter_ptrs(bt_ctx* c, const uint8_t* const* frames, const uint32_t
             return frames[i];
         },
         records, verdict, decide, pass_idx, n_pass);
+}
+
+int bt_host_register(bt_ctx* c, void* host, uint64_t bytes, void** dev_alias) {
+    if (!c || !host || !dev_alias || !bytes) return fail(BT_E_INVALID_ARGUMENT, "null argument / empty range");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipHostRegister(host, bytes, hipHostRegisterMapped));
+    hipError_t e = hipHostGetDevicePointer(dev_alias, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return fail(BT_E_INTERNAL, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    return BT_OK;
+}
+
+int bt_host_unregister(bt_ctx* c, void* host) {
+    if (!c || !host) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipHostUnregister(host));
+    return BT_OK;
 }
 
 int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {

@@ -232,12 +232,21 @@ typedef struct bt_opts {
 #define BT_OPT_CACHE_DEFAULT 0x80u /* default cache policy everywhere (A/B only)         */
 #define BT_OPT_SPIN_SYNC 0x100u    /* spin-wait host synchronisation (bench / latency)   */
 
-typedef struct bt_batch {          /* device-resident input */
-    const uint8_t* base;           /* packet bytes                                      */
-    const bt_pkt_desc* desc;       /* one per packet; NULL selects fixed-stride mode    */
+/* descriptor formats (bt_batch.desc_format) */
+#define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
+#define BT_DESC_XDP    1u          /* struct xdp_desc {u64 addr; u32 len; u32 options} as
+                                      an AF_XDP RX ring holds it (linux/if_xdp.h), aligned
+                                      chunk mode: addr = byte offset into the UMEM        */
+
+typedef struct bt_batch {          /* input; device memory or host memory mapped with
+                                      bt_host_register (zero-copy over PCIe)             */
+    const uint8_t* base;           /* packet bytes (e.g. the UMEM)                      */
+    const void* desc;              /* one descriptor per packet; NULL = fixed stride    */
     uint32_t stride;               /* fixed-stride mode: packet i = base[i*stride .. +stride) */
     uint32_t n;                    /* packets                                           */
     uint64_t bytes;                /* size of the base buffer (bounds check)            */
+    uint32_t desc_format;          /* BT_DESC_PACKED / BT_DESC_XDP                      */
+    uint32_t reserved;
 } bt_batch;
 
 typedef struct bt_outputs {        /* any pointer may be NULL = not produced            */
@@ -287,6 +296,13 @@ int  bt_parse_filter(bt_ctx* ctx, const uint8_t* base, const bt_pkt_desc* desc, 
 int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                           bt_rec* records, uint64_t* verdict, uint8_t* decide,
                           uint32_t* pass_idx, uint32_t* n_pass);
+
+/* Zero-copy ingest: page-lock a host range (an AF_XDP UMEM, an RX descriptor ring,
+ * an output array) and map it into the device; *dev_alias is the pointer kernels
+ * use (it may be passed as bt_batch.base / .desc or as an output). The kernels then
+ * read the header windows straight over PCIe: no host gather, no staging copy. */
+int  bt_host_register(bt_ctx* ctx, void* host, uint64_t bytes, void** dev_alias);
+int  bt_host_unregister(bt_ctx* ctx, void* host);
 
 /* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
 int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);

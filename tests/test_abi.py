@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported():
 def test_abi_version_and_struct_sizes():
     assert abi.lib().bt_abi_version() == 1
     assert ctypes.sizeof(abi.Opts) == 32
-    assert ctypes.sizeof(abi.Batch) == 32
+    assert ctypes.sizeof(abi.Batch) == 40
     assert ctypes.sizeof(abi.Outputs) == 48
     assert ctypes.sizeof(abi.FilterDesc) == 32
     assert ctypes.sizeof(abi.FilterSlot) == 20

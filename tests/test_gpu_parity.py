@@ -188,3 +188,79 @@ def test_graph_replay_outputs(gpu_ctx):
     rec, dec, npass = ol.oracle_run(data, desc, n, filters)
     assert np.array_equal(out["records"], rec) and np.array_equal(out["decide"], dec)
     check_filter_outputs(out, n)
+
+
+def _umem(frames_data, desc, chunk=2048, shuffle_seed=5):
+    """An AF_XDP-style UMEM (anonymous mmap, numBuffers x bufferSize chunks, headroom 0,
+    reference src/AF_XDPBackend.cpp:683-720) holding each frame at the start of a chunk,
+    plus the RX ring's xdp_desc {addr, len, options} (shuffled chunk order, as after
+    fill-ring recycling)."""
+    import mmap
+    n = len(desc)
+    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+    assert ln.max() <= chunk
+    mm = mmap.mmap(-1, n * chunk)
+    umem = np.frombuffer(mm, dtype=np.uint8)
+    order = np.random.default_rng(shuffle_seed).permutation(n)
+    for i in range(n):
+        c = order[i] * chunk
+        umem[c:c + ln[i]] = frames_data[off[i]:off[i] + ln[i]]
+    xdp = np.zeros((n, 2), np.uint64)
+    xdp[:, 0] = order.astype(np.uint64) * chunk
+    xdp[:, 1] = ln.astype(np.uint64)               # len in the low 32 bits, options = 0
+    packed = synth.make_desc(order.astype(np.uint64) * chunk, ln)
+    return mm, umem, xdp, packed
+
+
+def test_zero_copy_umem_ingest(gpu_ctx):
+    """AF_XDP UMEM + RX xdp_desc ring consumed zero-copy — both
+    registered with bt_host_register, the kernel reads the header windows over PCIe."""
+    n = 50000
+    data, desc = synth.capture(synth.C3, n, seed=31)
+    mm, umem, xdp, packed = _umem(data, desc)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    gpu_ctx.compile(filters)
+    d_umem = gpu_ctx.register(umem)
+    d_xdp = gpu_ctx.register(xdp)
+    try:
+        r = abi.DeviceRun(gpu_ctx, np.zeros(256, np.uint8), None, n, stride=1)
+        r.batch = abi.Batch(d_umem, d_xdp, 0, n, umem.nbytes, abi.DESC_XDP, 0)
+        r.run()
+        out = r.fetch()
+        r.free()
+    finally:
+        gpu_ctx.unregister(xdp)
+        gpu_ctx.unregister(umem)
+    rec, dec, npass = ol.oracle_run(umem, packed, n, filters)
+    assert np.array_equal(out["records"], rec)
+    assert np.array_equal(out["decide"], dec)
+    check_filter_outputs(out, n)
+    del umem
+    mm.close()
+
+
+def test_zero_copy_outputs(gpu_ctx):
+    """Outputs written by the kernel straight into registered host memory."""
+    n = 30000
+    data, desc = synth.capture(synth.C4, n, seed=77)
+    filters = [{"type": abi.BPF, "expr": "tcp", "priority": 1}]
+    gpu_ctx.compile(filters)
+    h_rec = np.zeros(((n + 63) // 64) * 6144, np.uint8)
+    h_dec = np.zeros(n, np.uint8)
+    h_ver = np.zeros((n + 63) // 64, np.uint64)
+    d_data, d_desc = gpu_ctx.register(data), gpu_ctx.register(desc)
+    aliases = [gpu_ctx.register(x) for x in (h_rec, h_dec, h_ver)]
+    try:
+        batch = abi.Batch(d_data, d_desc, 0, n, data.nbytes, abi.DESC_PACKED, 0)
+        gpu_ctx.run_device(batch, abi.Outputs(aliases[0], n, aliases[2], aliases[1], None, None))
+        gpu_ctx.synchronize()
+    finally:
+        for x in (h_rec, h_dec, h_ver, data, desc):
+            gpu_ctx.unregister(x)
+    rec, dec, _ = ol.oracle_run(data, desc, n, filters)
+    assert np.array_equal(abi.untile_records(h_rec, n), rec)
+    assert np.array_equal(h_dec, dec)
+    bits = np.unpackbits(h_ver.view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(bits, (dec >> 6) == 0)
