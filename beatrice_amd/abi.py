@@ -82,11 +82,17 @@ class Outputs(ctypes.Structure):
                 ("decide", ctypes.c_void_p), ("pass_idx", ctypes.c_void_p), ("n_pass", ctypes.c_void_p)]
 
 
+class Tpv3Ring(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("block_size", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
 EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
+    "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
 ]
 
 _lib = None
@@ -127,6 +133,9 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
         "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
+        "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
+                                             ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+        "bt_ring_release_tpv3": (ctypes.c_int, [ctypes.POINTER(Tpv3Ring), u32, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -285,6 +294,37 @@ class Context:
             out["pass_idx"] = pidx[: int(npass[0])]
             out["n_pass"] = int(npass[0])
         return out
+
+
+def ring_walk_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int = 0,
+                   max_blocks: int | None = None, cap: int | None = None, ctx: "Context | None" = None,
+                   out: np.ndarray | None = None):
+    """bt_ring_walk_tpv3 over a TPACKET_V3 ring image / mmap'd ring held in `ring` (uint8).
+    Returns (desc uint64[n], blocks taken); with `out` (contiguous uint64) the descriptors
+    are written there and desc is a view of it. Host-only: ctx may be None (no GPU)."""
+    L = lib()
+    if ring.nbytes < block_size * n_blocks:
+        raise ValueError("ring buffer smaller than block_size * n_blocks")
+    if out is not None:
+        if out.dtype != np.uint64 or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint64 array")
+        cap = len(out) if cap is None else min(cap, len(out))
+        desc = out
+    else:
+        if cap is None:
+            cap = int(ring.nbytes // 96) + 1
+        desc = np.empty(max(cap, 1), dtype=np.uint64)
+    r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
+    nd, nb = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(L.bt_ring_walk_tpv3(ctx.h if ctx else None, ctypes.byref(r), first,
+                               n_blocks if max_blocks is None else max_blocks, desc.ctypes.data, cap,
+                               ctypes.byref(nd), ctypes.byref(nb)))
+    return desc[:nd.value], nb.value
+
+
+def ring_release_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int, count: int):
+    r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
+    _check(lib().bt_ring_release_tpv3(ctypes.byref(r), first, count))
 
 
 def untile_records(buf: np.ndarray, n: int, planes: bool = False) -> np.ndarray:

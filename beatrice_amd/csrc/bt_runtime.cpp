@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "bt_device.h"
+#include "bt_host.h"
 
 using namespace bt;
 
@@ -78,6 +79,7 @@ public:
     // runs fn(worker) on every worker (the caller is worker 0) and waits
     void run(const std::function<void(unsigned)>& fn) {
         if (nthreads_ == 1) { fn(0); return; }
+        std::lock_guard<std::mutex> one_at_a_time(run_mu_);   // callers on several threads
         {
             std::lock_guard<std::mutex> lk(m_);
             fn_ = &fn;
@@ -111,7 +113,7 @@ private:
         }
     }
     std::vector<std::thread> th_;
-    std::mutex m_;
+    std::mutex m_, run_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)>* fn_ = nullptr;
     unsigned pending_ = 0, nthreads_ = 1;
@@ -141,7 +143,8 @@ struct bt_ctx {
     uint32_t chunk = 0;
     HostSlot hs[2];
     bool host_ready = false;
-    std::unique_ptr<HostPool> pool;
+    std::unique_ptr<HostPool> pool;   // created on first use (pool_of)
+    std::once_flag pool_once;
 
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -152,6 +155,39 @@ struct bt_ctx {
     bt_outputs tg_out{};
     uint32_t tg_iters = 0;
 };
+
+namespace bt {
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+HostPool& pool_of(bt_ctx* c) {
+    std::call_once(c->pool_once, [c] {
+        unsigned nt = c->opts.host_threads;
+        if (!nt) nt = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        c->pool = std::make_unique<HostPool>(std::min(nt, 16u));
+    });
+    return *c->pool;
+}
+
+void host_parallel(bt_ctx* ctx, const std::function<void(unsigned, unsigned)>& fn) {
+    if (!ctx) {
+        fn(0, 1);
+        return;
+    }
+    HostPool& pool = pool_of(ctx);
+    const unsigned T = pool.size();
+    pool.run([&](unsigned w) { fn(w, T); });
+}
+
+}  // namespace bt
 
 namespace {
 
@@ -250,9 +286,7 @@ int ensure_host(bt_ctx* c) {
     uint32_t chunk = c->opts.host_chunk_packets ? c->opts.host_chunk_packets : (1u << 20);
     chunk = (chunk + 63) / 64 * 64;
     c->chunk = chunk;
-    unsigned nt = c->opts.host_threads;
-    if (!nt) nt = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
-    c->pool = std::make_unique<HostPool>(std::min(nt, 16u));
+    (void)pool_of(c);
     for (auto& s : c->hs) {
         HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <sys/socket.h>
+#include <linux/if_packet.h>
 #include <random>
 #include <thread>
 #include <vector>
@@ -276,6 +278,75 @@ int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint
     }
     for (auto& x : th) x.join();
     return 0;
+}
+
+// Packs a capture into an AF_PACKET TPACKET_V3 RX-ring image the way the kernel lays
+// one out (net/packet/af_packet.c, tpacket_rcv / prb_* with tp_reserve 0, no block
+// private area): 48-B block header, frames 8-B aligned, each a tpacket3_hdr + sockaddr_ll
+// with the MAC header at tp_mac = 82, snaplen clamped to the block's max frame length,
+// and the last frame of a block with tp_next_offset 0. Frames are packed until
+// ring_blocks blocks are full. ring == NULL only counts. ring_desc (optional) gets
+// BT_DESC(ring offset of the MAC header, snaplen) per packed frame. Returns the number
+// of frames packed; *blocks_used the blocks written (all marked TP_STATUS_USER).
+uint64_t bt_synth_tpv3_pack(const uint8_t* data, const uint64_t* desc, uint64_t n, uint64_t block_size,
+                            uint8_t* ring, uint64_t ring_blocks, uint64_t* ring_desc, uint64_t* blocks_used) {
+    const uint32_t kBlkHdr = 48, kMacOff = 82, kAlign = 8;
+    const uint64_t max_frame = block_size - kBlkHdr;
+    uint64_t blk = 0, off = kBlkHdr, packed = 0, seq = 1;
+    uint32_t in_blk = 0;
+    uint8_t* prev = nullptr;
+    auto close_block = [&]() {
+        if (!in_blk) return;
+        if (ring) {
+            tpacket_block_desc* bd = reinterpret_cast<tpacket_block_desc*>(ring + blk * block_size);
+            bd->version = TPACKET_V3;
+            bd->offset_to_priv = kBlkHdr;
+            bd->hdr.bh1.num_pkts = in_blk;
+            bd->hdr.bh1.offset_to_first_pkt = kBlkHdr;
+            bd->hdr.bh1.blk_len = (uint32_t)off;
+            bd->hdr.bh1.seq_num = seq;
+            bd->hdr.bh1.block_status = TP_STATUS_USER;
+            reinterpret_cast<tpacket3_hdr*>(prev)->tp_next_offset = 0;
+        }
+        ++seq;
+        ++blk;
+        off = kBlkHdr;
+        in_blk = 0;
+    };
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t src = desc[i] & 0xFFFFFFFFFFFFull;
+        const uint32_t len = (uint32_t)(desc[i] >> 48);
+        const uint32_t snap = (uint32_t)std::min<uint64_t>(len, max_frame - kMacOff);
+        const uint64_t need = (kMacOff + snap + kAlign - 1) & ~(uint64_t)(kAlign - 1);
+        if (off + need > block_size) close_block();
+        if (blk >= ring_blocks) break;
+        if (ring) {
+            uint8_t* f = ring + blk * block_size + off;
+            std::memset(f, 0, kMacOff);
+            tpacket3_hdr* h = reinterpret_cast<tpacket3_hdr*>(f);
+            h->tp_next_offset = (uint32_t)need;
+            h->tp_sec = (uint32_t)(i / 1000000);
+            h->tp_nsec = (uint32_t)(i % 1000000) * 1000;
+            h->tp_snaplen = snap;
+            h->tp_len = len;
+            h->tp_status = TP_STATUS_USER;
+            h->tp_mac = kMacOff;
+            h->tp_net = kMacOff + 14;
+            sockaddr_ll* sll = reinterpret_cast<sockaddr_ll*>(f + 48);
+            sll->sll_family = AF_PACKET;
+            sll->sll_ifindex = 1;
+            sll->sll_halen = 6;
+            if (snap) std::memcpy(f + kMacOff, data + src, snap);
+            prev = f;
+        }
+        if (ring_desc) ring_desc[packed] = ((uint64_t)snap << 48) | (blk * block_size + off + kMacOff);
+        off += need;
+        ++in_blk;
+        ++packed;
+    }
+    if (blk < ring_blocks) close_block();
+    if (blocks_used) *blocks_used = blk;
+    return packed;
 }
 
 }  // extern "C"

@@ -1,0 +1,154 @@
+// GpuCapture.hpp — capture-ring ingest in front of the MI355X parse+filter stage
+// ("AF_PACKET TPACKET_V3 ring ingest replacing per-packet recv() +
+// copy"; the north star: the path starts and ends in host ring buffers).
+//
+//   GpuAfPacketBackend  drop-in for the reference's AF_PacketBackend
+//                       (include/beatrice/AF_PacketBackend.hpp, src/AF_PacketBackend.cpp):
+//                       the same ICaptureBackend interface and queue / callback
+//                       semantics, fed from a TPACKET_V3 ring (whole blocks per wake-up)
+//                       instead of one recv() + copy + 100 us sleep per packet.
+//   GpuTpacketStage     the zero-copy path: the ring is registered with the GPU once,
+//                       ready blocks become descriptors (bt_ring_walk_tpv3) and the
+//                       parse+filter kernels read the frames in place over PCIe; the
+//                       decisions / verdict bitmap / records land in registered host
+//                       memory. Nothing is copied on the host.
+//
+// Both live in libbeatrice_gpu_capture.so; Packet's out-of-line members resolve
+// against beatrice_core in the process that loads it, as for the plugin.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "GpuPacketFilter.hpp"
+#include "TpacketRing.hpp"
+#include "beatrice/ICaptureBackend.hpp"
+
+namespace beatrice {
+namespace gpu {
+
+class GpuAfPacketBackend : public ICaptureBackend {
+public:
+    GpuAfPacketBackend();
+    ~GpuAfPacketBackend() override;
+
+    Result<void> initialize(const Config& config) override;
+    Result<void> start() override;
+    Result<void> stop() override;
+    bool isRunning() const noexcept override;
+    std::optional<Packet> nextPacket(std::chrono::milliseconds timeout = std::chrono::milliseconds(1000)) override;
+    std::vector<Packet> getPackets(size_t maxPackets = 64,
+                                   std::chrono::milliseconds timeout = std::chrono::milliseconds(1000)) override;
+    void setPacketCallback(std::function<void(Packet)> callback) override;
+    void removePacketCallback() override;
+    Statistics getStatistics() const override;
+    void resetStatistics() override;
+    std::string getName() const override;
+    std::string getVersion() const override;
+    std::vector<std::string> getSupportedFeatures() const override;
+    bool isFeatureSupported(const std::string& feature) const override;
+    Config getConfig() const override;
+    Result<void> updateConfig(const Config& config) override;
+    std::string getLastError() const override;
+    bool isHealthy() const override;
+    Result<void> healthCheck() override;
+
+    bool isZeroCopyEnabled() const override;
+    bool isDMAAccessEnabled() const override;
+    Result<void> enableZeroCopy(bool enabled) override;
+    Result<void> enableDMAAccess(bool enabled, const std::string& device = "") override;
+    Result<void> setDMABufferSize(size_t size) override;
+    size_t getDMABufferSize() const override;
+    std::string getDMADevice() const override;
+    Result<void> allocateDMABuffers(size_t count) override;
+    Result<void> freeDMABuffers() override;
+
+    // ring geometry used by initialize(): the reference's buffer budget
+    // (bufferSize x numBuffers), in blocks of blockBytes
+    static TpacketV3Ring::Options ringOptions(const Config& config);
+
+private:
+    void captureLoop();
+    void setError(const std::string& e);
+
+    Config config_;
+    bool initialized_ = false;
+    std::atomic<bool> running_{false};
+    TpacketV3Ring ring_;
+    std::thread thread_;
+    std::queue<Packet> queue_;
+    std::mutex queueMutex_;
+    std::condition_variable queueCv_;
+    std::function<void(Packet)> callback_;
+    std::mutex callbackMutex_;
+    Statistics stats_;
+    mutable std::mutex statsMutex_;
+    std::string lastError_;
+    mutable std::mutex errorMutex_;
+    bool zeroCopy_ = true, dma_ = false;
+    std::string dmaDevice_;
+    size_t dmaBufferSize_ = 0;
+};
+
+class GpuTpacketStage {
+public:
+    struct Options {
+        uint32_t maxBlocks = 64;        // blocks per batch (upper bound; more blocks = more
+                                        // frame chains walked in parallel)
+        uint32_t maxPackets = 1u << 20; // descriptors per batch (upper bound)
+        bool records = false;           // also write bt_rec records (device tiled layout)
+    };
+    // One batch of ring blocks, owned by the caller until release().
+    struct Batch {
+        uint32_t n = 0, blocks = 0;
+        const bt_pkt_desc* desc = nullptr;   // ring-relative
+        const uint8_t* decide = nullptr;     // (code << 6) | slot, host-side slots resolved
+        const uint64_t* verdict = nullptr;   // bit i = packet i passed
+        const void* records = nullptr;       // tiled (include/beatrice_gpu.h); records == true only
+        std::vector<uint32_t> pass;          // ascending
+    };
+
+    // The filter supplies the context (device, stream) and the compiled program; the
+    // ring must stay open for the stage's lifetime. Throws std::runtime_error when the
+    // ring cannot be mapped into the device.
+    GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring, Options opts);
+    GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring) : GpuTpacketStage(filter, ring, Options()) {}
+    ~GpuTpacketStage();
+    GpuTpacketStage(const GpuTpacketStage&) = delete;
+    GpuTpacketStage& operator=(const GpuTpacketStage&) = delete;
+
+    // Waits up to `timeout` for a ready block, takes the ready blocks from the ring
+    // cursor and runs them through the GPU. An empty batch (n == 0, blocks == 0) means
+    // nothing arrived. Throws what GpuPacketFilter::applyFilters throws.
+    const Batch& poll(std::chrono::milliseconds timeout);
+    // Hands the last batch's blocks back to the kernel.
+    void release();
+
+    const uint8_t* frame(uint32_t i) const { return ringBase_ + BT_DESC_OFF(batch_.desc[i]); }
+    uint32_t length(uint32_t i) const { return BT_DESC_LEN(batch_.desc[i]); }
+    bt_rec record(uint32_t i) const;
+
+private:
+    GpuPacketFilter& filter_;
+    TpacketV3Ring& ring_;
+    Options opts_;
+    uint8_t* ringBase_ = nullptr;
+    void* ringDev_ = nullptr;
+    // registered host buffers: descriptors in, decisions / verdicts / records out
+    std::vector<bt_pkt_desc> desc_;
+    std::vector<uint8_t> decide_;
+    std::vector<uint64_t> verdict_;
+    std::vector<uint8_t> records_;
+    void *descDev_ = nullptr, *decideDev_ = nullptr, *verdictDev_ = nullptr, *recordsDev_ = nullptr;
+    Batch batch_;
+};
+
+}  // namespace gpu
+}  // namespace beatrice

@@ -276,5 +276,58 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
     return v;
 }
 
+std::vector<uint32_t> GpuPacketFilter::classifyMapped(const bt_batch& batch, const bt_outputs& out,
+                                                     uint8_t* decideHost, uint64_t* verdictHost,
+                                                     const std::function<Packet(uint32_t)>& packetOf) {
+    std::vector<uint32_t> pass;
+    std::lock_guard<std::mutex> lock(filtersMutex_);
+    if (dirty_) compileLocked();
+    if (!batch.n) return pass;
+    if (!out.decide || !decideHost) throw std::invalid_argument("GpuPacketFilter::classifyMapped: decide required");
+    const auto t0 = std::chrono::steady_clock::now();
+    if (bt_parse_filter_device(ctx_, &batch, &out, nullptr) != BT_OK || bt_synchronize(ctx_) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
+                     (int64_t)batch.n;
+    // stats are sums: count per (code, slot) and apply once (before a rethrow too)
+    uint64_t passed = 0, rejected[BT_MAX_FILTERS] = {};
+    uint32_t counted = 0;
+    auto flush = [&] {
+        std::lock_guard<std::mutex> sl(statsMutex_);
+        stats_.packetsProcessed += counted;
+        stats_.packetsPassed += passed;
+        stats_.packetsDropped += counted - passed;
+        stats_.totalProcessingTime += per * (int64_t)counted;
+        if (program_.empty()) {
+            if (counted) stats_.filterCounts[""] += counted;
+            return;
+        }
+        if (passed) stats_.filterCounts[program_.back().name] += passed;
+        for (size_t s = 0; s < program_.size(); ++s)
+            if (rejected[s]) stats_.filterCounts[program_[s].name] += rejected[s];
+    };
+    for (uint32_t i = 0; i < batch.n; ++i) {
+        uint32_t d = decideHost[i];
+        if ((d >> 6) == BT_DECIDE_HOST) {
+            decideHost[i] = (uint8_t)(d = resolveHost(packetOf(i), d & 63u));
+            if (verdictHost && (d >> 6) == BT_DECIDE_PASS) verdictHost[i / 64] |= 1ull << (i % 64);
+        }
+        const uint32_t code = d >> 6, slot = d & 63u;
+        if (code == BT_DECIDE_THROW) {
+            flush();
+            rethrow(program_[slot]);
+        }
+        ++counted;
+        if (code == BT_DECIDE_PASS) {
+            ++passed;
+            pass.push_back(i);
+        } else {
+            ++rejected[slot];
+        }
+    }
+    flush();
+    return pass;
+}
+
 }  // namespace gpu
 }  // namespace beatrice

@@ -61,6 +61,14 @@ public:
     };
     Verdicts classify(const std::vector<Packet>& packets);
 
+    // Zero-copy form over frames the device already sees (a capture ring registered
+    // with bt_host_register): runs parse+filter over `batch` into `out` (device-visible
+    // memory; out.decide is required, out.verdict optional), then — on the host views
+    // decideHost / verdictHost of those outputs — resolves PAYLOAD / CUSTOM slots with
+    // packetOf(i), updates stats and throws like classify. Returns the pass indices.
+    std::vector<uint32_t> classifyMapped(const bt_batch& batch, const bt_outputs& out, uint8_t* decideHost,
+                                         uint64_t* verdictHost, const std::function<Packet(uint32_t)>& packetOf);
+
     // Evaluation order of the enabled filters (names), as applyFilters uses it.
     std::vector<std::string> evaluationOrder();
     bt_ctx* context() const { return ctx_; }

@@ -30,6 +30,9 @@ def lib() -> ctypes.CDLL:
         L.bt_synth_fill.restype = ctypes.c_int
         L.bt_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int]
+        L.bt_synth_tpv3_pack.restype = ctypes.c_uint64
+        L.bt_synth_tpv3_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -75,3 +78,26 @@ def pack_frames(frames, align: int = 1, shift: int = 0):
     for o, f in zip(offs, frames):
         data[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
     return data, make_desc(offs, lens)
+
+
+TPV3_BLOCK = 1 << 20   # 1 MiB blocks: ~6.9k 64-B frames or ~680 1500-B frames per block
+
+
+def tpv3_ring(data: np.ndarray, desc: np.ndarray, block_size: int = TPV3_BLOCK, n_blocks: int | None = None):
+    """Packs a capture into a TPACKET_V3 RX-ring image laid out exactly as the kernel
+    writes one (bt_synth_tpv3_pack). Returns (ring uint8, ring_desc uint64, blocks used);
+    ring_desc[i] = BT_DESC(ring offset, snaplen) of packed frame i. With n_blocks None
+    the ring is sized to hold every frame; otherwise packing stops when it is full."""
+    L = lib()
+    n = len(desc)
+    if n_blocks is None:
+        used = ctypes.c_uint64()
+        L.bt_synth_tpv3_pack(data.ctypes.data, desc.ctypes.data, n, block_size, None, 1 << 40, None,
+                             ctypes.byref(used))
+        n_blocks = max(1, used.value)
+    ring = np.zeros(n_blocks * block_size, dtype=np.uint8)
+    ring_desc = np.empty(max(n, 1), dtype=np.uint64)
+    used = ctypes.c_uint64()
+    k = L.bt_synth_tpv3_pack(data.ctypes.data, desc.ctypes.data, n, block_size, ring.ctypes.data, n_blocks,
+                             ring_desc.ctypes.data, ctypes.byref(used))
+    return ring, ring_desc[:k], int(used.value)

@@ -304,6 +304,37 @@ int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint3
 int  bt_host_register(bt_ctx* ctx, void* host, uint64_t bytes, void** dev_alias);
 int  bt_host_unregister(bt_ctx* ctx, void* host);
 
+/* ---- capture-ring ingest: AF_PACKET TPACKET_V3 ---------------
+ * Replaces the per-packet recv() + heap copy + queue push of the reference's
+ * AF_PacketBackend::packetProcessingLoop (src/AF_PacketBackend.cpp:318-363). A
+ * PACKET_RX_RING of n_blocks blocks of block_size bytes (linux/if_packet.h,
+ * struct tpacket_req3) is mmap'd once; the kernel fills a block with a chain of
+ * tpacket3_hdr frames and flips block_status to TP_STATUS_USER. The walker turns
+ * ready blocks into bt_pkt_desc entries whose offsets are relative to the ring base,
+ * so the ring itself (registered with bt_host_register, or copied to the device) is
+ * the bt_batch.base: the frames are never copied on the host. */
+typedef struct bt_tpv3_ring {
+    void* base;                    /* host address of the mmap'd ring */
+    uint64_t block_size;           /* tpacket_req3.tp_block_size      */
+    uint32_t n_blocks;             /* tpacket_req3.tp_block_nr        */
+    uint32_t reserved;
+} bt_tpv3_ring;
+
+/* Takes the ready blocks first_block, first_block+1, ... (mod n_blocks): at most
+ * max_blocks of them, stopping at the first block the kernel still owns or whose
+ * packets would overflow `cap` descriptors. Writes one descriptor per frame in ring
+ * order, BT_DESC(block * block_size + frame offset + tp_mac, min(tp_snaplen, 65535)),
+ * and the counts. Blocks are walked in parallel on ctx's host pool (ctx may be NULL:
+ * single-threaded, no GPU needed). A malformed block (a frame chain leaving the block)
+ * returns BT_E_INVALID_ARGUMENT and takes nothing. The blocks stay owned by the
+ * caller until bt_ring_release_tpv3. */
+int  bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block,
+                       uint32_t max_blocks, bt_pkt_desc* desc, uint32_t cap,
+                       uint32_t* n_desc, uint32_t* n_blocks_taken);
+/* Hands `count` blocks starting at first_block back to the kernel (TP_STATUS_KERNEL,
+ * release-ordered). Call it once the device has finished reading them. */
+int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);
+
 /* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
 int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);
 int  bt_dev_free(bt_ctx* ctx, void* p);

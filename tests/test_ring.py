@@ -1,0 +1,168 @@
+"""CPU: AF_PACKET TPACKET_V3 capture-ring ingest — the block walker
+bt_ring_walk_tpv3 / bt_ring_release_tpv3 and the ring-image packer, against
+
+  * tests/golden/ring_lo.npz, a ring WRITTEN BY THE LINUX KERNEL on `lo`
+    (tests/golden/make_ring_fixture.py) with the compiled reference's records and
+    PacketFilter outcomes for every frame in it;
+  * tests/ring_util.walk_tpv3, a plain-Python restatement of the walk;
+  * a live ring on `lo` when this process may open AF_PACKET sockets.
+
+None of these need a GPU: the walker is host code (ctx = NULL)."""
+import mmap
+import os
+import socket
+import struct
+import time
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+import ring_util as ru
+from beatrice_amd import abi, synth
+from conftest import GOLDEN
+from golden_util import compare_decisions
+
+
+def _fixture():
+    g = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
+    bs, nb = (int(x) for x in g["geometry"])
+    return g, bs, nb
+
+
+def test_walk_kernel_ring_matches_python_walk():
+    g, bs, nb = _fixture()
+    ring = g["ring"].copy()
+    desc, taken = abi.ring_walk_tpv3(ring, bs, nb)
+    ref, ref_taken = ru.walk_tpv3(ring, bs, nb)
+    assert taken == ref_taken == nb
+    assert np.array_equal(desc, ref) and np.array_equal(desc, g["desc"])
+    assert len(desc) > 900
+
+
+def test_kernel_ring_layout_is_what_the_packer_writes():
+    g, bs, nb = _fixture()
+    assert ru.layout_violations(g["ring"], bs, nb) == []
+    frames = np.array(g["ring"])
+    ring, rdesc, used = synth.tpv3_ring(frames, g["desc"], block_size=bs)
+    assert ru.layout_violations(ring, bs, used) == []
+    assert np.array_equal(ru.walk_tpv3(ring, bs, used)[0], rdesc)
+
+
+def test_oracle_on_kernel_ring_matches_reference():
+    """The reference's own outputs on kernel-captured frames pin the oracle there too."""
+    g, bs, nb = _fixture()
+    import json
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    info = man["rings"]["ring_lo"]
+    n = len(g["desc"])
+    rec, _, _ = ol.oracle_run(g["ring"], g["desc"], n, None, parse=True)
+    assert np.array_equal(rec, g["rec"])
+    for s in info["filter_sets"]:
+        filters = man["filter_sets"][s]
+        _, dec, _ = ol.oracle_run(g["ring"], g["desc"], n, filters, parse=False)
+        compare_decisions(dec, g[f"code__{s}"], g[f"src__{s}"], filters, where=f"ring_lo/{s}")
+
+
+@pytest.mark.parametrize("cfg,block", [(synth.C2, 1 << 16), (synth.C3, 1 << 17), (synth.C4, 1 << 20)])
+def test_packed_ring_round_trip(cfg, block):
+    data, desc = synth.capture(cfg, 20000, seed=5)
+    ring, rdesc, used = synth.tpv3_ring(data, desc, block_size=block)
+    assert len(rdesc) == len(desc) and used > 1
+    got, taken = abi.ring_walk_tpv3(ring, block, used)
+    assert taken == used and np.array_equal(got, rdesc)
+    off, ln = synth.desc_off(got), synth.desc_len(got)
+    assert np.array_equal(ln, synth.desc_len(desc))
+    src = synth.desc_off(desc)
+    for i in np.random.default_rng(0).integers(0, len(desc), 300):
+        assert bytes(ring[off[i]:off[i] + ln[i]]) == bytes(data[src[i]:src[i] + ln[i]])
+
+
+def test_walk_limits_wrap_and_release():
+    data, desc = synth.capture(synth.C3, 6000, seed=9)
+    bs = 1 << 16
+    ring, rdesc, used = synth.tpv3_ring(data, desc, block_size=bs)
+    per_block = [npk for _, npk, _, _ in ru.frame_headers(ring, bs, used)]
+    start = np.concatenate([[0], np.cumsum(per_block)])
+    # max_blocks and cap stop at whole blocks
+    d, t = abi.ring_walk_tpv3(ring, bs, used, first=0, max_blocks=3)
+    assert t == 3 and np.array_equal(d, rdesc[:start[3]])
+    d, t = abi.ring_walk_tpv3(ring, bs, used, first=0, cap=int(start[2]) + 1)
+    assert t == 2 and len(d) == start[2]
+    # starting mid-ring wraps round to block 0
+    d, t = abi.ring_walk_tpv3(ring, bs, used, first=used - 2, max_blocks=4)
+    assert t == 4 and np.array_equal(d, np.concatenate([rdesc[start[used - 2]:], rdesc[:start[2]]]))
+    # released blocks belong to the kernel again: the walk stops there
+    abi.ring_release_tpv3(ring, bs, used, 1, 2)
+    d, t = abi.ring_walk_tpv3(ring, bs, used, first=0)
+    assert t == 1 and len(d) == start[1]
+    d, t = abi.ring_walk_tpv3(ring, bs, used, first=1)
+    assert t == 0 and len(d) == 0
+    assert np.all(ring.reshape(used, bs)[1:3, 8:12].view(np.uint32) == ru.TP_STATUS_KERNEL)
+
+
+def test_malformed_ring_is_rejected():
+    data, desc = synth.capture(synth.C2, 3000, seed=3)
+    bs = 1 << 16
+    ring, _, used = synth.tpv3_ring(data, desc, block_size=bs)
+    _, _, _, frames = next(ru.frame_headers(ring, bs, used))
+    bad = ring.copy()
+    off = bs + frames[5][0]        # frame 5 of block 1 points far outside the block
+    bad[off:off + 4] = np.frombuffer(struct.pack("<I", bs), np.uint8)
+    with pytest.raises(abi.BtError, match="frame chain leaves the block"):
+        abi.ring_walk_tpv3(bad, bs, used)
+    bad = ring.copy()              # first-frame offset past the block
+    bad[bs + 16:bs + 20] = np.frombuffer(struct.pack("<I", bs + 8), np.uint8)
+    with pytest.raises(abi.BtError, match="first frame outside block"):
+        abi.ring_walk_tpv3(bad, bs, used)
+    with pytest.raises(abi.BtError):
+        abi.ring_walk_tpv3(ring, bs, used, first=used)
+
+
+def _can_raw():
+    try:
+        socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3)).close()
+        return True
+    except (PermissionError, OSError):
+        return False
+
+
+@pytest.mark.skipif(not _can_raw(), reason="no CAP_NET_RAW: cannot open an AF_PACKET ring")
+def test_live_ring_on_loopback():
+    bs, nb = 1 << 16, 8
+    s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3))
+    s.setsockopt(263, 10, 2)                                           # PACKET_VERSION = TPACKET_V3
+    s.setsockopt(263, 5, struct.pack("7I", bs, nb, 2048, bs * nb // 2048, 5, 0, 0))   # PACKET_RX_RING
+    s.bind(("lo", 3))
+    m = mmap.mmap(s.fileno(), bs * nb)
+    try:
+        u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        marks = [b"bt-ring-%04d" % i for i in range(50)]
+        for i, mk in enumerate(marks):
+            u.sendto(mk * (1 + i % 7), ("127.0.0.1", 4000 + i))
+        u.close()
+        time.sleep(0.1)
+        ring = np.frombuffer(m, dtype=np.uint8)
+        desc, taken = abi.ring_walk_tpv3(ring, bs, nb)
+        assert taken >= 1 and np.array_equal(desc, ru.walk_tpv3(ring, bs, nb)[0])
+        frames = [bytes(ring[o:o + n]) for o, n in zip(synth.desc_off(desc), synth.desc_len(desc))]
+        for mk in marks:
+            assert any(mk in f for f in frames), mk
+        abi.ring_release_tpv3(ring, bs, nb, 0, taken)
+        del ring
+    finally:
+        m.close()
+        s.close()
+
+
+CAPTURE_BIN = os.path.join(os.path.dirname(GOLDEN), "cpp", "test_capture")
+
+
+@pytest.mark.skipif(not _can_raw(), reason="no CAP_NET_RAW: cannot open an AF_PACKET ring")
+def test_cpp_backend_on_loopback():
+    """GpuAfPacketBackend (ICaptureBackend drop-in) on a live TPACKET_V3 ring on lo."""
+    import subprocess
+    assert os.path.exists(CAPTURE_BIN), "tests/cpp/test_capture not built (make -C tests/cpp)"
+    r = subprocess.run([CAPTURE_BIN, "backend"], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
