@@ -53,12 +53,19 @@ if a.tpacket:
         d_dec, d_ver = ctx.register(h_dec), ctx.register(h_ver)
         d_rec = ctx.register(h_rec) if rec else None
 
-        def one_pass():
+        counts = []
+
+        def one_pass(walk=True):
             start, tile = 0, 0
             for k in range(nbat):
-                got, taken = abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B),
-                                                ctx=ctx, out=h_desc[start:])
-                cnt = len(got)
+                if walk:
+                    got, taken = abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B),
+                                                    ctx=ctx, out=h_desc[start:])
+                    cnt = len(got)
+                    if len(counts) < nbat:
+                        counts.append(cnt)
+                else:
+                    cnt = counts[k]
                 batch = abi.Batch(d_ring, d_desc + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
                 outs = abi.Outputs(d_rec + 6144 * tile if rec else None, cnt, d_ver + 8 * tile, d_dec + 64 * tile,
                                    None, None)
@@ -74,6 +81,11 @@ if a.tpacket:
             done = one_pass()
             best = min(best, time.perf_counter() - t0)
         assert done == n
+        kbest = 1e9
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            one_pass(walk=False)
+            kbest = min(kbest, time.perf_counter() - t0)
         t0 = time.perf_counter()
         for k in range(nbat):
             abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
@@ -84,6 +96,7 @@ if a.tpacket:
         print(json.dumps({"config": a.config, "mode": "tpacket_v3 ring, zero-copy, " + mode, "packets": n,
                           "ring_blocks": used, "block_bytes": bs, "batch_blocks": B, "seconds": round(best, 4),
                           "mpps": round(n / best / 1e6, 1), "walk_only_mpps": round(n / walk / 1e6, 1),
+                          "kernels_only_mpps": round(n / kbest / 1e6, 1),
                           "pcie_read_GBps": round(pcie / best / 1e9, 2),
                           "pcie_write_GBps": round(n * (1.125 + (96 if rec else 0)) / best / 1e9, 2)}), flush=True)
         for h in (h_dec, h_ver) + ((h_rec,) if rec else ()):

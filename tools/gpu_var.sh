@@ -1,3 +1,2 @@
 mkdir -p gpurun_out
-timeout -k 10 120 ./tools/ringwalk/walk_scaling 3 8000000 1048576 16 pool || exit 3
-for cfg in c2 c3 c4; do timeout -k 10 300 python tools/e2e.py --config $cfg --tpacket --host-threads 16 > gpurun_out/tp_$cfg.jsonl || exit 5; cat gpurun_out/tp_$cfg.jsonl; done
+for cfg in c2 c3; do for bb in 128 512; do timeout -k 10 300 python tools/e2e.py --config $cfg --tpacket --host-threads 16 --ring-batch-blocks $bb --reps 3 || exit 5; done; done
