@@ -20,7 +20,8 @@ BT_MAX_FILTERS = 64
 # FilterType order (reference include/beatrice/PacketFilter.hpp:17-24)
 BPF, PROTOCOL, IP_RANGE, PORT_RANGE, PAYLOAD, CUSTOM = range(6)
 DECIDE_PASS, DECIDE_REJECT, DECIDE_THROW, DECIDE_HOST = range(4)
-KINDS = ["TRUE", "FALSE", "BPF", "PROTO_EQ", "PROTO_NZ", "IP_MASK", "PORT", "IP_THROW", "PORT_THROW", "HOST"]
+KINDS = ["TRUE", "FALSE", "BPF", "PROTO_EQ", "PROTO_NZ", "IP_MASK", "PORT", "IP_THROW", "PORT_THROW", "HOST",
+         "PAYLOAD"]
 
 L_ETH, L_VLAN0, L_VLAN1, L_IPV4, L_IPV6, L_TCP, L_UDP, L_ICMP = (1 << i for i in range(8))
 
@@ -66,6 +67,7 @@ OPT_NT_STORES = 0x20
 OPT_NT_LOADS = 0x40
 OPT_CACHE_DEFAULT = 0x80
 OPT_SPIN_SYNC = 0x100
+OPT_PAYLOAD_HOST = 0x200
 
 
 DESC_PACKED, DESC_XDP = 0, 1
@@ -93,6 +95,7 @@ EXPORTS = [
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
+    "bt_payload_dfa_compile", "bt_payload_dfa_search", "bt_payload_dfa_eval",
 ]
 
 _lib = None
@@ -136,6 +139,9 @@ def lib() -> ctypes.CDLL:
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
                                              ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_ring_release_tpv3": (ctypes.c_int, [ctypes.POINTER(Tpv3Ring), u32, u32]),
+        "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
+        "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
+        "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -325,6 +331,32 @@ def ring_walk_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int 
 def ring_release_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int, count: int):
     r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
     _check(lib().bt_ring_release_tpv3(ctypes.byref(r), first, count))
+
+
+def payload_dfa(expr: str):
+    """bt_payload_dfa_compile: the DFA blob (bytes), None when the expression is outside
+    the GPU subset (it stays on the host), or raises BtError if std::regex rejects it."""
+    L = lib()
+    e = expr.encode("latin-1")
+    size = ctypes.c_uint32()
+    rc = L.bt_payload_dfa_compile(e, None, 0, ctypes.byref(size))
+    if rc == 11:
+        return None
+    if rc:
+        raise BtError(rc, f"bt_payload_dfa_compile({expr!r}) = {rc}")
+    buf = ctypes.create_string_buffer(size.value)
+    _check(L.bt_payload_dfa_compile(e, buf, size.value, ctypes.byref(size)))
+    return buf.raw
+
+
+def payload_dfa_search(blob: bytes, s: bytes) -> bool:
+    return bool(lib().bt_payload_dfa_search(blob, s, len(s)))
+
+
+def payload_dfa_eval(blob: bytes, frame) -> bool:
+    """applyPayloadFilter(frame) for the compiled (non-empty) expression, on the host."""
+    f = bytes(frame)
+    return bool(lib().bt_payload_dfa_eval(blob, f, len(f)))
 
 
 def untile_records(buf: np.ndarray, n: int, planes: bool = False) -> np.ndarray:

@@ -34,7 +34,11 @@ struct MainArgs {
     uint32_t* tile_pass;       // per-tile pass counts (compaction input)
     uint32_t blocked;          // tile order: 0 cyclic, 1 one contiguous range per wavefront
     uint32_t nt;               // bit0 non-temporal record stores, bit1 non-temporal header loads
+    const uint8_t* dfa;        // PAYLOAD DFA pool (device), copied to dynamic LDS per block
+    uint32_t dfa_bytes;        // 0: the program has no BT_K_PAYLOAD slot
 };
+
+constexpr uint32_t kDfaPoolMax = 16384;   // bytes of DFA tables per program (LDS budget)
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;

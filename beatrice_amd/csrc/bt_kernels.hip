@@ -195,6 +195,51 @@ __device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_
     }
 }
 
+// PAYLOAD filter on the GPU (BT_K_PAYLOAD): applyPayloadFilter's window
+// (src/PacketFilter.cpp:293-309: IPv4 only, bytes [14 + 4*IHL, +min(len - that, 100)))
+// run through the host-compiled byte DFA (bt_regex_dfa.cpp; blob layout there) that
+// sits in this block's dynamic LDS. The window lies beyond the header image, so the
+// lane stages it into its own LDS row first (the row is the lane's alone once PARSE
+// is done): <= 8 16-B loads, then one class lookup + one transition per byte.
+__device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
+                                                 uint64_t frame_off, uint32_t len, const uint32_t* w0,
+                                                 uint32_t& staged_sh) {
+    if (!(len >= 34u && be16_of(w0, 12) == 0x0800u)) return 0u;
+    const uint32_t po = 14u + (byte_of(w0, 14) & 15u) * 4u;
+    if (len <= po) return 0u;
+    const uint32_t L = min(len - po, 100u);
+    if (staged_sh == ~0u) {
+        const uint64_t start = frame_off + po;
+        const uint64_t al = start & ~15ull;
+        staged_sh = (uint32_t)(start & 15ull);
+        const uint32_t nch = (staged_sh + L + 15u) >> 4;   // <= 8: 128 B of the 132-B row
+        // one chunk in flight at a time: keeps the main loop's register budget (a fully
+        // unrolled staging held 32 more VGPRs and cost a wave of occupancy)
+#pragma unroll 1
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint64_t g = al + 16ull * c;
+            const uint4 v = g + 16ull <= a.bytes ? ld16(a.base + g, a.nt & 2u) : make_uint4(0, 0, 0, 0);
+            row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+        }
+    }
+    const uint8_t* pay = reinterpret_cast<const uint8_t*>(row) + staged_sh;
+    const uint32_t C = *reinterpret_cast<const uint16_t*>(blob + 2);
+    const uint32_t S = *reinterpret_cast<const uint16_t*>(blob);
+    const uint8_t* cls = blob + 8;
+    const uint8_t* acc = blob + 264;
+    const uint8_t* next = acc + ((S + 3u) & ~3u);
+    uint32_t q = blob[4];
+    uint32_t f = acc[q];
+    if (f & 1u) return 1u;
+    if (f & 4u) return 0u;
+    for (uint32_t i = 0; i < L; ++i) {
+        q = next[q * C + cls[pay[i]]];
+        f = acc[q];
+        if (f & 5u) return f & 1u;
+    }
+    return (f >> 1) & 1u;
+}
+
 // Header windows of one 64-packet tile in flight in registers (LOAD stage).
 //  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
 //  descriptors:  round A = the first 64 B (chunks 0..3) of every packet's 16-B-aligned
@@ -339,10 +384,17 @@ template <int FIXED_LOG2, int REC, bool FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
     __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRowDwords];
+    extern __shared__ uint4 dyn_lds[];   // PAYLOAD DFA pool (a.dfa_bytes), else empty
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = threadIdx.x >> 6;
     uint32_t* img = lds_all + wid * (kWave * kRowDwords);
     const uint32_t* row = img + lane * kRowDwords;
+    if (FILTER && a.dfa_bytes) {   // uniform: the whole block copies the pool once
+        const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
+        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
+        __syncthreads();
+    }
+    const uint8_t* dfa_lds = reinterpret_cast<const uint8_t*>(dyn_lds);
 
     const uint32_t total_waves = gridDim.x * kWavesPerBlock;
 
@@ -434,9 +486,16 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             x.l4_ok = (x.proto == 6 && len >= 54) || (x.proto == 17 && len >= 42);
             uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
             bool open = live;
+            uint32_t staged_sh = ~0u;   // payload window not staged yet
             for (uint32_t f = 0; f < prog.n; ++f) {
                 if (__ballot(open) == 0ull) break;
-                const uint32_t r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
+                uint32_t r;
+                if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
+                    r = open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRowDwords, my_off, len, w0,
+                                            staged_sh)
+                             : 0u;
+                else
+                    r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
                 if (open && r != 1u) {
                     code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
                     slot = f;
@@ -537,16 +596,26 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
 // One residency wave of blocks: the persistent grid-stride loop then has no tail of
 // late blocks (measured: 2x residency cost C3 11 %).
 template <class K>
-int resident_grid(K kernel) {
-    static int blocks = 0;   // per kernel instantiation
-    if (!blocks) {
+int resident_grid(K kernel, uint32_t dyn) {
+    static int blocks = 0;   // per kernel instantiation, no dynamic LDS
+    auto query = [&](uint32_t bytes) {
         int dev = 0, per_cu = 0;
         hipDeviceProp_t prop;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu < 1)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, bytes) != hipSuccess || per_cu < 1)
             return 1024;
-        blocks = prop.multiProcessorCount * per_cu;
+        return prop.multiProcessorCount * per_cu;
+    };
+    if (dyn) {   // a PAYLOAD program: occupancy depends on its DFA pool size
+        static uint32_t last_dyn = 0;
+        static int last_blocks = 0;
+        if (dyn != last_dyn) {
+            last_blocks = query(dyn);
+            last_dyn = dyn;
+        }
+        return last_blocks;
     }
+    if (!blocks) blocks = query(0);
     return blocks;
 }
 
@@ -554,9 +623,10 @@ template <int FL, int REC, bool F>
 void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st) {
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     auto go = [&](auto kernel) {
-        int g = grid > 0 ? grid : resident_grid(kernel);
+        const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
+        int g = grid > 0 ? grid : resident_grid(kernel, dyn);
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
-        hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), 0, st, a, prog);
+        hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
     };
     if (pf) go(bt_parse_filter_main<FL, REC, F, true>);
     else go(bt_parse_filter_main<FL, REC, F, false>);

@@ -1,0 +1,623 @@
+// bt_regex_dfa.cpp — PAYLOAD filter regex -> byte DFA for the GPU.
+//
+// The reference evaluates a PAYLOAD filter as
+//     std::regex_search(std::string(payload, min(len - off, 100)), std::regex(expr))
+// (src/PacketFilter.cpp:288-321) with libstdc++'s ECMAScript grammar. This file
+// compiles the regular subset of that grammar into a DFA over bytes that answers the
+// same question — "does any substring match?" — in one pass:
+//
+//   * unanchored search: the NFA start is re-injected at every position, so a DFA
+//     state is the set of partial matches alive at that position;
+//   * `^` is an assertion true only at position 0, `$` only at the end (no multiline,
+//     as regex_search with default flags); each DFA state records whether a match is
+//     complete now (search succeeds: stop), complete if the input ends here, or
+//     impossible from here on (stop);
+//   * character sets follow libstdc++ exactly as measured (`.` = all but \n \r; \s
+//     = 09-0d, 20; \w / \d ASCII; ranges compared as signed char).
+//
+// Anything outside the modelled subset — backreferences, lookaheads, \b \B, \c \u,
+// POSIX [[:classes:]], escapes of letters libstdc++ treats idiosyncratically, more
+// than 255 DFA states — returns BT_E_NOT_IMPLEMENTED and the filter stays on the
+// host (std::regex), as before. Only patterns std::regex itself accepts reach here
+// (the filter compiler probes first), so the parser never needs error recovery for
+// patterns the reference rejects. Agreement with std::regex is fuzzed in
+// tests/cpp/test_regex_dfa.cpp.
+//
+// Blob layout (4-B aligned, little endian), shared by the host executor below and
+// the kernel (bt_kernels.hip, eval_payload):
+//   u16 n_states, u16 n_classes, u8 init, u8 pad[3]
+//   u8  cls[256]                   byte -> class
+//   u8  acc[n_states] (pad to 4)   bit0 match complete (stop: true)
+//                                  bit1 match complete if the input ends here
+//                                  bit2 no match possible from here (stop: false)
+//                                  bit3 (init only) match on the empty input
+//   u8  next[n_states * n_classes]
+#include <algorithm>
+#include <bitset>
+#include <cstring>
+#include <map>
+#include <regex>
+#include <string>
+#include <vector>
+
+#include "beatrice_gpu.h"
+
+namespace {
+
+using Set = std::bitset<256>;
+
+constexpr int kMaxNfa = 6000;
+constexpr int kMaxDfa = 255;
+constexpr int kMaxRepeat = 100;   // payload windows are <= 100 bytes
+
+// ------------------------------------------------------------------ parse -> AST
+
+struct Node {
+    enum T { SET, CAT, ALT, REP, BOL, EOL, EMPTY } t;
+    Set set;
+    std::vector<int> kids;
+    int lo = 0, hi = 0;   // REP: hi < 0 = unbounded
+};
+
+struct Unsupported {};
+
+class Parser {
+public:
+    explicit Parser(const std::string& p) : p_(p) {}
+    std::vector<Node> nodes;
+
+    int parse() {
+        const int r = disjunction();
+        if (i_ != p_.size()) throw Unsupported{};
+        return r;
+    }
+
+private:
+    const std::string& p_;
+    size_t i_ = 0;
+
+    bool more() const { return i_ < p_.size(); }
+    unsigned char peek() const { return (unsigned char)p_[i_]; }
+
+    int add(Node n) {
+        nodes.push_back(std::move(n));
+        return (int)nodes.size() - 1;
+    }
+    int set_node(const Set& s) {
+        Node n{Node::SET};
+        n.set = s;
+        return add(n);
+    }
+
+    int disjunction() {
+        std::vector<int> alts{alternative()};
+        while (more() && peek() == '|') {
+            ++i_;
+            alts.push_back(alternative());
+        }
+        if (alts.size() == 1) return alts[0];
+        Node n{Node::ALT};
+        n.kids = alts;
+        return add(n);
+    }
+
+    int alternative() {
+        std::vector<int> terms;
+        while (more() && peek() != '|' && peek() != ')') terms.push_back(term());
+        if (terms.empty()) return add(Node{Node::EMPTY});
+        if (terms.size() == 1) return terms[0];
+        Node n{Node::CAT};
+        n.kids = terms;
+        return add(n);
+    }
+
+    int term() {
+        const unsigned char c = peek();
+        if (c == '^' || c == '$') {
+            ++i_;
+            if (more() && (peek() == '*' || peek() == '+' || peek() == '?' || peek() == '{'))
+                throw Unsupported{};   // quantified assertion
+            return add(Node{c == '^' ? Node::BOL : Node::EOL});
+        }
+        int a = atom();
+        while (more()) {   // libstdc++ accepts stacked quantifiers (a**): apply each in turn
+            int lo, hi;
+            if (!quantifier(lo, hi)) break;
+            Node n{Node::REP};
+            n.kids = {a};
+            n.lo = lo;
+            n.hi = hi;
+            a = add(n);
+        }
+        return a;
+    }
+
+    bool number(int& v) {
+        if (!more() || !isdigit(peek())) return false;
+        long x = 0;
+        while (more() && isdigit(peek())) {
+            x = x * 10 + (peek() - '0');
+            if (x > 100000) throw Unsupported{};
+            ++i_;
+        }
+        v = (int)x;
+        return true;
+    }
+
+    bool quantifier(int& lo, int& hi) {
+        const unsigned char c = peek();
+        if (c == '*') { lo = 0; hi = -1; ++i_; }
+        else if (c == '+') { lo = 1; hi = -1; ++i_; }
+        else if (c == '?') { lo = 0; hi = 1; ++i_; }
+        else if (c == '{') {
+            ++i_;
+            if (!number(lo)) throw Unsupported{};
+            hi = lo;
+            if (more() && peek() == ',') {
+                ++i_;
+                if (!number(hi)) hi = -1;
+            }
+            if (!more() || peek() != '}') throw Unsupported{};
+            ++i_;
+            if (lo > kMaxRepeat || hi > kMaxRepeat) throw Unsupported{};
+        } else {
+            return false;
+        }
+        if (more() && peek() == '?') ++i_;   // lazy: the same language
+        return true;
+    }
+
+    static Set range(int a, int b) {
+        Set s;
+        for (int x = a; x <= b; ++x) s.set(x & 0xFF);
+        return s;
+    }
+    static Set digit() { return range('0', '9'); }
+    static Set word() { return range('0', '9') | range('A', 'Z') | range('a', 'z') | range('_', '_'); }
+    static Set space() { return range(9, 13) | range(' ', ' '); }
+
+    static int hexval(unsigned char c) {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    }
+
+    // After a backslash. Returns true with `single` set for a one-byte escape, or false
+    // with `cls` set for a class escape (\d \w \s and negations).
+    bool escape(bool in_class, int& single, Set& cls) {
+        if (!more()) throw Unsupported{};
+        const unsigned char c = peek();
+        ++i_;
+        switch (c) {
+        case 'd': cls = digit(); return false;
+        case 'D': cls = ~digit(); return false;
+        case 'w': cls = word(); return false;
+        case 'W': cls = ~word(); return false;
+        case 's': cls = space(); return false;
+        case 'S': cls = ~space(); return false;
+        case 't': single = 9; return true;
+        case 'n': single = 10; return true;
+        case 'v': single = 11; return true;
+        case 'f': single = 12; return true;
+        case 'r': single = 13; return true;
+        case 'b':
+            if (!in_class) throw Unsupported{};   // word boundary
+            single = 8;
+            return true;
+        case '0':
+            if (more() && isdigit(peek())) throw Unsupported{};
+            single = 0;
+            return true;
+        case 'x': {
+            if (i_ + 2 > p_.size()) throw Unsupported{};
+            const int h = hexval((unsigned char)p_[i_]), l = hexval((unsigned char)p_[i_ + 1]);
+            if (h < 0 || l < 0) throw Unsupported{};
+            i_ += 2;
+            single = h * 16 + l;
+            return true;
+        }
+        default:
+            if (isalnum(c) || c == '_') throw Unsupported{};   // \1.. \c \u \B and letters
+            single = c;                                         // identity escape
+            return true;
+        }
+    }
+
+    Set char_class() {   // after '['
+        bool neg = false;
+        if (more() && peek() == '^') {
+            neg = true;
+            ++i_;
+        }
+        Set s;
+        bool first = true;
+        while (true) {
+            if (!more()) throw Unsupported{};
+            unsigned char c = peek();
+            if (c == ']') {
+                ++i_;
+                break;
+            }
+            if (c == '[') throw Unsupported{};   // [[:alpha:]] and friends
+            int lo = -1;
+            Set cls;
+            ++i_;
+            if (c == '\\') {
+                int single = 0;
+                if (escape(true, single, cls)) lo = single;
+            } else {
+                lo = c;
+            }
+            (void)first;
+            first = false;
+            if (lo < 0) {   // class escape: a following '-' is literal or an error
+                if (more() && peek() == '-' && i_ + 1 < p_.size() && p_[i_ + 1] != ']') throw Unsupported{};
+                s |= cls;
+                continue;
+            }
+            if (more() && peek() == '-' && i_ + 1 < p_.size() && p_[i_ + 1] != ']') {
+                ++i_;
+                unsigned char d = peek();
+                ++i_;
+                int hi;
+                if (d == '\\') {
+                    int single = 0;
+                    Set c2;
+                    if (!escape(true, single, c2)) throw Unsupported{};
+                    hi = single;
+                } else if (d == '[') {
+                    throw Unsupported{};
+                } else {
+                    hi = d;
+                }
+                // libstdc++ compares range ends as (signed) char
+                const int slo = (int)(signed char)lo, shi = (int)(signed char)hi;
+                if (slo > shi) throw Unsupported{};   // std::regex rejects these itself
+                for (int v = slo; v <= shi; ++v) s.set((unsigned char)(signed char)v);
+            } else {
+                s.set(lo);
+            }
+        }
+        return neg ? ~s : s;
+    }
+
+    int atom() {
+        const unsigned char c = peek();
+        switch (c) {
+        case '(': {
+            ++i_;
+            if (more() && peek() == '?') {
+                if (i_ + 1 < p_.size() && p_[i_ + 1] == ':') i_ += 2;
+                else throw Unsupported{};   // lookahead
+            }
+            const int r = disjunction();
+            if (!more() || peek() != ')') throw Unsupported{};
+            ++i_;
+            return r;
+        }
+        case '.': {
+            ++i_;
+            Set s;
+            s.set();
+            s.reset('\n');
+            s.reset('\r');
+            return set_node(s);
+        }
+        case '[':
+            ++i_;
+            return set_node(char_class());
+        case '\\': {
+            ++i_;
+            int single = 0;
+            Set cls;
+            if (escape(false, single, cls)) {
+                Set s;
+                s.set(single);
+                return set_node(s);
+            }
+            return set_node(cls);
+        }
+        case '*': case '+': case '?': case '{': case ')': case '|':
+            throw Unsupported{};
+        default: {
+            ++i_;
+            Set s;
+            s.set(c);
+            return set_node(s);
+        }
+        }
+    }
+};
+
+// ------------------------------------------------------------------ AST -> NFA
+
+struct NState {
+    enum T : uint8_t { SET, EPS, SPLIT, BOL, EOL, MATCH } t;
+    int set_id = -1;
+    int out = -1, out1 = -1;
+};
+
+class Nfa {
+public:
+    std::vector<NState> st;
+    std::vector<Set> sets;
+
+    int make(NState::T t) {
+        if ((int)st.size() >= kMaxNfa) throw Unsupported{};
+        st.push_back(NState{t});
+        return (int)st.size() - 1;
+    }
+
+    // fragment: entry state, exit EPS state (out unpatched)
+    std::pair<int, int> build(const std::vector<Node>& ast, int id) {
+        const Node& n = ast[id];
+        switch (n.t) {
+        case Node::SET: {
+            const int s = make(NState::SET), e = make(NState::EPS);
+            st[s].set_id = (int)sets.size();
+            sets.push_back(n.set);
+            st[s].out = e;
+            return {s, e};
+        }
+        case Node::EMPTY: {
+            const int e = make(NState::EPS);
+            return {e, e};
+        }
+        case Node::BOL:
+        case Node::EOL: {
+            const int s = make(n.t == Node::BOL ? NState::BOL : NState::EOL), e = make(NState::EPS);
+            st[s].out = e;
+            return {s, e};
+        }
+        case Node::CAT: {
+            auto f = build(ast, n.kids[0]);
+            for (size_t k = 1; k < n.kids.size(); ++k) {
+                auto g = build(ast, n.kids[k]);
+                st[f.second].out = g.first;
+                f.second = g.second;
+            }
+            return f;
+        }
+        case Node::ALT: {
+            const int e = make(NState::EPS);
+            int entry = -1, prev_split = -1;
+            for (size_t k = 0; k < n.kids.size(); ++k) {
+                auto g = build(ast, n.kids[k]);
+                st[g.second].out = e;
+                if (k + 1 < n.kids.size()) {
+                    const int sp = make(NState::SPLIT);
+                    st[sp].out = g.first;
+                    if (prev_split >= 0) st[prev_split].out1 = sp;
+                    else entry = sp;
+                    prev_split = sp;
+                } else {
+                    if (prev_split >= 0) st[prev_split].out1 = g.first;
+                    else entry = g.first;
+                }
+            }
+            return {entry, e};
+        }
+        case Node::REP: {
+            const int e0 = make(NState::EPS);
+            int entry = e0, tail = e0;
+            for (int k = 0; k < n.lo; ++k) {
+                auto g = build(ast, n.kids[0]);
+                st[tail].out = g.first;
+                tail = g.second;
+            }
+            if (n.hi < 0) {   // x*
+                auto g = build(ast, n.kids[0]);
+                const int sp = make(NState::SPLIT), e = make(NState::EPS);
+                st[tail].out = sp;
+                st[sp].out = g.first;
+                st[sp].out1 = e;
+                st[g.second].out = sp;
+                return {entry, e};
+            }
+            const int e = make(NState::EPS);
+            for (int k = n.lo; k < n.hi; ++k) {   // nested optionals
+                auto g = build(ast, n.kids[0]);
+                const int sp = make(NState::SPLIT);
+                st[tail].out = sp;
+                st[sp].out = g.first;
+                st[sp].out1 = e;
+                tail = g.second;
+            }
+            st[tail].out = e;
+            return {entry, e};
+        }
+        }
+        throw Unsupported{};
+    }
+
+    // epsilon closure; BOL edges only when bol, EOL edges only when eol
+    void closure(std::vector<int>& set, bool bol, bool eol) const {
+        std::vector<char> seen(st.size(), 0);
+        std::vector<int> stack(set.begin(), set.end());
+        set.clear();
+        while (!stack.empty()) {
+            const int s = stack.back();
+            stack.pop_back();
+            if (s < 0 || seen[s]) continue;
+            seen[s] = 1;
+            set.push_back(s);
+            const NState& n = st[s];
+            switch (n.t) {
+            case NState::EPS: stack.push_back(n.out); break;
+            case NState::SPLIT: stack.push_back(n.out); stack.push_back(n.out1); break;
+            case NState::BOL: if (bol) stack.push_back(n.out); break;
+            case NState::EOL: if (eol) stack.push_back(n.out); break;
+            default: break;
+            }
+        }
+        std::sort(set.begin(), set.end());
+    }
+
+    bool has_match(const std::vector<int>& set) const {
+        for (int s : set)
+            if (st[s].t == NState::MATCH) return true;
+        return false;
+    }
+};
+
+struct Dfa {
+    int n_classes = 0, init = 0;
+    uint8_t cls[256];
+    std::vector<uint8_t> acc;
+    std::vector<uint8_t> next;   // [state][class]
+};
+
+Dfa build_dfa(const std::string& pattern) {
+    Parser ps(pattern);
+    const int root = ps.parse();
+    Nfa nfa;
+    auto frag = nfa.build(ps.nodes, root);
+    const int match = nfa.make(NState::MATCH);
+    nfa.st[frag.second].out = match;
+    const int start = frag.first;
+
+    // byte classes: bytes with the same membership in every set are interchangeable
+    Dfa d;
+    {
+        std::map<std::vector<bool>, int> sig;
+        for (int b = 0; b < 256; ++b) {
+            std::vector<bool> v(nfa.sets.size());
+            for (size_t k = 0; k < nfa.sets.size(); ++k) v[k] = nfa.sets[k].test(b);
+            auto it = sig.find(v);
+            if (it == sig.end()) it = sig.emplace(v, (int)sig.size()).first;
+            d.cls[b] = (uint8_t)it->second;
+        }
+        d.n_classes = (int)sig.size();
+    }
+    std::vector<int> rep(d.n_classes, -1);   // a representative byte per class
+    for (int b = 0; b < 256; ++b)
+        if (rep[d.cls[b]] < 0) rep[d.cls[b]] = b;
+
+    std::vector<int> inject{start};
+    nfa.closure(inject, false, false);
+    std::vector<int> init{start};
+    nfa.closure(init, true, false);
+
+    std::map<std::vector<int>, int> ids;
+    std::vector<std::vector<int>> sets;
+    auto intern = [&](const std::vector<int>& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        if ((int)sets.size() >= kMaxDfa) throw Unsupported{};
+        ids.emplace(s, (int)sets.size());
+        sets.push_back(s);
+        return (int)sets.size() - 1;
+    };
+    d.init = intern(init);
+    for (size_t q = 0; q < sets.size(); ++q) {
+        for (int c = 0; c < d.n_classes; ++c) {
+            std::vector<int> mv;
+            for (int s : sets[q]) {
+                const NState& n = nfa.st[s];
+                if (n.t == NState::SET && nfa.sets[n.set_id].test(rep[c])) mv.push_back(n.out);
+            }
+            nfa.closure(mv, false, false);
+            std::vector<int> u;
+            std::set_union(mv.begin(), mv.end(), inject.begin(), inject.end(), std::back_inserter(u));
+            const int to = intern(u);
+            if (d.next.size() < (q + 1) * (size_t)d.n_classes) d.next.resize((q + 1) * (size_t)d.n_classes);
+            d.next[q * d.n_classes + c] = (uint8_t)to;
+        }
+    }
+    const int S = (int)sets.size();
+    d.next.resize((size_t)S * d.n_classes);
+    d.acc.assign(S, 0);
+    for (int q = 0; q < S; ++q) {
+        if (nfa.has_match(sets[q])) d.acc[q] |= 1;
+        std::vector<int> e = sets[q];
+        nfa.closure(e, false, true);
+        if (nfa.has_match(e)) d.acc[q] |= 2;
+    }
+    {
+        std::vector<int> e = init;
+        nfa.closure(e, true, true);
+        if (nfa.has_match(e)) d.acc[d.init] |= 8;
+    }
+    // states from which no match can complete: stop early with false
+    std::vector<char> live(S, 0);
+    for (int q = 0; q < S; ++q) live[q] = (d.acc[q] & 3) != 0;
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (int q = 0; q < S; ++q) {
+            if (live[q]) continue;
+            for (int c = 0; c < d.n_classes && !live[q]; ++c)
+                if (live[d.next[q * d.n_classes + c]]) live[q] = changed = true;
+        }
+    }
+    for (int q = 0; q < S; ++q)
+        if (!live[q]) d.acc[q] |= 4;
+    return d;
+}
+
+uint32_t blob_size(int S, int C) { return 8 + 256 + ((S + 3) & ~3) + (uint32_t)S * C; }
+
+}  // namespace
+
+extern "C" {
+
+int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size) {
+    if (!expression || !size) return BT_E_INVALID_ARGUMENT;
+    const std::string e(expression);
+    try {
+        std::regex probe(e);   // the reference's own acceptance (src/PacketFilter.cpp:311-316)
+    } catch (const std::regex_error&) {
+        return BT_E_INVALID_ARGUMENT;
+    }
+    Dfa d;
+    try {
+        d = build_dfa(e);
+    } catch (const Unsupported&) {
+        return BT_E_NOT_IMPLEMENTED;
+    }
+    const int S = (int)d.acc.size(), C = d.n_classes;
+    *size = blob_size(S, C);
+    if (!blob) return BT_OK;
+    if (cap < *size) return BT_E_RESOURCE;
+    uint8_t* p = static_cast<uint8_t*>(blob);
+    std::memset(p, 0, *size);
+    const uint16_t s16 = (uint16_t)S, c16 = (uint16_t)C;
+    std::memcpy(p, &s16, 2);
+    std::memcpy(p + 2, &c16, 2);
+    p[4] = (uint8_t)d.init;
+    std::memcpy(p + 8, d.cls, 256);
+    std::memcpy(p + 264, d.acc.data(), S);
+    std::memcpy(p + 264 + ((S + 3) & ~3), d.next.data(), (size_t)S * C);
+    return BT_OK;
+}
+
+int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n) {
+    const uint8_t* p = static_cast<const uint8_t*>(blob);
+    uint16_t S, C;
+    std::memcpy(&S, p, 2);
+    std::memcpy(&C, p + 2, 2);
+    const uint8_t* cls = p + 8;
+    const uint8_t* acc = p + 264;
+    const uint8_t* next = acc + ((S + 3) & ~3);
+    uint32_t q = p[4];
+    if (n == 0) return (acc[q] >> 3) & 1;
+    if (acc[q] & 1) return 1;
+    if (acc[q] & 4) return 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        q = next[q * C + cls[s[i]]];
+        if (acc[q] & 1) return 1;
+        if (acc[q] & 4) return 0;
+    }
+    return (acc[q] >> 1) & 1;
+}
+
+int bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len) {
+    // applyPayloadFilter's window (src/PacketFilter.cpp:293-309)
+    if (len < 34) return 0;
+    if (((uint32_t)frame[12] << 8 | frame[13]) != 0x0800u) return 0;
+    const uint32_t off = 14 + (uint32_t)(frame[14] & 0x0F) * 4;
+    if (len <= off) return 0;
+    return bt_payload_dfa_search(blob, frame + off, std::min<uint32_t>(len - off, 100));
+}
+
+}  // extern "C"

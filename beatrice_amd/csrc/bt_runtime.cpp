@@ -132,6 +132,9 @@ struct bt_ctx {
 
     std::vector<bt_filter_slot> slots;
     DevProgram prog{};
+    std::vector<uint8_t> dfa_pool;     // BT_K_PAYLOAD tables of the current program
+    uint8_t* dfa_dev = nullptr;
+    size_t dfa_cap = 0;
 
     // device workspace for bt_parse_filter_device
     uint32_t ws_cap = 0;
@@ -239,6 +242,8 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
     a.tile_pass = compact ? c->tile_pass : nullptr;
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
+    a.dfa = c->dfa_dev;
+    a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
     // Cache policy (measured, profiles/r01): non-temporal record stores everywhere
     // (C2 +3..9 %), non-temporal header loads in descriptor mode (C3 +15 %, C4 +8 %;
     // they cost C2 a little). BT_OPT_CACHE_DEFAULT turns both off, BT_OPT_NT_* force on.
@@ -373,6 +378,7 @@ void bt_destroy(bt_ctx* c) {
     c->pool.reset();
     if (c->tgraph) (void)hipGraphExecDestroy(c->tgraph);
     if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
+    if (c->dfa_dev) (void)hipFree(c->dfa_dev);
     for (auto e : c->tev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -396,7 +402,43 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
     int rc = bt_filter_compile_host(f, n, slots.data(), BT_MAX_FILTERS, &m);
     if (rc) return rc;
     slots.resize(m);
+    // PAYLOAD regexes the DFA compiler takes run on the GPU (BT_K_PAYLOAD); the pool of
+    // their tables is copied into each block's LDS, so it is capped at kDfaPoolMax.
+    std::vector<uint8_t> pool;
+    if (!(c->opts.flags & BT_OPT_PAYLOAD_HOST)) {
+        for (auto& s : slots) {
+            const bt_filter_desc& d = f[s.source_index];
+            if (s.kind != BT_K_HOST || d.type != BT_FILTER_PAYLOAD || !d.expression) continue;
+            uint32_t size = 0;
+            if (bt_payload_dfa_compile(d.expression, nullptr, 0, &size) != BT_OK) continue;
+            const size_t at = (pool.size() + 15) & ~(size_t)15;
+            if (at + size > kDfaPoolMax) continue;
+            pool.resize(at + size);
+            if (bt_payload_dfa_compile(d.expression, pool.data() + at, size, &size) != BT_OK) {
+                pool.resize(at);
+                continue;
+            }
+            s.kind = BT_K_PAYLOAD;
+            s.a = (uint32_t)at;
+            s.b = size;
+        }
+    }
     std::lock_guard<std::mutex> lk(c->mu);
+    if (!pool.empty()) {
+        HIP_TRY(hipSetDevice(c->device));
+        if (pool.size() > c->dfa_cap) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (c->dfa_dev) HIP_TRY(hipFree(c->dfa_dev));
+            c->dfa_dev = nullptr;
+            c->dfa_cap = 0;
+            HIP_TRY(hipMalloc(&c->dfa_dev, kDfaPoolMax));
+            c->dfa_cap = kDfaPoolMax;
+        }
+        // ordered behind work already queued on the context stream
+        HIP_TRY(hipMemcpyAsync(c->dfa_dev, pool.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    c->dfa_pool = std::move(pool);
     c->slots = slots;
     to_device_program(c->slots.data(), m, &c->prog);
     return BT_OK;

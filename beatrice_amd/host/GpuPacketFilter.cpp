@@ -181,7 +181,7 @@ uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
     for (uint32_t s = first; s < program_.size(); ++s) {
         const Slot& sl = program_[s];
         int r;
-        if (sl.compiled.kind != BT_K_HOST) {
+        if (sl.compiled.kind != BT_K_HOST && sl.compiled.kind != BT_K_PAYLOAD) {
             r = eval_builtin(sl.compiled, d, len);
         } else if (sl.entry->config.type == FilterType::CUSTOM) {
             r = sl.entry->customFunc ? (sl.entry->customFunc(p) ? 1 : 0) : 1;   // :323-328

@@ -190,7 +190,10 @@ enum bt_filter_kind {
     BT_K_PORT = 6,        /* inclusive range or exact port (:249-286, :362-372)                   */
     BT_K_IP_THROW = 7,    /* expression makes std::stoi throw once the IPv4 gates pass            */
     BT_K_PORT_THROW = 8,  /* same for the port filter once the TCP/UDP length gates pass          */
-    BT_K_HOST = 9         /* PAYLOAD regex / installed CUSTOM callback: evaluated on the host     */
+    BT_K_HOST = 9,        /* PAYLOAD regex outside the DFA subset / installed CUSTOM callback:    */
+                          /* evaluated on the host                                                */
+    BT_K_PAYLOAD = 10     /* PAYLOAD regex compiled to a byte DFA (bt_payload_dfa_compile):       */
+                          /* a = byte offset of its blob in the context's DFA pool, b = blob size */
 };
 
 typedef struct bt_filter_slot {       /* one compiled program slot, in evaluation order */
@@ -231,6 +234,7 @@ typedef struct bt_opts {
 #define BT_OPT_NT_LOADS 0x40u      /* force non-temporal header loads                    */
 #define BT_OPT_CACHE_DEFAULT 0x80u /* default cache policy everywhere (A/B only)         */
 #define BT_OPT_SPIN_SYNC 0x100u    /* spin-wait host synchronisation (bench / latency)   */
+#define BT_OPT_PAYLOAD_HOST 0x200u /* keep every PAYLOAD filter on the host (std::regex) */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
@@ -303,6 +307,25 @@ int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint3
  * read the header windows straight over PCIe: no host gather, no staging copy. */
 int  bt_host_register(bt_ctx* ctx, void* host, uint64_t bytes, void** dev_alias);
 int  bt_host_unregister(bt_ctx* ctx, void* host);
+
+/* ---- PAYLOAD filters on the GPU ---------------------------------
+ * Replaces the per-packet std::regex construction + regex_search of
+ * PacketFilter::applyPayloadFilter (src/PacketFilter.cpp:288-321) for the regular
+ * subset of libstdc++'s ECMAScript grammar: the expression is compiled once to a byte
+ * DFA that the kernel runs over the same <= 100-byte window after the IPv4 header.
+ * bt_filter_compile does this for every PAYLOAD filter it can (BT_K_PAYLOAD slots, up
+ * to 16 KiB of tables per program); the rest stay BT_K_HOST. The helpers below expose
+ * the compiler and a host executor of the same DFA (tests, other hosts).
+ *   bt_payload_dfa_compile  BT_OK (+ blob; blob == NULL: size only),
+ *                           BT_E_INVALID_ARGUMENT if std::regex rejects the expression
+ *                           (the reference's filter is then always false),
+ *                           BT_E_NOT_IMPLEMENTED outside the modelled subset / too big,
+ *                           BT_E_RESOURCE if cap is too small.
+ *   bt_payload_dfa_search   regex_search(string(s, n), regex(expr)) for a compiled expr
+ *   bt_payload_dfa_eval     applyPayloadFilter(frame, len) for a non-empty expression */
+int  bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size);
+int  bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);
+int  bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len);
 
 /* ---- capture-ring ingest: AF_PACKET TPACKET_V3 ---------------
  * Replaces the per-packet recv() + heap copy + queue push of the reference's

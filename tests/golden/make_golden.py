@@ -74,6 +74,64 @@ FILTER_SETS = {
 for t, exprs in QUIRK_EXPRS.items():
     FILTER_SETS.update(single(t, exprs))
 
+# PAYLOAD regexes for the GPU DFA: realistic application patterns and
+# the corners of libstdc++'s ECMAScript semantics; a few stay on the host (\b, \1).
+PAYLOAD_REGEXES = [
+    "GET|POST", "^GET /", "HTTP/1\\.[01]", "Host: [a-z0-9.-]+\\.com", "User-Agent: .*(bot|curl)",
+    "^\\x16\\x03[\\x00-\\x03]", "[\\x80-\\xff]{4,}", "\\d{3} [A-Z]", "\\r\\n\\r\\n", "^.{0,5}$",
+    "^$", "a|", "[^]", "[]", "\\s+$", "(?:GET|HEAD) /[^ ]* HTTP", "x{0}y", "^[\\x00-\\x1f]",
+    "passw(or)?d=", "\\bfoo", "(ab)\\1", "\\0", ".$", "[\\n\\r]",
+]
+FILTER_SETS.update({f"payload_re_{i}": [{"type": T["PAYLOAD"], "expr": e}] for i, e in enumerate(PAYLOAD_REGEXES)})
+FILTER_SETS.update({
+    # a GPU-resolvable PAYLOAD slot between built-in slots, and two of them in one program
+    "payload_chain": [{"type": T["BPF"], "expr": "tcp", "priority": 4},
+                      {"type": T["PAYLOAD"], "expr": "HTTP/1\\.[01]", "priority": 3},
+                      {"type": T["PORT_RANGE"], "expr": "0-1023", "priority": 2},
+                      {"type": T["PAYLOAD"], "expr": "Host: ", "priority": 1}],
+    "payload_host_mix": [{"type": T["PAYLOAD"], "expr": "GET|POST", "priority": 3},
+                         {"type": T["PAYLOAD"], "expr": "(GE)\\1?T", "priority": 2},
+                         {"type": T["CUSTOM"], "expr": "", "priority": 1, "custom": 1}],
+})
+
+
+def http_frames(n=3000, seed=7):
+    """Frames with application payloads for the PAYLOAD filter: HTTP requests and
+    responses, TLS records, binary noise; IPv4 with IHL 5..15, TCP and UDP, frame lengths
+    cutting the 100-byte window anywhere; some VLAN / IPv6 / short frames the filter's
+    gates reject."""
+    import random
+    import struct
+    rnd = random.Random(seed)
+    texts = [b"GET /index.html HTTP/1.1\r\nHost: www.example.com\r\nUser-Agent: curl/8.0\r\n\r\n",
+             b"POST /api/login HTTP/1.0\r\nHost: api.test.com\r\n\r\npassword=hunter2",
+             b"HTTP/1.1 200 OK\r\nContent-Length: 12\r\n\r\nhello world!",
+             b"HEAD /x HTTP/1.1\r\nUser-Agent: Googlebot\r\n\r\n",
+             b"\x16\x03\x01\x02\x00\x01\x00\x01\xfc\x03\x03" + bytes(range(32)),
+             b"passwd=secret&user=root", b"", b"x", b"\n", b"GEGET GT", b"404 Not Found\r\n"]
+    out = []
+    for i in range(n):
+        kind = rnd.random()
+        body = rnd.choice(texts)
+        if rnd.random() < 0.3:
+            body = bytes(rnd.randrange(256) for _ in range(rnd.randrange(0, 140))) + body
+        ihl = 5 if rnd.random() < 0.6 else rnd.randrange(5, 16)
+        proto = 6 if rnd.random() < 0.7 else 17
+        l4 = (struct.pack(">HHIIBBHHH", rnd.randrange(65536), rnd.choice([80, 443, 8080, 53]), i, 0, 0x50, 0x18,
+                          1024, 0, 0) if proto == 6 else struct.pack(">HHHH", 5353, 53, 8 + len(body), 0))
+        ip = bytes([0x40 | ihl, 0]) + struct.pack(">HHHBBH", 20 + len(l4) + len(body), i & 0xFFFF, 0, 64, proto, 0)
+        ip += bytes([10, 1, i & 255, 7]) + bytes([192, 168, 1, 1]) + bytes(4 * (ihl - 5)) + l4 + body
+        if kind < 0.05:
+            f = b"\x01" * 12 + b"\x81\x00\x00\x05\x08\x00" + ip        # VLAN: gate fails
+        elif kind < 0.08:
+            f = b"\x01" * 12 + b"\x86\xdd" + ip                            # IPv6 EtherType
+        else:
+            f = b"\x02" * 12 + b"\x08\x00" + ip
+        if rnd.random() < 0.25:
+            f = f[: rnd.randrange(0, len(f) + 1)]                            # cut anywhere
+        out.append(f)
+    return out
+
 
 def edge_frames():
     """Hand-built frames for the walk's and the filters' boundary cases."""
@@ -158,14 +216,22 @@ def build():
         "c4": (synth.capture(synth.C4, 2048), "C4: QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets"),
         "fuzz": (synth.capture(synth.FUZZ, 8192), "fuzz: short/odd frames, byte mutations"),
         "edge": (synth.pack_frames(edge_frames(), align=4, shift=2), "edge: hand-built boundary frames"),
+        "http": (synth.pack_frames(http_frames(), align=2, shift=0),
+                 "http: application payloads (HTTP, TLS, noise) for PAYLOAD regexes, IHL 5..15, cut frames"),
     }
     manifest = {"filter_sets": FILTER_SETS, "captures": {}}
     for name, ((data, desc), what) in caps.items():
         n = len(desc)
         rec = ol.ref_parse(data, desc, n)
         arrays = {"data": data, "desc": desc, "rec": rec}
-        sets = list(FILTER_SETS) if name in ("edge", "fuzz") else ["c3", "mixed", "throw_after", "payload_mid",
-                                                                    "custom", "empty"]
+        payload_sets = [k for k in FILTER_SETS if k.startswith("payload_re_")] + ["payload_chain",
+                                                                                   "payload_host_mix"]
+        if name in ("edge", "fuzz"):
+            sets = list(FILTER_SETS)
+        elif name == "http":
+            sets = ["c3", "payload_mid", "empty"] + [k for k in FILTER_SETS if k.startswith("payload_")]
+        else:
+            sets = ["c3", "mixed", "throw_after", "payload_mid", "custom", "empty"] + payload_sets[:6]
         for s in sets:
             code, src = ol.ref_filter(data, desc, n, FILTER_SETS[s])
             arrays[f"code__{s}"] = code
@@ -173,7 +239,13 @@ def build():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
         manifest["captures"][name] = {"n": n, "what": what, "filter_sets": sets}
         print(name, n, "frames", data.nbytes, "bytes;", len(sets), "filter sets")
-    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+    path = os.path.join(HERE, "manifest.json")
+    if os.path.exists(path):   # keep entries other generators own (make_ring_fixture.py: "rings")
+        with open(path) as fh:
+            old = json.load(fh)
+        for k, v in old.items():
+            manifest.setdefault(k, v)
+    with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1)
 
 

@@ -1,7 +1,7 @@
 """Helpers to compare decision bytes with the golden PacketFilter outcomes."""
 import numpy as np
 
-CAPTURES = ["c1", "c3", "c4", "fuzz", "edge"]
+CAPTURES = ["c1", "c3", "c4", "fuzz", "edge", "http"]
 
 
 def eval_order(filters):

@@ -1,0 +1,96 @@
+"""GPU: PAYLOAD filters evaluated by the kernel's byte DFA (BT_K_PAYLOAD)
+instead of being resumed on the host, checked against the compiled reference
+(goldens; oracle/_ref on a live sample) and the DFA's host executor (full size)."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+from beatrice_amd import abi, synth
+from conftest import load_golden
+from golden_util import compare_decisions
+
+pytestmark = pytest.mark.gpu
+
+BUILTIN_HEADLINE = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+                    {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2}]
+
+
+def _run(ctx, data, desc, records=False):
+    run = abi.DeviceRun(ctx, data, desc, len(desc), records=records)
+    run.run()
+    out = run.fetch()
+    run.free()
+    return out
+
+
+def test_payload_sets_decide_on_gpu(gpu_ctx):
+    g, man = load_golden("http")
+    n = len(g["desc"])
+    gpu_decided = 0
+    for s in man["captures"]["http"]["filter_sets"]:
+        if not s.startswith("payload_"):
+            continue
+        filters = man["filter_sets"][s]
+        prog = gpu_ctx.compile(filters)
+        out = _run(gpu_ctx, g["data"], g["desc"])
+        compare_decisions(out["decide"], g[f"code__{s}"], g[f"src__{s}"], filters, where=f"http/{s}")
+        # every slot the DFA compiler took is decided on the device: no HOST code at it
+        dslot = out["decide"] & 63
+        host = (out["decide"] >> 6) == 3
+        for k, slot in enumerate(prog):
+            if abi.KINDS[slot.kind] == "PAYLOAD":
+                assert not np.any(host & (dslot == k)), f"{s}: HOST decision at GPU slot {k}"
+                gpu_decided += 1
+    assert gpu_decided >= 20
+
+
+@pytest.mark.parametrize("cfg", [synth.C3, synth.C4])
+def test_payload_full_size_vs_host_executor(gpu_ctx, cfg):
+    n = 1 << 20
+    data, desc = synth.capture(cfg, n, seed=99)
+    expr = "[\\x80-\\xff]{3}|\\d\\d"
+    blob = abi.payload_dfa(expr)
+    gpu_ctx.compile([{"type": abi.PAYLOAD, "expr": expr, "priority": 1}])
+    assert abi.KINDS[gpu_ctx.program()[0].kind] == "PAYLOAD"
+    out = _run(gpu_ctx, data, desc)
+    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+    want = np.array([abi.payload_dfa_eval(blob, data[o:o + m]) for o, m in zip(off, ln)])
+    got = (out["decide"] >> 6) == 0
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} differ, first {bad[:5]}"
+    assert 0 < want.sum() < n
+
+
+@pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref (compiled reference) not built")
+def test_payload_chain_vs_reference_sample(gpu_ctx):
+    """A chain with two GPU PAYLOAD slots between built-ins, against the reference's
+    own PacketFilter (std::regex per packet) on a 64k-packet sample."""
+    n = 1 << 16
+    data, desc = synth.capture(synth.C3, n, seed=5)
+    filters = BUILTIN_HEADLINE[:1] + [{"type": abi.PAYLOAD, "expr": "[\\x00-\\x1f][a-z]", "priority": 2},
+                                      {"type": abi.PAYLOAD, "expr": "^..?\\d", "priority": 1},
+                                      {"type": abi.PORT_RANGE, "expr": "0-40000", "priority": 0}]
+    prog = gpu_ctx.compile(filters)
+    assert [abi.KINDS[p.kind] for p in prog] == ["PROTO_EQ", "PAYLOAD", "PAYLOAD", "PORT"]
+    out = _run(gpu_ctx, data, desc)
+    code, src = ol.ref_filter(data, desc, n, filters)
+    compare_decisions(out["decide"], code, src, filters, where="c3/payload_chain")
+    assert not np.any((out["decide"] >> 6) == 3)
+
+
+def test_payload_host_option_and_pool_limit():
+    ctx = abi.Context(0, flags=abi.OPT_PAYLOAD_HOST)
+    try:
+        prog = ctx.compile([{"type": abi.PAYLOAD, "expr": "GET", "priority": 1}])
+        assert abi.KINDS[prog[0].kind] == "HOST"
+    finally:
+        ctx.close()
+    ctx = abi.Context(0)
+    try:
+        big = "GET|POST|PUT|HEAD|DELETE|OPTIONS|PATCH|CONNECT|TRACE"   # ~1 KB of tables each
+        fs = [{"type": abi.PAYLOAD, "expr": big + "x" * k, "priority": -k} for k in range(40)]
+        kinds = [abi.KINDS[p.kind] for p in ctx.compile(fs)]
+        assert kinds[0] == "PAYLOAD" and "HOST" in kinds   # the 16 KiB pool fills, the rest stay on the host
+        assert kinds.index("HOST") == kinds.count("PAYLOAD")
+    finally:
+        ctx.close()

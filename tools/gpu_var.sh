@@ -1,2 +1,3 @@
 mkdir -p gpurun_out
-for cfg in c2 c3; do for bb in 128 512; do timeout -k 10 300 python tools/e2e.py --config $cfg --tpacket --host-threads 16 --ring-batch-blocks $bb --reps 3 || exit 5; done; done
+timeout -k 10 900 python -m pytest tests/test_gpu_payload.py tests/test_gpu_parity.py tests/test_cpp_adapter.py -q -x -p no:cacheprovider > gpurun_out/pytest_payload.log 2>&1; rc=$?
+tail -15 gpurun_out/pytest_payload.log; exit $rc
