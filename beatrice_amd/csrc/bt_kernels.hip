@@ -200,7 +200,9 @@ __device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_
 // run through the host-compiled byte DFA (bt_regex_dfa.cpp; blob layout there) that
 // sits in this block's dynamic LDS. The window lies beyond the header image, so the
 // lane stages it into its own LDS row first (the row is the lane's alone once PARSE
-// is done): <= 8 16-B loads, then one class lookup + one transition per byte.
+// is done): <= 8 16-B loads, 4 in flight at a time (all 8 would cost the variant a
+// wave of occupancy). The walk is one dependent LDS read per byte (C == 256) or two
+// (byte classes); the sinks K (match) / K+1 (none possible) end it early.
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
                                                  uint32_t& staged_sh) {
@@ -213,31 +215,46 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
         const uint64_t al = start & ~15ull;
         staged_sh = (uint32_t)(start & 15ull);
         const uint32_t nch = (staged_sh + L + 15u) >> 4;   // <= 8: 128 B of the 132-B row
-        // one chunk in flight at a time: keeps the main loop's register budget (a fully
-        // unrolled staging held 32 more VGPRs and cost a wave of occupancy)
-#pragma unroll 1
-        for (uint32_t c = 0; c < nch; ++c) {
-            const uint64_t g = al + 16ull * c;
-            const uint4 v = g + 16ull <= a.bytes ? ld16(a.base + g, a.nt & 2u) : make_uint4(0, 0, 0, 0);
-            row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+#pragma unroll
+        for (uint32_t h = 0; h < 8u; h += 4u) {
+            if (h < nch) {
+                uint4 v[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; ++k) {
+                    const uint64_t g = al + 16ull * (h + k);
+                    v[k] = (h + k < nch && g + 16ull <= a.bytes) ? ld16(a.base + g, a.nt & 2u) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; ++k) {
+                    uint32_t* d = row + 4u * (h + k);
+                    d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+                }
+            }
         }
     }
-    const uint8_t* pay = reinterpret_cast<const uint8_t*>(row) + staged_sh;
+    const uint32_t K = *reinterpret_cast<const uint16_t*>(blob);
     const uint32_t C = *reinterpret_cast<const uint16_t*>(blob + 2);
-    const uint32_t S = *reinterpret_cast<const uint16_t*>(blob);
-    const uint8_t* cls = blob + 8;
-    const uint8_t* acc = blob + 264;
-    const uint8_t* next = acc + ((S + 3u) & ~3u);
     uint32_t q = blob[4];
-    uint32_t f = acc[q];
-    if (f & 1u) return 1u;
-    if (f & 4u) return 0u;
-    for (uint32_t i = 0; i < L; ++i) {
-        q = next[q * C + cls[pay[i]]];
-        f = acc[q];
-        if (f & 5u) return f & 1u;
+    if (q >= K) return q == K ? 1u : 0u;
+    const uint8_t* endacc = blob + 8;
+    const uint8_t* cls = endacc + ((K + 3u) & ~3u);
+    const uint8_t* next = C == 256u ? cls : cls + 256;
+    const uint32_t dw = staged_sh >> 2, sh8 = (staged_sh & 3u) * 8u;
+    for (uint32_t i = 0; i < L; i += 4u) {
+        // four payload bytes from two aligned row dwords (independent of q: issued early)
+        const uint32_t lo = row[dw + (i >> 2)], hi = row[dw + (i >> 2) + 1u];
+        const uint32_t w = sh8 ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh8) : lo;
+        const uint32_t m = min(4u, L - i);
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) {
+            if (k < m) {
+                const uint32_t b = (w >> (8u * k)) & 0xFFu;
+                q = next[q * C + (C == 256u ? b : (uint32_t)cls[b])];
+                if (q >= K) return q == K ? 1u : 0u;
+            }
+        }
     }
-    return (f >> 1) & 1u;
+    return endacc[q];
 }
 
 // Header windows of one 64-packet tile in flight in registers (LOAD stage).

@@ -24,14 +24,16 @@
 // tests/cpp/test_regex_dfa.cpp.
 //
 // Blob layout (4-B aligned, little endian), shared by the host executor below and
-// the kernel (bt_kernels.hip, eval_payload):
-//   u16 n_states, u16 n_classes, u8 init, u8 pad[3]
-//   u8  cls[256]                   byte -> class
-//   u8  acc[n_states] (pad to 4)   bit0 match complete (stop: true)
-//                                  bit1 match complete if the input ends here
-//                                  bit2 no match possible from here (stop: false)
-//                                  bit3 (init only) match on the empty input
-//   u8  next[n_states * n_classes]
+// the kernel (bt_kernels.hip, eval_payload). States 0..K-1 are live; K is the ACCEPT
+// sink (a match completed: search succeeds) and K+1 the DEAD sink (no match can
+// complete any more), so the per-byte loop exits on `q >= K` without a table read.
+//   u16 K, u16 C          C = 256: `next` is indexed by the byte itself (one dependent
+//                         LDS read per byte); otherwise C byte classes via cls[]
+//   u8  init, u8 empty    init state (may be a sink); empty = match on the empty input
+//   u16 pad
+//   u8  endacc[K] (pad 4) 1 = a match completes if the input ends in this state
+//   u8  cls[256]          only when C != 256
+//   u8  next[K * C]
 #include <algorithm>
 #include <bitset>
 #include <cstring>
@@ -555,7 +557,47 @@ Dfa build_dfa(const std::string& pattern) {
     return d;
 }
 
-uint32_t blob_size(int S, int C) { return 8 + 256 + ((S + 3) & ~3) + (uint32_t)S * C; }
+// Live states, sinks and table shape of the serialized DFA.
+struct Packed {
+    int K = 0, C = 0, init = 0, empty = 0;
+    std::vector<uint8_t> endacc, cls, next;
+};
+
+constexpr int kByteTableMaxStates = 32;   // K * 256 <= 8 KiB: index by the byte, skip cls[]
+
+Packed pack(const Dfa& d) {
+    const int S = (int)d.acc.size();
+    // live = neither "match complete" (absorbing true) nor "no match possible"
+    std::vector<int> id(S, -1);
+    int K = 0;
+    for (int q = 0; q < S; ++q)
+        if (!(d.acc[q] & 1) && !(d.acc[q] & 4)) id[q] = K++;
+    if (K + 2 > 256) throw Unsupported{};
+    auto map = [&](int q) { return (d.acc[q] & 1) ? K : (d.acc[q] & 4) ? K + 1 : id[q]; };
+    Packed p;
+    p.K = K;
+    p.init = map(d.init);
+    p.empty = (d.acc[d.init] >> 3) & 1;
+    p.endacc.assign(K, 0);
+    for (int q = 0; q < S; ++q)
+        if (id[q] >= 0) p.endacc[id[q]] = (d.acc[q] >> 1) & 1;
+    const bool bytes = K <= kByteTableMaxStates;
+    p.C = bytes ? 256 : d.n_classes;
+    if (!bytes) p.cls.assign(d.cls, d.cls + 256);
+    p.next.assign((size_t)K * p.C, 0);
+    for (int q = 0; q < S; ++q) {
+        if (id[q] < 0) continue;
+        for (int c = 0; c < p.C; ++c) {
+            const int cl = bytes ? d.cls[c] : c;
+            p.next[(size_t)id[q] * p.C + c] = (uint8_t)map(d.next[(size_t)q * d.n_classes + cl]);
+        }
+    }
+    return p;
+}
+
+uint32_t blob_size(const Packed& p) {
+    return 8 + ((p.K + 3) & ~3) + (p.C == 256 ? 0 : 256) + (uint32_t)p.K * p.C;
+}
 
 }  // namespace
 
@@ -569,46 +611,49 @@ int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uin
     } catch (const std::regex_error&) {
         return BT_E_INVALID_ARGUMENT;
     }
-    Dfa d;
+    Packed pk;
     try {
-        d = build_dfa(e);
+        pk = pack(build_dfa(e));
     } catch (const Unsupported&) {
         return BT_E_NOT_IMPLEMENTED;
     }
-    const int S = (int)d.acc.size(), C = d.n_classes;
-    *size = blob_size(S, C);
+    *size = blob_size(pk);
     if (!blob) return BT_OK;
     if (cap < *size) return BT_E_RESOURCE;
     uint8_t* p = static_cast<uint8_t*>(blob);
     std::memset(p, 0, *size);
-    const uint16_t s16 = (uint16_t)S, c16 = (uint16_t)C;
-    std::memcpy(p, &s16, 2);
+    const uint16_t k16 = (uint16_t)pk.K, c16 = (uint16_t)pk.C;
+    std::memcpy(p, &k16, 2);
     std::memcpy(p + 2, &c16, 2);
-    p[4] = (uint8_t)d.init;
-    std::memcpy(p + 8, d.cls, 256);
-    std::memcpy(p + 264, d.acc.data(), S);
-    std::memcpy(p + 264 + ((S + 3) & ~3), d.next.data(), (size_t)S * C);
+    p[4] = (uint8_t)pk.init;
+    p[5] = (uint8_t)pk.empty;
+    uint8_t* q = p + 8;
+    if (pk.K) std::memcpy(q, pk.endacc.data(), pk.K);
+    q += (pk.K + 3) & ~3;
+    if (pk.C != 256) {
+        std::memcpy(q, pk.cls.data(), 256);
+        q += 256;
+    }
+    if (!pk.next.empty()) std::memcpy(q, pk.next.data(), pk.next.size());
     return BT_OK;
 }
 
 int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n) {
     const uint8_t* p = static_cast<const uint8_t*>(blob);
-    uint16_t S, C;
-    std::memcpy(&S, p, 2);
+    uint16_t K, C;
+    std::memcpy(&K, p, 2);
     std::memcpy(&C, p + 2, 2);
-    const uint8_t* cls = p + 8;
-    const uint8_t* acc = p + 264;
-    const uint8_t* next = acc + ((S + 3) & ~3);
+    const uint8_t* endacc = p + 8;
+    const uint8_t* cls = endacc + ((K + 3) & ~3);
+    const uint8_t* next = C == 256 ? cls : cls + 256;
     uint32_t q = p[4];
-    if (n == 0) return (acc[q] >> 3) & 1;
-    if (acc[q] & 1) return 1;
-    if (acc[q] & 4) return 0;
+    if (n == 0) return p[5];
+    if (q >= K) return q == K;
     for (uint32_t i = 0; i < n; ++i) {
-        q = next[q * C + cls[s[i]]];
-        if (acc[q] & 1) return 1;
-        if (acc[q] & 4) return 0;
+        q = next[q * C + (C == 256 ? s[i] : cls[s[i]])];
+        if (q >= K) return q == K;
     }
-    return (acc[q] >> 1) & 1;
+    return endacc[q];
 }
 
 int bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len) {

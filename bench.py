@@ -51,6 +51,20 @@ WORKLOADS = {
 }
 
 
+def payload_extra_bytes(data: np.ndarray, desc: np.ndarray) -> float:
+    """Bytes a PAYLOAD slot reads beyond the 128-B header window: applyPayloadFilter's
+    window is [14 + 4*IHL, +min(len - that, 100)) of IPv4 frames (src/PacketFilter.cpp:293-309)."""
+    off = synth.desc_off(desc).astype(np.int64)
+    ln = synth.desc_len(desc).astype(np.int64)
+    ok = ln >= 34
+    idx = np.minimum(off + 14, len(data) - 1)
+    ipv4 = ok & (data[np.minimum(off + 12, len(data) - 1)] == 8) & (data[np.minimum(off + 13, len(data) - 1)] == 0)
+    po = 14 + (data[idx].astype(np.int64) & 15) * 4
+    end = np.minimum(ln, po + 100)
+    extra = np.where(ipv4 & (ln > po), np.maximum(0, end - 128), 0)
+    return float(extra.sum())
+
+
 def algorithmic_bytes(desc: np.ndarray, fixed: bool, parse: bool, filt: bool, n_pass: int) -> float:
     """Bytes the main kernel must move per launch (SURVEY.md §8(d) formula):
     min(len,128) header read + 8 B descriptor (0 for fixed stride) + 96 B record
@@ -114,6 +128,9 @@ def main():
     ap.add_argument("--grid-waves", type=int, default=0, help="persistent grid size in wavefronts (0 = auto)")
     ap.add_argument("--no-prefetch", action="store_true", help="A/B: disable the next-tile load prefetch")
     ap.add_argument("--flags", type=int, default=None, help="raw bt_opts.flags (A/B experiments)")
+    ap.add_argument("--payload", default=None,
+                    help="c3/c4: put a PAYLOAD regex FIRST in the filter program (every IPv4 packet runs the "
+                         "GPU DFA: worst case); reported in config, not the default workload")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -132,8 +149,15 @@ def main():
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
     flags |= abi.OPT_SPIN_SYNC   # the timed region's end is not delayed by a sleeping host thread
     ctx = abi.Context(local, grid_waves=args.grid_waves, flags=flags)
+    if args.payload is not None:
+        if not wl["filters"]:
+            sys.exit("--payload needs a filtering workload (c3 / c4)")
+        wl = dict(wl, filters=[{"type": abi.PAYLOAD, "expr": args.payload, "priority": 9}] + wl["filters"],
+                  name=wl["name"] + f" + PAYLOAD /{args.payload}/ first")
     if wl["filters"]:
-        ctx.compile(wl["filters"])
+        prog = ctx.compile(wl["filters"])
+        if args.payload is not None and abi.KINDS[prog[0].kind] != "PAYLOAD":
+            sys.exit(f"--payload {args.payload!r} is not GPU-compilable (kind {abi.KINDS[prog[0].kind]})")
     filt = wl["filters"] is not None
     run = abi.DeviceRun(ctx, data, None if wl["fixed"] else desc, n, stride=64 if wl["fixed"] else 0,
                         records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt)
@@ -167,6 +191,8 @@ def main():
     value = total_pkts / step_s / 1e6
 
     algo = algorithmic_bytes(desc, wl["fixed"], wl["parse"], filt, n_pass)
+    if args.payload is not None:
+        algo += payload_extra_bytes(data, desc)
     achieved = algo / (main_ms * 1e-3) / 1e9
     traffic, traffic_src = None, None
     if os.path.exists(args.traffic_json):   # rocprofv3 PMC passes of this kernel (tools/pmc_traffic.py)
