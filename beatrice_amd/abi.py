@@ -24,14 +24,16 @@ KINDS = ["TRUE", "FALSE", "BPF", "PROTO_EQ", "PROTO_NZ", "IP_MASK", "PORT", "IP_
          "PAYLOAD"]
 
 L_ETH, L_VLAN0, L_VLAN1, L_IPV4, L_IPV6, L_TCP, L_UDP, L_ICMP = (1 << i for i in range(8))
+# bt_rec.detect_code: reference ProtocolDetector::detectProtocol names (ProtocolRegistry.cpp:353-388)
+DETECT_NAMES = ("unknown", "", "ethernet", "tcp", "udp", "icmp")
 
 # numpy view of bt_rec (96 B, include/beatrice_gpu.h)
 REC_DTYPE = np.dtype({
     "names": ["eth_dst", "eth_src", "ethertype", "pkt_len", "vlan_tpid", "vlan_tci", "present", "ok",
-              "l3_off", "l4_off", "l3", "l4", "reserved"],
+              "l3_off", "l4_off", "l3", "l4", "detect_code", "detect_is", "detect_is2", "reserved"],
     "formats": [("u1", 6), ("u1", 6), "<u2", "<u2", ("<u2", 2), ("<u2", 2), "u1", "u1", "u1", "u1",
-                ("u1", 40), ("u1", 20), ("u1", 8)],
-    "offsets": [0, 6, 12, 14, 16, 20, 24, 25, 26, 27, 28, 68, 88],
+                ("u1", 40), ("u1", 20), "u1", "u1", "u1", ("u1", 5)],
+    "offsets": [0, 6, 12, 14, 16, 20, 24, 25, 26, 27, 28, 68, 88, 89, 90, 91],
     "itemsize": 96,
 })
 

@@ -82,6 +82,31 @@ struct Parsed {
     uint32_t r[24];   // bt_rec as 24 little-endian dwords
 };
 
+// ProtocolDetector column (bt_rec bytes 88..90) from the first 38 frame bytes:
+// detectProtocol (reference src/parser/ProtocolRegistry.cpp:353-388), the is*
+// predicates (:418-487) and detectMultipleProtocols' second entry (:390-416). Every
+// byte it reads is gated by the reference's own length checks, so bytes past the
+// frame end (another frame's, in the LDS image) never decide anything.
+__device__ __forceinline__ uint32_t detect_word(const uint32_t* w0, uint32_t len) {
+    const uint32_t et = be16_of(w0, 12), b0 = byte_of(w0, 0), pr = byte_of(w0, 23);
+    const uint32_t ports = be16_of(w0, 34) | (be16_of(w0, 36) << 16);
+    const bool eth = len >= 14 && (et == 0x0800u || et == 0x86DDu || et == 0x0806u);
+    const bool l34 = len >= 34;
+    uint32_t code = len < 14 ? BT_DET_UNKNOWN : eth ? BT_DET_ETHERNET : BT_DET_NONE;
+    if (eth && l34) code = pr == 6 ? BT_DET_TCP : pr == 17 ? BT_DET_UDP : pr == 1 ? BT_DET_ICMP : code;
+    const bool v4 = l34 && (b0 >> 4) == 4u;
+    const bool tcp = v4 && pr == 6, udp = v4 && pr == 17;
+    const bool p80 = (ports & 0xFFFFu) == 80u || (ports >> 16) == 80u;
+    const bool p53 = (ports & 0xFFFFu) == 53u || (ports >> 16) == 53u;
+    const uint32_t is = (eth ? BT_IS_ETHERNET : 0u) | (v4 ? BT_IS_IPV4 : 0u) |
+                        (len >= 54 && (b0 >> 4) == 6u ? BT_IS_IPV6 : 0u) | (tcp ? BT_IS_TCP : 0u) |
+                        (udp ? BT_IS_UDP : 0u) | (v4 && pr == 1 ? BT_IS_ICMP : 0u) |
+                        (tcp && len >= 54 && p80 ? BT_IS_HTTP : 0u) | (udp && len >= 42 && p53 ? BT_IS_DNS : 0u);
+    const uint32_t is2 = (len >= 28 && et == 0x0806u ? BT_IS2_ARP : 0u) | (l34 && pr == 6 ? BT_IS2_MULTI_TCP : 0u) |
+                         (l34 && pr == 17 ? BT_IS2_MULTI_UDP : 0u);
+    return code | (is << 8) | (is2 << 16);
+}
+
 // The layer walk + field extraction for one packet whose byte 0 sits at byte `s` of
 // the lane's LDS row. Field semantics: ProtocolRegistry.cpp tables, extractValue<T>
 // big-endian decode, all-or-nothing per layer (ProtocolParser.cpp:244-247).
@@ -165,7 +190,8 @@ __device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, ui
                             (v4ok ? BT_L_IPV4 : 0u) | (v6ok ? BT_L_IPV6 : 0u) |
                             (tcp_ok ? BT_L_TCP : 0u) | (udp_ok ? BT_L_UDP : 0u) | (icmp_ok ? BT_L_ICMP : 0u);
     p.r[6] = present | (okbits << 8) | ((l3bit ? o3 : 0u) << 16) | ((l4 ? o4 : 0u) << 24);
-    p.r[22] = p.r[23] = 0;
+    p.r[22] = detect_word(w0, len);
+    p.r[23] = 0;
 }
 
 // One filter slot on one packet: 1 pass, 0 reject, 2 throw, 3 host.

@@ -5,6 +5,7 @@
 // ParseResult header fields :238-284.
 #include "GpuProtocolParser.hpp"
 
+#include <chrono>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
@@ -201,6 +202,37 @@ ParseResult GpuParsedBatch::layer(size_t i, const std::string& name) const {
     res.status = ParseStatus::PROTOCOL_NOT_FOUND;
     res.errorMessage = "Protocol not found: " + name;
     return res;
+}
+
+GpuParsedBatch::DetectionResult GpuParsedBatch::detect(size_t i) const {
+    // names, confidences and reasons of ProtocolDetector::detectProtocol (:353-388)
+    static const struct { const char* name; double conf; const char* reason; } kDet[] = {
+        {"unknown", 0.0, "Packet too short"},        {"", 0.0, ""},
+        {"ethernet", 0.95, "Valid Ethernet frame"},  {"tcp", 0.98, "Ethernet + IPv4 + TCP"},
+        {"udp", 0.98, "Ethernet + IPv4 + UDP"},      {"icmp", 0.98, "Ethernet + IPv4 + ICMP"}};
+    const uint8_t c = recs_.at(i).detect_code;
+    if (c > BT_DET_ICMP) throw std::logic_error("GpuParsedBatch::detect: bad detector code");
+    DetectionResult r;
+    r.protocolName = kDet[c].name;
+    r.confidence = kDet[c].conf;
+    r.reason = kDet[c].reason;
+    r.detectionTime = std::chrono::microseconds(0);
+    return r;
+}
+
+std::vector<GpuParsedBatch::DetectionResult> GpuParsedBatch::detectMultiple(size_t i) const {
+    std::vector<DetectionResult> out{detect(i)};
+    const uint8_t x = recs_[i].detect_is2;
+    if (x & (BT_IS2_MULTI_TCP | BT_IS2_MULTI_UDP)) {   // :395-413
+        DetectionResult r;
+        const bool tcp = (x & BT_IS2_MULTI_TCP) != 0;
+        r.protocolName = tcp ? "tcp" : "udp";
+        r.confidence = 0.98;
+        r.reason = tcp ? "TCP over IPv4" : "UDP over IPv4";
+        r.detectionTime = std::chrono::microseconds(0);
+        out.push_back(r);
+    }
+    return out;
 }
 
 GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts) {

@@ -8,6 +8,13 @@
 //     ProtocolParser(cfg with enablePerformanceMetrics=false)
 //         .parsePacket(std::vector<uint8_t>(frame + offset, frame + len), name)
 // in every member except the wall-clock timings (parseTime / totalParseTime = 0).
+//
+// detect(i) / detectMultiple(i) / is(i, BT_IS_*) answer the reference's static
+// ProtocolDetector (include/parser/ProtocolRegistry.hpp:83-108) for the whole frame
+// from the record's detector column, which the same kernel pass fills: equal to
+// ProtocolDetector::detectProtocol(frame) etc. except `confidence` of a non-Ethernet
+// frame, which the reference leaves uninitialised (ProtocolRegistry.cpp:355) and this
+// layer reports as 0.0.
 #pragma once
 
 #include <cstdint>
@@ -17,6 +24,7 @@
 #include "beatrice/Packet.hpp"
 #include "beatrice_gpu.h"
 #include "parser/ParserResult.hpp"
+#include "parser/ProtocolRegistry.hpp"
 
 namespace beatrice {
 namespace gpu {
@@ -35,6 +43,13 @@ public:
     parser::ParseResult layer(size_t i, size_t k) const;
     // first walked layer called `name` (PROTOCOL_NOT_FOUND result when absent)
     parser::ParseResult layer(size_t i, const std::string& name) const;
+
+    using DetectionResult = parser::ProtocolDetector::DetectionResult;
+    DetectionResult detect(size_t i) const;                     // detectProtocol (:353-388)
+    std::vector<DetectionResult> detectMultiple(size_t i) const; // detectMultipleProtocols (:390-416)
+    // isEthernet .. isDNS as BT_IS_* bits; isARP as BT_IS2_ARP via isARP()
+    bool is(size_t i, uint32_t bt_is_bit) const { return (recs_.at(i).detect_is & bt_is_bit) != 0; }
+    bool isARP(size_t i) const { return (recs_.at(i).detect_is2 & BT_IS2_ARP) != 0; }
 
 private:
     friend class GpuProtocolParser;

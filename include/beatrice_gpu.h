@@ -32,7 +32,8 @@
  * little-endian; BYTES / IPV4_ADDRESS / IPV6_ADDRESS fields are the raw bytes.
  * A layer whose slice is shorter than its table's getTotalLength() has status
  * PACKET_TOO_SHORT and no fields (:244-247): its field bytes are zero here.
- * Bytes of absent layers and reserved bytes are zero.
+ * Bytes of absent layers and reserved bytes are zero. Bytes 88..90 hold the
+ * ProtocolDetector column of the whole frame (BT_DET_* / BT_IS_* below).
  *
  * On the device the records are stored tiled by 64 packets (one wavefront tile),
  * SoA by 16-byte slab inside the tile: slab k (k = 0..5) of packet i lives at
@@ -81,6 +82,34 @@ typedef uint64_t bt_pkt_desc;
 #define BT_L_TCP   0x20u
 #define BT_L_UDP   0x40u
 #define BT_L_ICMP  0x80u
+
+/* bt_rec.detect_*: reference ProtocolDetector (src/parser/ProtocolRegistry.cpp:353-484)
+ * applied to the whole frame. detect_code is detectProtocol(frame).protocolName:
+ *   BT_DET_UNKNOWN   "unknown",  confidence 0.0,  reason "Packet too short"   (len < 14)
+ *   BT_DET_NONE      "" / "" (the reference leaves confidence uninitialised)  (:356-357)
+ *   BT_DET_ETHERNET  "ethernet", 0.95, "Valid Ethernet frame"
+ *   BT_DET_TCP/UDP/ICMP  "tcp"/"udp"/"icmp", 0.98, "Ethernet + IPv4 + TCP|UDP|ICMP"
+ *                    (frame byte 23 once len >= 34, whatever the EtherType)
+ * detect_is: isEthernet, isIPv4, isIPv6, isTCP, isUDP, isICMP, isHTTP, isDNS (:418-480;
+ * the IPv4/IPv6 tests read the version nibble of frame byte 0, as the reference does).
+ * detect_is2: isARP (:482-487) and the second entry of detectMultipleProtocols (:390-416). */
+#define BT_DET_UNKNOWN  0u
+#define BT_DET_NONE     1u
+#define BT_DET_ETHERNET 2u
+#define BT_DET_TCP      3u
+#define BT_DET_UDP      4u
+#define BT_DET_ICMP     5u
+#define BT_IS_ETHERNET  0x01u
+#define BT_IS_IPV4      0x02u
+#define BT_IS_IPV6      0x04u
+#define BT_IS_TCP       0x08u
+#define BT_IS_UDP       0x10u
+#define BT_IS_ICMP      0x20u
+#define BT_IS_HTTP      0x40u
+#define BT_IS_DNS       0x80u
+#define BT_IS2_ARP       0x01u
+#define BT_IS2_MULTI_TCP 0x02u   /* detectMultipleProtocols adds {"tcp", 0.98, "TCP over IPv4"} */
+#define BT_IS2_MULTI_UDP 0x04u   /* ... {"udp", 0.98, "UDP over IPv4"}                          */
 
 #pragma pack(push, 1)
 typedef struct bt_ipv4_fields {   /* reference src/parser/ProtocolRegistry.cpp:161-178 */
@@ -154,8 +183,11 @@ typedef struct bt_rec {
     /* slabs 1..4: L3 union at 28, L4 union at 68 */
     union { bt_ipv4_fields ipv4; bt_ipv6_fields ipv6; } l3;
     union { bt_tcp_fields tcp; bt_udp_fields udp; bt_icmp_fields icmp; } l4;
-    /* slab 5 tail */
-    uint8_t  _reserved[8];
+    /* slab 5 tail: the ProtocolDetector column for the whole frame */
+    uint8_t  detect_code;              /* BT_DET_*: detectProtocol(frame)            */
+    uint8_t  detect_is;                /* BT_IS_* predicate bits                     */
+    uint8_t  detect_is2;               /* BT_IS2_* bits                              */
+    uint8_t  _reserved[5];
 } bt_rec;
 #pragma pack(pop)
 
@@ -385,6 +417,7 @@ void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_
 static_assert(sizeof(bt_rec) == BT_REC_BYTES, "bt_rec must be 96 bytes");
 static_assert(offsetof(bt_rec, l3) == 28, "L3 union at 28");
 static_assert(offsetof(bt_rec, l4) == 68, "L4 union at 68");
+static_assert(offsetof(bt_rec, detect_code) == 88, "detector column at 88");
 #endif
 
 #endif /* BEATRICE_GPU_H */

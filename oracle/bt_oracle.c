@@ -149,9 +149,52 @@ static int parse_layer(const uint8_t* slice, uint32_t slen, const field_def* t, 
 
 static uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 
+/* ProtocolDetector, src/parser/ProtocolRegistry.cpp:353-487, one predicate per
+ * reference function, each over the whole frame. */
+static int det_is_ethernet(const uint8_t* p, uint32_t n)   /* :418-423 */
+{
+    if (n < 14) return 0;
+    uint32_t et = be16(p + 12);
+    return et == 0x0800 || et == 0x0806 || et == 0x86DD;
+}
+static int det_is_ipv4(const uint8_t* p, uint32_t n) { return n >= 34 && (p[0] >> 4) == 4; }  /* :425-430 */
+static int det_is_ipv6(const uint8_t* p, uint32_t n) { return n >= 54 && (p[0] >> 4) == 6; }  /* :432-437 */
+static int det_is_tcp(const uint8_t* p, uint32_t n) { return det_is_ipv4(p, n) && p[23] == 6; }
+static int det_is_udp(const uint8_t* p, uint32_t n) { return det_is_ipv4(p, n) && p[23] == 17; }
+static int det_is_icmp(const uint8_t* p, uint32_t n) { return det_is_ipv4(p, n) && p[23] == 1; }
+static int det_is_http(const uint8_t* p, uint32_t n)      /* :460-469 */
+{
+    if (!det_is_tcp(p, n) || n < 54) return 0;
+    return be16(p + 36) == 80 || be16(p + 34) == 80;
+}
+static int det_is_dns(const uint8_t* p, uint32_t n)       /* :471-480 */
+{
+    if (!det_is_udp(p, n) || n < 42) return 0;
+    return be16(p + 36) == 53 || be16(p + 34) == 53;
+}
+static int det_is_arp(const uint8_t* p, uint32_t n) { return n >= 28 && be16(p + 12) == 0x0806; }
+
+static void detect(const uint8_t* p, uint32_t n, uint8_t* out)
+{
+    uint8_t code;                                          /* detectProtocol :353-388 */
+    if (n < 14) code = 0;                                  /* "unknown"  */
+    else if (!det_is_ethernet(p, n)) code = 1;             /* ""         */
+    else {
+        code = 2;                                          /* "ethernet" */
+        if (n >= 34) code = p[23] == 6 ? 3 : p[23] == 17 ? 4 : p[23] == 1 ? 5 : code;
+    }
+    out[0] = code;
+    out[1] = (uint8_t)(det_is_ethernet(p, n) | det_is_ipv4(p, n) << 1 | det_is_ipv6(p, n) << 2 |
+                       det_is_tcp(p, n) << 3 | det_is_udp(p, n) << 4 | det_is_icmp(p, n) << 5 |
+                       det_is_http(p, n) << 6 | det_is_dns(p, n) << 7);
+    /* detectMultipleProtocols :390-416 appends tcp/udp when n >= 34 */
+    out[2] = (uint8_t)(det_is_arp(p, n) | (n >= 34 && p[23] == 6) << 1 | (n >= 34 && p[23] == 17) << 2);
+}
+
 void bto_parse(const uint8_t* frame, uint32_t len, uint8_t rec[96])
 {
     memset(rec, 0, 96);
+    detect(frame, len, rec + 88);
     uint16_t pl = (uint16_t)(len > 0xFFFF ? 0xFFFF : len);
     memcpy(rec + 14, &pl, 2);
     uint8_t present = L_ETH, ok = 0;

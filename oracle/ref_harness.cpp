@@ -66,6 +66,23 @@ bool status_ok(const ParseResult& r, bool* ok) {
     return false;
 }
 
+// bt_rec bytes 88..90 from the reference's own ProtocolDetector over the whole frame
+void detect(const uint8_t* f, uint32_t len, uint8_t* out) {
+    const std::vector<uint8_t> v(f, f + len);
+    const auto d = ProtocolDetector::detectProtocol(v);
+    const std::string& nm = d.protocolName;
+    out[0] = nm == "unknown" ? 0 : nm.empty() ? 1 : nm == "ethernet" ? 2 : nm == "tcp" ? 3 : nm == "udp" ? 4
+           : nm == "icmp" ? 5 : 0xFF;
+    out[1] = (uint8_t)(ProtocolDetector::isEthernet(v) | ProtocolDetector::isIPv4(v) << 1 |
+                       ProtocolDetector::isIPv6(v) << 2 | ProtocolDetector::isTCP(v) << 3 |
+                       ProtocolDetector::isUDP(v) << 4 | ProtocolDetector::isICMP(v) << 5 |
+                       ProtocolDetector::isHTTP(v) << 6 | ProtocolDetector::isDNS(v) << 7);
+    const auto m = ProtocolDetector::detectMultipleProtocols(v);
+    uint8_t extra = 0;
+    if (m.size() > 1) extra = m[1].protocolName == "tcp" ? 0x02 : m[1].protocolName == "udp" ? 0x04 : 0x80;
+    out[2] = (uint8_t)(ProtocolDetector::isARP(v) | extra | (m.size() > 2 ? 0x80 : 0));
+}
+
 int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
     std::memset(rec, 0, 96);
     put<uint16_t>(rec, 14, (uint16_t)(len > 0xFFFF ? 0xFFFF : len));
@@ -233,7 +250,8 @@ Packet make_packet(const uint8_t* f, uint32_t len) {
 
 extern "C" {
 
-// Per-packet bt_rec (AoS, 96 B) from the reference parser. Returns the number of
+// Per-packet bt_rec (AoS, 96 B) from the reference parser, bytes 88..90 from the
+// reference ProtocolDetector (the CPU baseline, ref_bench, times the parser only). Returns the number of
 // packets whose layers produced an unexpected ParseStatus (must be 0).
 int ref_parse(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n, uint8_t* records) {
     Walker w;
@@ -242,6 +260,7 @@ int ref_parse(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32
         uint32_t len;
         const uint8_t* f = frame_at(base, desc, stride, i, &len);
         bad += walk(w, f, len, records + (uint64_t)i * 96);
+        detect(f, len, records + (uint64_t)i * 96 + 88);
     }
     return bad;
 }

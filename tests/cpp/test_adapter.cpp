@@ -188,7 +188,31 @@ static bool parser_case(const char* label, const Capture& cap) {
                       n.c_str());
         }
     }
-    std::printf("ok   parser  %-22s %zu packets, %zu layer results\n", label, cap.packets.size(), nlayers);
+    // ProtocolDetector over the whole frame (ProtocolRegistry.cpp:353-487)
+    for (size_t i = 0; i < cap.packets.size(); ++i) {
+        const std::vector<uint8_t> v(cap.packets[i].data(), cap.packets[i].data() + cap.packets[i].length());
+        const auto want = ProtocolDetector::detectMultipleProtocols(v);
+        const auto got = batch.detectMultiple(i);
+        const auto d = batch.detect(i);
+        CHECK(want.size() == got.size() && d.protocolName == got[0].protocolName, "%s: packet %zu detector entries",
+              label, i);
+        for (size_t k = 0; k < want.size() && k < got.size(); ++k) {
+            // the reference leaves confidence uninitialised for a non-Ethernet frame (name "")
+            const bool conf_defined = !want[k].protocolName.empty();
+            CHECK(want[k].protocolName == got[k].protocolName && want[k].reason == got[k].reason &&
+                      (!conf_defined || want[k].confidence == got[k].confidence) &&
+                      want[k].detectionTime == got[k].detectionTime,
+                  "%s: packet %zu detector entry %zu: %s/%s", label, i, k, want[k].protocolName.c_str(),
+                  got[k].protocolName.c_str());
+        }
+        const bool is_ref[8] = {ProtocolDetector::isEthernet(v), ProtocolDetector::isIPv4(v), ProtocolDetector::isIPv6(v),
+                                ProtocolDetector::isTCP(v),      ProtocolDetector::isUDP(v),  ProtocolDetector::isICMP(v),
+                                ProtocolDetector::isHTTP(v),     ProtocolDetector::isDNS(v)};
+        for (int b = 0; b < 8; ++b)
+            CHECK(is_ref[b] == batch.is(i, 1u << b), "%s: packet %zu predicate bit %d", label, i, b);
+        CHECK(ProtocolDetector::isARP(v) == batch.isARP(i), "%s: packet %zu isARP", label, i);
+    }
+    std::printf("ok   parser  %-22s %zu packets, %zu layer results, detector\n", label, cap.packets.size(), nlayers);
     return true;
 }
 

@@ -205,6 +205,19 @@ def edge_frames():
         f.append(eth(0x0800, ipv4(6, tcp(sp, dp))))
     # a frame longer than 65535 is impossible in bt_pkt_desc; a long one near the cap
     f.append(eth(0x0800, ipv4(17, udp(1500, 1500, bytes(9000)))))
+    # ProtocolDetector (ProtocolRegistry.cpp:353-487): its isIPv4/isIPv6 read the version
+    # nibble of frame byte 0 (the destination MAC), so these frames put 0x4_/0x6_ there;
+    # HTTP/DNS ports on either side, every length gate (14, 28, 34, 42, 54) and ARP
+    for mac0 in (b"\x45", b"\x4f", b"\x60", b"\x6a", b"\x05"):
+        dst = mac0 + b"\x00\x00\x00\x00\x01"
+        for fr in (eth(0x0800, ipv4(6, tcp(80, 1234)), dst=dst), eth(0x0800, ipv4(6, tcp(1234, 80)), dst=dst),
+                   eth(0x0800, ipv4(17, udp(53, 9)), dst=dst), eth(0x0800, ipv4(17, udp(9, 53)), dst=dst),
+                   eth(0x0800, ipv4(1, bytes(8)), dst=dst), eth(0x86DD, ipv6(6, tcp(80, 80)), dst=dst),
+                   eth(0x0806, bytes(28), dst=dst), eth(0x0800, ipv4(6, tcp(8080, 80)), dst=dst)):
+            f.append(fr)
+        for n in (13, 14, 27, 28, 33, 34, 41, 42, 53, 54):
+            f.append(eth(0x0806 if n < 34 else 0x0800, ipv4(17 if n < 50 else 6,
+                                                             udp(53, 53) if n < 50 else tcp(80, 80)), dst=dst)[:n])
     return f
 
 
