@@ -44,7 +44,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kRowDwords = 33;                    // 128 B header window + 4 B pad (bank spread)
-constexpr int kChunkTiles = 1024;                 // compaction chunk = 64Ki packets
+constexpr int kChunkTiles = 256;                  // compaction chunk = 16Ki packets (one tile per thread)
 constexpr uint32_t kNeedParse = 102;              // 14 + 2*4 + 60 (IPv4 max) + 20 (TCP fields)
 constexpr uint32_t kNeedFilter = 38;              // PacketFilter reads bytes 12..37
 
