@@ -97,7 +97,7 @@ EXPORTS = [
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
-    "bt_payload_dfa_compile", "bt_payload_dfa_search", "bt_payload_dfa_eval",
+    "bt_payload_dfa_compile", "bt_payload_dfa_search", "bt_payload_dfa_eval", "bt_format_records",
 ]
 
 _lib = None
@@ -144,6 +144,7 @@ def lib() -> ctypes.CDLL:
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
         "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
+        "bt_format_records": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, ctypes.POINTER(u64), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -179,6 +180,26 @@ def compile_host(filters):
     n = ctypes.c_uint32(0)
     _check(lib().bt_filter_compile_host(arr, len(filters), out, BT_MAX_FILTERS, ctypes.byref(n)))
     return [out[i] for i in range(n.value)]
+
+
+FMT_JSON, FMT_XML, FMT_CSV, FMT_HUMAN = range(4)
+
+
+def format_records(records: np.ndarray, fmt: int = FMT_JSON, ctx: "Context | None" = None,
+                   offsets: bool = False):
+    """bt_format_records over host bt_rec (REC_DTYPE or (n, 96) u8): the reference
+    ParseResult text of every walked layer. Returns bytes (and the n+1 packet offsets)."""
+    recs = np.ascontiguousarray(records).view(np.uint8).reshape(-1, 96)
+    n = len(recs)
+    need = ctypes.c_uint64(0)
+    h = ctx.h if ctx is not None else None
+    _check(lib().bt_format_records(h, recs.ctypes.data, n, fmt, None, 0, ctypes.byref(need), None))
+    out = np.empty(max(1, need.value), np.uint8)
+    off = np.empty(n + 1, np.uint64) if offsets else None
+    _check(lib().bt_format_records(h, recs.ctypes.data, n, fmt, out.ctypes.data, need.value, ctypes.byref(need),
+                                   off.ctypes.data if offsets else None))
+    text = out[:need.value].tobytes()
+    return (text, off) if offsets else text
 
 
 def device_count() -> int:

@@ -235,6 +235,24 @@ std::vector<GpuParsedBatch::DetectionResult> GpuParsedBatch::detectMultiple(size
     return out;
 }
 
+namespace {
+std::string format_recs(bt_ctx* ctx, const bt_rec* r, uint32_t n, uint32_t fmt) {
+    uint64_t need = 0;
+    if (bt_format_records(ctx, r, n, fmt, nullptr, 0, &need, nullptr) != BT_OK)
+        throw std::invalid_argument(std::string("GpuParsedBatch::format: ") + bt_last_error());
+    std::string s(need, '\0');
+    if (need && bt_format_records(ctx, r, n, fmt, &s[0], need, &need, nullptr) != BT_OK)
+        throw std::runtime_error(std::string("GpuParsedBatch::format: ") + bt_last_error());
+    return s;
+}
+}  // namespace
+
+std::string GpuParsedBatch::format(size_t i, uint32_t fmt) const { return format_recs(nullptr, &recs_.at(i), 1, fmt); }
+
+std::string GpuParsedBatch::format(uint32_t fmt) const {
+    return format_recs(ctx_, recs_.data(), (uint32_t)recs_.size(), fmt);
+}
+
 GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts) {
     if (bt_create(device, opts, &ctx_) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
@@ -245,6 +263,7 @@ GpuProtocolParser::~GpuProtocolParser() { bt_destroy(ctx_); }
 void GpuProtocolParser::run(GpuParsedBatch& b) {
     const uint32_t n = (uint32_t)b.frames_.size();
     b.recs_.resize(n);
+    b.ctx_ = ctx_;
     if (n && bt_parse_filter_ptrs(ctx_, b.frames_.data(), b.lens_.data(), n, b.recs_.data(), nullptr, nullptr,
                                   nullptr, nullptr) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());

@@ -51,12 +51,20 @@ public:
     bool is(size_t i, uint32_t bt_is_bit) const { return (recs_.at(i).detect_is & bt_is_bit) != 0; }
     bool isARP(size_t i) const { return (recs_.at(i).detect_is2 & BT_IS2_ARP) != 0; }
 
+    // Text of layer(i, k).toJsonString() / toXmlString() / toCsvString() /
+    // toHumanReadableString() (fmt = BT_FMT_*) for every walked layer, each followed by
+    // '\n', straight from the records (bt_format_records): packet i, or the whole batch
+    // on the context's host threads.
+    std::string format(size_t i, uint32_t fmt) const;
+    std::string format(uint32_t fmt) const;
+
 private:
     friend class GpuProtocolParser;
     std::vector<bt_rec> recs_;
     std::vector<const uint8_t*> frames_;
     std::vector<uint32_t> lens_;
     std::vector<Packet> keep_;   // owns the frames of a vector<Packet> batch
+    bt_ctx* ctx_ = nullptr;      // host pool for format(); owned by the GpuProtocolParser
 };
 
 class GpuProtocolParser {

@@ -405,6 +405,24 @@ int  bt_synchronize(bt_ctx* ctx);
 int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
                     uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
 
+/* ---- text output --------------------------------------------------------------
+ * The text the reference's ParseResult formatters print for every walked layer of
+ * records [0, n) (reference src/parser/ParserResult.cpp:214-349; each layer is the
+ * ParseResult ProtocolParser::parsePacket(slice, name) returns, wall-clock values 0),
+ * each layer's text followed by '\n', packets in order. Replaces a loop of
+ * parsePacket(...).toJsonString() etc. (e.g. src/beatrice_cli.cpp:1654-1660).
+ * `recs` are host bt_rec (AoS, e.g. from bt_parse_filter or bt_record_gather).
+ * out == NULL: size query (*out_len = bytes needed). pkt_off (optional, n + 1
+ * entries) receives each packet's start offset and the total. A `cap` below the
+ * size returns BT_E_INVALID_ARGUMENT with *out_len set. ctx (optional, may be NULL)
+ * lends its host thread pool; no device is used. */
+#define BT_FMT_JSON  0u   /* ParseResult::toJsonString          (:214-254) */
+#define BT_FMT_XML   1u   /* ParseResult::toXmlString           (:256-298) */
+#define BT_FMT_CSV   2u   /* ParseResult::toCsvString           (:300-313) */
+#define BT_FMT_HUMAN 3u   /* ParseResult::toHumanReadableString (:315-349) */
+int  bt_format_records(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format, char* out, uint64_t cap,
+                       uint64_t* out_len, uint64_t* pkt_off);
+
 /* host-side record gather from the device layout (after a D2H copy) */
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out);
 void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out);

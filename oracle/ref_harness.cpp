@@ -83,14 +83,20 @@ void detect(const uint8_t* f, uint32_t len, uint8_t* out) {
     out[2] = (uint8_t)(ProtocolDetector::isARP(v) | extra | (m.size() > 2 ? 0x80 : 0));
 }
 
-int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
+// `results`, when given, receives every walked layer's ParseResult in walk order.
+int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec, std::vector<ParseResult>* results = nullptr) {
+    auto layer = [&](const uint8_t* fr, uint32_t l, uint32_t off, const char* name) {
+        ParseResult r = w.layer(fr, l, off, name);
+        if (results) results->push_back(r);
+        return r;
+    };
     std::memset(rec, 0, 96);
     put<uint16_t>(rec, 14, (uint16_t)(len > 0xFFFF ? 0xFFFF : len));
     uint8_t present = 0x01, okb = 0;
     bool ok;
     int err = 0;
     do {
-        ParseResult eth = w.layer(f, len, 0, "ethernet");
+        ParseResult eth = layer(f, len, 0, "ethernet");
         if (!status_ok(eth, &ok)) { err = 1; break; }
         if (!ok) break;
         okb |= 0x01;
@@ -104,7 +110,7 @@ int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
         while (k < 2 && (et == 0x8100 || et == 0x88A8)) {
             uint32_t vo = 12 + 4 * k;
             present |= (uint8_t)(0x02 << k);
-            ParseResult v = w.layer(f, len, vo, "vlan");
+            ParseResult v = layer(f, len, vo, "vlan");
             if (!status_ok(v, &ok)) { err = 1; stop = true; break; }
             if (!ok) { stop = true; break; }
             okb |= (uint8_t)(0x02 << k);
@@ -121,7 +127,7 @@ int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
         if (et == 0x0800) {
             present |= 0x08;
             rec[26] = (uint8_t)o3;
-            ParseResult ip = w.layer(f, len, o3, "ipv4");
+            ParseResult ip = layer(f, len, o3, "ipv4");
             if (!status_ok(ip, &ok)) { err = 1; break; }
             if (!ok) break;
             okb |= 0x08;
@@ -143,7 +149,7 @@ int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
         } else if (et == 0x86DD) {
             present |= 0x10;
             rec[26] = (uint8_t)o3;
-            ParseResult ip = w.layer(f, len, o3, "ipv6");
+            ParseResult ip = layer(f, len, o3, "ipv6");
             if (!status_ok(ip, &ok)) { err = 1; break; }
             if (!ok) break;
             okb |= 0x10;
@@ -164,7 +170,7 @@ int walk(Walker& w, const uint8_t* f, uint32_t len, uint8_t* rec) {
         present |= l4;
         rec[27] = (uint8_t)o4;
         const char* name = l4 == 0x20 ? "tcp" : l4 == 0x40 ? "udp" : "icmp";
-        ParseResult t = w.layer(f, len, o4, name);
+        ParseResult t = layer(f, len, o4, name);
         if (!status_ok(t, &ok)) { err = 1; break; }
         if (!ok) break;
         okb |= l4;
@@ -263,6 +269,33 @@ int ref_parse(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32
         detect(f, len, records + (uint64_t)i * 96 + 88);
     }
     return bad;
+}
+
+// The reference's own ParseResult formatters (src/parser/ParserResult.cpp:214-349) over
+// every walked layer of every packet, each text followed by '\n': fmt 0 toJsonString,
+// 1 toXmlString, 2 toCsvString, 3 toHumanReadableString. Each field's parseTime is a
+// wall-clock duration_cast<microseconds> of one extractField call (ProtocolParser.cpp:256-261),
+// so it is set to 0 before formatting. Returns the bytes needed; writes when they fit `cap`.
+uint64_t ref_format(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n, int fmt, char* out,
+                    uint64_t cap) {
+    Walker w;
+    std::string all;
+    uint8_t rec[96];
+    std::vector<ParseResult> rs;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t len;
+        const uint8_t* f = frame_at(base, desc, stride, i, &len);
+        rs.clear();
+        walk(w, f, len, rec, &rs);
+        for (auto& r : rs) {
+            for (auto& kv : r.fields) kv.second.parseTime = std::chrono::microseconds(0);
+            all += fmt == 0 ? r.toJsonString() : fmt == 1 ? r.toXmlString() : fmt == 2 ? r.toCsvString()
+                                                                              : r.toHumanReadableString();
+            all += '\n';
+        }
+    }
+    if (out && all.size() <= cap) std::memcpy(out, all.data(), all.size());
+    return all.size();
 }
 
 // Per-packet PacketFilter::applyFilters(const Packet&) outcome:

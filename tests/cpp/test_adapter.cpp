@@ -188,6 +188,27 @@ static bool parser_case(const char* label, const Capture& cap) {
                       n.c_str());
         }
     }
+    // the reference's formatters over the materialised layers == bt_format_records text
+    // (wall-clock field parse times zeroed; ParserResult.cpp:214-349)
+    for (uint32_t fmt = BT_FMT_JSON; fmt <= BT_FMT_HUMAN; ++fmt) {
+        std::string want;
+        for (size_t i = 0; i < cap.packets.size() && i < 2000; ++i) {
+            const uint8_t* f = cap.packets[i].data();
+            const size_t len = cap.packets[i].length();
+            for (const auto& L : batch.layers(i)) {
+                ParseResult r = ref.parsePacket(std::vector<uint8_t>(f + L.offset, f + len), L.name);
+                for (auto& kv : r.fields) kv.second.parseTime = std::chrono::microseconds(0);
+                want += fmt == BT_FMT_JSON ? r.toJsonString() : fmt == BT_FMT_XML ? r.toXmlString()
+                      : fmt == BT_FMT_CSV ? r.toCsvString() : r.toHumanReadableString();
+                want += '\n';
+            }
+            const std::string one = batch.format(i, fmt);
+            CHECK(want.size() >= one.size() && want.compare(want.size() - one.size(), one.size(), one) == 0,
+                  "%s: packet %zu format %u differs", label, i, fmt);
+        }
+        const std::string all = batch.format(fmt);
+        CHECK(all.compare(0, want.size(), want) == 0, "%s: batch text (format %u) differs", label, fmt);
+    }
     // ProtocolDetector over the whole frame (ProtocolRegistry.cpp:353-487)
     for (size_t i = 0; i < cap.packets.size(); ++i) {
         const std::vector<uint8_t> v(cap.packets[i].data(), cap.packets[i].data() + cap.packets[i].length());

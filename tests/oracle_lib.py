@@ -80,6 +80,9 @@ def ref():
         L.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+        L.ref_format.restype = ctypes.c_uint64
+        L.ref_format.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
         _ref = L
     return _ref
 
@@ -103,6 +106,14 @@ def ref_parse(data, desc, n, stride=0):
     bad = ref().ref_parse(_ptr(data), _ptr(desc), stride, n, _ptr(rec))
     assert bad == 0, f"reference returned unexpected ParseStatus for {bad} packets"
     return rec
+
+
+def ref_format(data, desc, n, fmt, stride=0):
+    """The reference ParseResult formatter text of every walked layer (oracle/ref_harness.cpp)."""
+    need = ref().ref_format(_ptr(data), _ptr(desc), stride, n, fmt, None, 0)
+    out = np.empty(max(1, need), np.uint8)
+    ref().ref_format(_ptr(data), _ptr(desc), stride, n, fmt, out.ctypes.data, need)
+    return out[:need].tobytes()
 
 
 def ref_filter(data, desc, n, filters, stride=0):
