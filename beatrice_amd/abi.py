@@ -439,6 +439,10 @@ class DeviceRun:
             out["pass_idx"] = self.d_pidx.download(np.zeros(max(npass, 1), dtype=np.uint32))[:npass]
         return out
 
+    def n_pass(self) -> int:
+        self.ctx.synchronize()
+        return int(self.d_npass.download(np.zeros(1, dtype=np.uint32))[0]) if self.d_npass else 0
+
     def free(self):
         for b in (self.d_data, self.d_desc, self.d_rec, self.d_dec, self.d_ver, self.d_pidx, self.d_npass):
             if b is not None:
