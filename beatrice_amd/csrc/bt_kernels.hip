@@ -358,6 +358,17 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
     }
 }
 
+// LDS row (dwords) of one packet: the 128-B header window + 1 pad dword in descriptor
+// mode; in fixed-stride mode the whole frame (stride <= 64 B) + 1 pad dword. An odd row
+// stride spreads the per-lane reads over the banks. The smaller rows of the 16/32/64-B
+// strides cut a block's LDS (C2: 33.8 -> 17.4 KB), so the VGPR budget, not LDS, sets
+// the residency. Reads past a short frame's row land in the next row (or the block's
+// tail pad) and are never used: every field the walk keeps is gated by len.
+template <int FIXED_LOG2>
+__device__ constexpr uint32_t row_dw() {
+    return FIXED_LOG2 >= 0 && FIXED_LOG2 < 3 ? (4u << (FIXED_LOG2 >= 0 ? FIXED_LOG2 : 0)) + 1u : (uint32_t)kRowDwords;
+}
+
 template <int FIXED_LOG2>
 __device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32_t* img, uint32_t lane) {
     if constexpr (FIXED_LOG2 >= 0) {
@@ -366,19 +377,19 @@ __device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32
 #pragma unroll
         for (uint32_t j = 0; j < cpp; ++j) {
             const uint32_t g = j * 64u + lane;
-            uint32_t* dst = img + (g >> kL) * kRowDwords + (g & (cpp - 1u)) * 4u;
+            uint32_t* dst = img + (g >> kL) * row_dw<FIXED_LOG2>() + (g & (cpp - 1u)) * 4u;
             dst[0] = st.v[j].x; dst[1] = st.v[j].y; dst[2] = st.v[j].z; dst[3] = st.v[j].w;
         }
     } else {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-            uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + (lane & 3u) * 4u;
+            uint32_t* dst = img + (j * 16u + (lane >> 2)) * row_dw<FIXED_LOG2>() + (lane & 3u) * 4u;
             dst[0] = st.v[j].x; dst[1] = st.v[j].y; dst[2] = st.v[j].z; dst[3] = st.v[j].w;
         }
         if (st.wide) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
-                uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + 16u + (lane & 3u) * 4u;
+                uint32_t* dst = img + (j * 16u + (lane >> 2)) * row_dw<FIXED_LOG2>() + 16u + (lane & 3u) * 4u;
                 dst[0] = st.v[4 + j].x; dst[1] = st.v[4 + j].y; dst[2] = st.v[4 + j].z; dst[3] = st.v[4 + j].w;
             }
         }
@@ -418,7 +429,7 @@ __device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint
     }
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
-        uint32_t* dst = img + (j * 16u + (lane >> 2)) * kRowDwords + c * 4u;
+        uint32_t* dst = img + (j * 16u + (lane >> 2)) * row_dw<FIXED_LOG2>() + c * 4u;
         dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
     }
 }
@@ -426,12 +437,13 @@ __device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint
 template <int FIXED_LOG2, int REC, bool FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
-    __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRowDwords];
+    constexpr uint32_t kRow = row_dw<FIXED_LOG2>();
+    __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRow + 32];   // + tail pad for over-reads
     extern __shared__ uint4 dyn_lds[];   // PAYLOAD DFA pool (a.dfa_bytes), else empty
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = threadIdx.x >> 6;
-    uint32_t* img = lds_all + wid * (kWave * kRowDwords);
-    const uint32_t* row = img + lane * kRowDwords;
+    uint32_t* img = lds_all + wid * (kWave * kRow);
+    const uint32_t* row = img + lane * kRow;
     if (FILTER && a.dfa_bytes) {   // uniform: the whole block copies the pool once
         const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
         for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
@@ -534,7 +546,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                 if (__ballot(open) == 0ull) break;
                 uint32_t r;
                 if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
-                    r = open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRowDwords, my_off, len, w0,
+                    r = open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0,
                                             staged_sh)
                              : 0u;
                 else
