@@ -70,6 +70,8 @@ OPT_NT_LOADS = 0x40
 OPT_CACHE_DEFAULT = 0x80
 OPT_SPIN_SYNC = 0x100
 OPT_PAYLOAD_HOST = 0x200
+OPT_WIDE_NEVER = 0x400
+OPT_WIDE_ALWAYS = 0x800
 
 
 DESC_PACKED, DESC_XDP = 0, 1

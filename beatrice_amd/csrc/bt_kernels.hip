@@ -300,6 +300,17 @@ struct Stage {
     bool wide;
 };
 
+// Round A of a wide tile reads the packet's window [a0, a0 + sq + min(len, need_max))
+// only up to the end of a0's 128-B line: the line is then fetched once, and round B reads
+// the next line's chunks only if the walked headers reach them. (Reading the whole window
+// up front, the first version, fetched the second line for 1.78 instead of 1.60 lines per
+// C4 packet.)
+__device__ __forceinline__ uint32_t round_a_end_wide(uint64_t a0, uint32_t sq, uint32_t len, uint32_t need_max) {
+    const uint32_t line_rem = 128u - ((uint32_t)a0 & 127u);
+    const uint32_t want = sq + (len < need_max ? len : need_max);
+    return want < line_rem ? want : line_rem;
+}
+
 template <int FIXED_LOG2>
 __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint32_t lane, Stage<FIXED_LOG2>& st,
                                             bool wide, uint32_t need_max) {
@@ -336,6 +347,11 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
         const uint32_t off_lo = (uint32_t)st.off, off_hi = (uint32_t)(st.off >> 32);
         const uint32_t c = lane & 3u;
         st.wide = wide;
+        // Non-temporal header loads pay off in two-round-free tiles (C3: 0.595 -> 0.564 ms),
+        // but in wide tiles they raised C4's read traffic from the exact-line 214 to 235 B
+        // per packet (rocprofv3 FETCH_SIZE, tools/gpu_fetch_modes.sh); wide tiles and
+        // round B use the default policy.
+        const bool ntl = (a.nt & 2u) && !wide;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t q = j * 16u + (lane >> 2);
@@ -347,12 +363,14 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
             const uint32_t sq = (uint32_t)qo & 15u;
             st.qa0[j] = a0;
             const bool live_q = p0 + q < a.n;
-            const bool ok = live_q && (16u * c < sq + ql) && (addr + 16u <= a.bytes);
-            st.v[j] = ok ? ld16(a.base + addr, a.nt & 2u) : make_uint4(0, 0, 0, 0);
-            if (wide) {   // chunks 4..7 up to the longest header the walk can read
-                const uint32_t nq = ql < need_max ? ql : need_max;
-                const bool okb = live_q && (16u * (c + 4u) < sq + nq) && (addr + 64u + 16u <= a.bytes);
-                st.v[4 + j] = okb ? ld16(a.base + addr + 64u, a.nt & 2u) : make_uint4(0, 0, 0, 0);
+            // bytes from a0 this round may read: the frame; when wide, only up to the end
+            // of a0's 128-B line (round B takes the next line, and only what is needed)
+            const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
+            const bool ok = live_q && (16u * c < a_end) && (addr + 16u <= a.bytes);
+            st.v[j] = ok ? ld16(a.base + addr, ntl) : make_uint4(0, 0, 0, 0);
+            if (wide) {   // chunks 4..7 of the same line
+                const bool okb = live_q && (16u * (c + 4u) < a_end) && (addr + 64u + 16u <= a.bytes);
+                st.v[4 + j] = okb ? ld16(a.base + addr + 64u, false) : make_uint4(0, 0, 0, 0);
             }
         }
     }
@@ -413,24 +431,35 @@ __device__ __forceinline__ uint32_t header_end(const uint32_t* row, uint32_t s, 
     return end < len ? end : len;
 }
 
-// Round B: chunks 4..7 for the packets whose headers run past round A's 64 B.
+// Round B: the chunks [lo, hi) of each packet's window that round A did not read and
+// the walk needs (my_b = lo | hi << 8, in chunks / bytes from a0; hi = 0: none). Lane
+// (lane & 3) of a packet's four takes chunks lo + (lane & 3) and, when `second`, + 4.
 template <int FIXED_LOG2>
 __device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint32_t lane, const uint64_t* qa0,
-                                             uint32_t my_need, uint32_t* img) {
-    const uint32_t c = 4u + (lane & 3u);
-    uint4 v[4];
+                                             uint32_t my_b, uint32_t* img, bool second) {
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t q = j * 16u + (lane >> 2);
-        const uint32_t qn = (uint32_t)__shfl((int)my_need, (int)q);   // bytes of q's window needed
-        const uint64_t addr = qa0[j] + 16u * c;
-        const bool ok = (t * 64u + q < a.n) && (16u * c < qn) && (addr + 16u <= a.bytes);
-        v[j] = ok ? ld16(a.base + addr, a.nt & 2u) : make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t k = 0; k < 2; ++k) {
+        if (k == 1 && !second) break;
+        uint4 v[4];
+        uint32_t cs[4];
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        uint32_t* dst = img + (j * 16u + (lane >> 2)) * row_dw<FIXED_LOG2>() + c * 4u;
-        dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t q = j * 16u + (lane >> 2);
+            const uint32_t qb = (uint32_t)__shfl((int)my_b, (int)q);
+            const uint32_t c = (qb & 0xFFu) + (lane & 3u) + 4u * k;
+            const uint64_t addr = qa0[j] + 16u * c;
+            const bool want = c < 8u && (16u * c < (qb >> 8));   // never overwrite round A's chunks
+            cs[j] = want ? c : 8u;
+            const bool ok = want && (t * 64u + q < a.n) && (addr + 16u <= a.bytes);
+            v[j] = ok ? ld16(a.base + addr, false) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            if (cs[j] < 8u) {
+                uint32_t* dst = img + (j * 16u + (lane >> 2)) * row_dw<FIXED_LOG2>() + cs[j] * 4u;
+                dst[0] = v[j].x; dst[1] = v[j].y; dst[2] = v[j].z; dst[3] = v[j].w;
+            }
+        }
     }
 }
 
@@ -490,14 +519,24 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         if constexpr (FIXED_LOG2 < 0) {
             if (REC != kRecNone) {   // filter-only needs <= 38 B: round A always suffices
                 const uint32_t s0 = (uint32_t)my_off & 15u;
-                const uint32_t end = live ? s0 + header_end(row, s0, my_len, FILTER ? kNeedFilter : 0u) : 0u;
-                const uint32_t my_need = end > 64u ? end : 0u;
-                const uint64_t needs_b = __ballot(my_need != 0u);
-                if (!this_wide && needs_b != 0ull) {
-                    load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_need, img);
+                // bytes from a0 that round A read, and whether they hold what header_end reads;
+                // the floor of 38 B covers the PacketFilter gates and the detector column
+                const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s0, my_len, need_max)
+                                                 : min(64u, s0 + my_len);
+                const bool cov = a_end >= s0 + min(my_len, 28u);
+                const uint32_t end = !live ? 0u
+                                   : cov ? s0 + header_end(row, s0, my_len, kNeedFilter)
+                                         : s0 + min(my_len, need_max);
+                const uint32_t lo = (a_end + 15u) >> 4;   // first chunk round A did not read
+                const bool my_nb = end > 16u * lo;
+                const uint64_t needs_b = __ballot(my_nb);
+                if (needs_b != 0ull) {
+                    const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
+                    load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
                     wave_lds_sync();
                 }
-                wide = __popcll(needs_b) > 32;   // decides the wave's next issue
+                wide = __popcll(__ballot(end > 64u)) > 32;   // decides the wave's next issue
+                if (a.nt & 12u) wide = (a.nt & 8u) != 0u;   // A/B knobs
             }
         }
 

@@ -251,6 +251,8 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     else a.nt = 1u | (b->desc ? 2u : 0u);
     if (c->opts.flags & BT_OPT_NT_STORES) a.nt |= 1u;
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
+    if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
+    if (c->opts.flags & BT_OPT_WIDE_ALWAYS) a.nt |= 8u;
     int rec = kRecNone;
     if (o->records) {
         if (aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) rec = kRecAoS;

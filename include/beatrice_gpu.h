@@ -267,6 +267,8 @@ typedef struct bt_opts {
 #define BT_OPT_CACHE_DEFAULT 0x80u /* default cache policy everywhere (A/B only)         */
 #define BT_OPT_SPIN_SYNC 0x100u    /* spin-wait host synchronisation (bench / latency)   */
 #define BT_OPT_PAYLOAD_HOST 0x200u /* keep every PAYLOAD filter on the host (std::regex) */
+#define BT_OPT_WIDE_NEVER 0x400u   /* descriptor mode: always two-round loads (A/B only)   */
+#define BT_OPT_WIDE_ALWAYS 0x800u  /* descriptor mode: always wide round A (A/B only)      */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
