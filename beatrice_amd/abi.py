@@ -100,6 +100,7 @@ EXPORTS = [
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_search", "bt_payload_dfa_eval", "bt_format_records",
+    "bt_record_unpack", "bt_record_slabs",
 ]
 
 _lib = None
@@ -147,8 +148,12 @@ def lib() -> ctypes.CDLL:
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
         "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
         "bt_format_records": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, ctypes.POINTER(u64), vp]),
+        "bt_record_unpack": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, ctypes.POINTER(u64)]),
+        "bt_record_slabs": (u32, [vp]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(L, name):   # an older build under BT_LIB_PATH (A/B runs); tests check EXPORTS
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -384,14 +389,60 @@ def payload_dfa_eval(blob: bytes, frame) -> bool:
     return bool(lib().bt_payload_dfa_eval(blob, f, len(f)))
 
 
-def untile_records(buf: np.ndarray, n: int, planes: bool = False) -> np.ndarray:
-    """bt_rec[n] (AoS) from the device record layout (include/beatrice_gpu.h)."""
-    if planes:
-        p = buf[: 6 * n * 16].reshape(6, n, 16)
-        return np.ascontiguousarray(p.transpose(1, 0, 2)).reshape(n, 96)
+def untile_records(buf: np.ndarray, n: int, planes: bool = False, ctx: "Context | None" = None,
+                   n_cap: int | None = None) -> np.ndarray:
+    """bt_rec[n] (AoS) from the packed device record layout (include/beatrice_gpu.h),
+    unpacked by bt_record_unpack."""
+    out = np.zeros((n, BT_REC_BYTES), np.uint8)
+    buf = np.ascontiguousarray(buf)
+    _check(lib().bt_record_unpack(ctx.h if ctx is not None else None, buf.ctypes.data,
+                                  n if n_cap is None else n_cap, n, int(planes), out.ctypes.data, None))
+    return out
+
+
+def record_slabs(rec: np.ndarray) -> np.ndarray:
+    """Slabs the packed device form of each bt_rec occupies (bt_record_slabs)."""
+    ok = np.ascontiguousarray(rec).view(np.uint8).reshape(-1, BT_REC_BYTES)[:, 25].astype(np.int64)
+    nd = 8 + np.where(ok & L_IPV4, 5, np.where(ok & L_IPV6, 10, 0)) + \
+        np.where(ok & L_TCP, 5, np.where(ok & (L_UDP | L_ICMP), 2, 0))
+    return (nd + 3) // 4
+
+
+def pack_records(rec: np.ndarray) -> np.ndarray:
+    """numpy restatement of the kernel's pack_record (test helper): bt_rec[n] -> [n, 24]
+    packed dwords, zero past each record's stored slabs."""
+    r = np.ascontiguousarray(rec).view(np.uint8).reshape(-1, BT_REC_BYTES).view("<u4").astype(np.uint64)
+    n = len(r)
+    ok = (r[:, 6] >> 8) & 0xFF
+    ok4, ok6 = (ok & L_IPV4) != 0, (ok & L_IPV6) != 0
+    c = np.zeros((n, 24), np.uint64)
+    c[:, 0:4] = r[:, 0:4]
+    c[:, 4] = r[:, 6]
+    c[:, 5] = (r[:, 5] & 0xFFFF) | (r[:, 4] & 0xFFFF0000)
+    c[:, 6] = (r[:, 5] >> 16) | ((r[:, 22] << 16) & 0xFFFF0000)
+    c[:, 7] = (r[:, 22] >> 16) & 0xFF
+    v4 = np.stack([(r[:, 7] & 0xFF) | ((r[:, 7] >> 8) & 0xFF00) | ((r[:, 7] >> 8) & 0xFF0000) | ((r[:, 8] & 0xFF) << 24),
+                   (r[:, 8] >> 16) | ((r[:, 9] & 0xFFFF) << 16), (r[:, 9] >> 16) | ((r[:, 10] & 0xFFFF) << 16),
+                   r[:, 11], r[:, 12], r[:, 17], r[:, 18], r[:, 19], r[:, 20], r[:, 21]], axis=1)
+    c[:, 8:18] = np.where(ok4[:, None], v4, np.where(ok6[:, None], r[:, 7:17], 0))
+    c[:, 18:23] = np.where(ok6[:, None], r[:, 17:22], 0)
+    return c.astype(np.uint32)
+
+
+def tile_packed(c: np.ndarray, nslab: np.ndarray, planes: bool = False, seed: int = 1) -> np.ndarray:
+    """Test helper: packed records [n, 24] in the device layout (tiled, or plane-major
+    with n_cap = n). Slabs a record does not store hold random bytes, as on the device."""
+    n = len(c)
     nt = (n + 63) // 64
-    t = buf[: nt * 6144].reshape(nt, 6, 64, 16)
-    return np.ascontiguousarray(t.transpose(0, 2, 1, 3)).reshape(nt * 64, 96)[:n]
+    rng = np.random.default_rng(seed)
+    slabs = c.reshape(n, 6, 16 // 4).view(np.uint8).reshape(n, 6, 16).copy()
+    keep = np.arange(6)[None, :] < nslab[:, None]
+    slabs[~keep] = rng.integers(0, 256, size=(int((~keep).sum()), 16), dtype=np.uint8)
+    if planes:
+        return np.ascontiguousarray(slabs.transpose(1, 0, 2)).reshape(-1)
+    t = np.zeros((nt * 64, 6, 16), np.uint8)
+    t[:n] = slabs
+    return np.ascontiguousarray(t.reshape(nt, 64, 6, 16).transpose(0, 2, 1, 3)).reshape(-1)
 
 
 class DeviceRun:
@@ -440,6 +491,19 @@ class DeviceRun:
             out["n_pass"] = npass
             out["pass_idx"] = self.d_pidx.download(np.zeros(max(npass, 1), dtype=np.uint32))[:npass]
         return out
+
+    def record_slabs(self) -> int:
+        """Total 16-B slabs the last run stored (packed records), counted on the host."""
+        if not self.d_rec:
+            return 0
+        if not hasattr(lib(), "bt_record_unpack"):   # A/B against a build from before packed records
+            return 6 * self.n
+        self.ctx.synchronize()
+        buf = self.d_rec.download(np.zeros(self.d_rec.nbytes, np.uint8))
+        tot = ctypes.c_uint64(0)
+        _check(lib().bt_record_unpack(self.ctx.h, buf.ctypes.data, self.n, self.n,
+                                      int(bool(self.ctx.flags & OPT_RECORDS_PLANES)), None, ctypes.byref(tot)))
+        return int(tot.value)
 
     def n_pass(self) -> int:
         self.ctx.synchronize()

@@ -110,8 +110,15 @@ __device__ __forceinline__ uint32_t detect_word(const uint32_t* w0, uint32_t len
 // The layer walk + field extraction for one packet whose byte 0 sits at byte `s` of
 // the lane's LDS row. Field semantics: ProtocolRegistry.cpp tables, extractValue<T>
 // big-endian decode, all-or-nothing per layer (ProtocolParser.cpp:244-247).
-__device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, uint32_t len,
-                                             const uint32_t* w0, Parsed& p) {
+// PACKED = false: p.r is the 96-B bt_rec (host AoS path); returns 6.
+// PACKED = true:  p.r is the packed device record (include/beatrice_gpu.h): the fields
+// of the layers that parsed, L4 right after L3, so an Eth/IPv4/UDP packet fills 4
+// slabs instead of 6; returns the slab count (2..6). Dwords past it are 0, because
+// every field of a layer that did not parse is 0. Both forms come from the same
+// branch-free selects, so the packed form costs no registers beyond bt_rec's.
+template <bool PACKED>
+__device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s, uint32_t len,
+                                                 const uint32_t* w0, Parsed& p) {
     const uint32_t pl = len > 0xFFFFu ? 0xFFFFu : len;
     // Ethernet (ProtocolRegistry.cpp:150-159): total length 14
     const bool eth_ok = len >= 14;
@@ -130,9 +137,8 @@ __device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, ui
     const bool v1ok = v1 && len >= 20;
     const bool has_et2 = v1ok && len >= 22;
     const uint32_t et2 = be16_of(w0, 20);
-    const uint32_t tci0 = be16_of(w0, 14), tci1 = be16_of(w0, 18);
-    p.r[4] = (v0ok ? et0 : 0u) | ((v1ok ? et1 : 0u) << 16);
-    p.r[5] = (v0ok ? tci0 : 0u) | ((v1ok ? tci1 : 0u) << 16);
+    const uint32_t tp0 = v0ok ? et0 : 0u, tp1 = v1ok ? et1 : 0u;
+    const uint32_t tc0 = v0ok ? be16_of(w0, 14) : 0u, tc1 = v1ok ? be16_of(w0, 18) : 0u;
 
     bool have_et;
     uint32_t l3et, o3;
@@ -153,35 +159,22 @@ __device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, ui
     if (v4ok && o4 <= len) l4 = proto == 6 ? BT_L_TCP : proto == 17 ? BT_L_UDP : proto == 1 ? BT_L_ICMP : 0u;
     if (v6ok) l4 = nh == 6 ? BT_L_TCP : nh == 17 ? BT_L_UDP : 0u;
 
-    // L3 union at byte 28 (dwords 7..16); branch-free selects keep p.r in VGPRs
-    {   // IPv4: ProtocolRegistry.cpp:161-178, IPv6: :180-192
-        const uint32_t v4[10] = {b0 | (b0 << 8) | (byte_of(w3, 1) << 16) | (byte_of(w3, 8) << 24),
-                                 proto | (be16_of(w3, 2) << 16),
-                                 be16_of(w3, 4) | (be16_of(w3, 6) << 16),
-                                 be16_of(w3, 10),
-                                 w3[3], w3[4], 0u, 0u, 0u, 0u};
-        const uint32_t v6[10] = {be32_of(w3, 0),
-                                 be16_of(w3, 4) | (nh << 16) | (byte_of(w3, 7) << 24),
-                                 w3[2], w3[3], w3[4], w3[5], w3[6], w3[7], w3[8], w3[9]};
-#pragma unroll
-        for (int k = 0; k < 10; ++k) p.r[7 + k] = v4ok ? v4[k] : (v6ok ? v6[k] : 0u);
-    }
-
-    // L4 union at byte 68 (dwords 17..21)
+    // L4 fields (bt_rec dwords 17..21): TCP :194-209, UDP :211-221, ICMP :223-234
     uint32_t w4[5];
     window<5>(row, s + (l4 ? o4 : 0u), w4);
     const bool tcp_ok = l4 == BT_L_TCP && len >= o4 + 20;
     const bool udp_ok = l4 == BT_L_UDP && len >= o4 + 8;
     const bool icmp_ok = l4 == BT_L_ICMP && len >= o4 + 8;
-    {   // TCP :194-209, UDP :211-221, ICMP :223-234
+    uint32_t l4v[5];
+    {
         const uint32_t ports = be16_of(w4, 0) | (be16_of(w4, 2) << 16);
         const uint32_t icmp0 = byte_of(w4, 0) | (byte_of(w4, 1) << 8) | (be16_of(w4, 2) << 16);
         const uint32_t pair45 = be16_of(w4, 4) | (be16_of(w4, 6) << 16);
-        p.r[17] = tcp_ok || udp_ok ? ports : (icmp_ok ? icmp0 : 0u);
-        p.r[18] = tcp_ok ? be32_of(w4, 4) : (udp_ok || icmp_ok ? pair45 : 0u);
-        p.r[19] = tcp_ok ? be32_of(w4, 8) : 0u;
-        p.r[20] = tcp_ok ? byte_of(w4, 12) | (byte_of(w4, 13) << 8) | (be16_of(w4, 14) << 16) : 0u;
-        p.r[21] = tcp_ok ? be16_of(w4, 16) | (be16_of(w4, 18) << 16) : 0u;
+        l4v[0] = tcp_ok || udp_ok ? ports : (icmp_ok ? icmp0 : 0u);
+        l4v[1] = tcp_ok ? be32_of(w4, 4) : (udp_ok || icmp_ok ? pair45 : 0u);
+        l4v[2] = tcp_ok ? be32_of(w4, 8) : 0u;
+        l4v[3] = tcp_ok ? byte_of(w4, 12) | (byte_of(w4, 13) << 8) | (be16_of(w4, 14) << 16) : 0u;
+        l4v[4] = tcp_ok ? be16_of(w4, 16) | (be16_of(w4, 18) << 16) : 0u;
     }
 
     const uint32_t l3bit = is4 ? BT_L_IPV4 : is6 ? BT_L_IPV6 : 0u;
@@ -189,9 +182,42 @@ __device__ __forceinline__ void parse_packet(const uint32_t* row, uint32_t s, ui
     const uint32_t okbits = (eth_ok ? BT_L_ETH : 0u) | (v0ok ? BT_L_VLAN0 : 0u) | (v1ok ? BT_L_VLAN1 : 0u) |
                             (v4ok ? BT_L_IPV4 : 0u) | (v6ok ? BT_L_IPV6 : 0u) |
                             (tcp_ok ? BT_L_TCP : 0u) | (udp_ok ? BT_L_UDP : 0u) | (icmp_ok ? BT_L_ICMP : 0u);
-    p.r[6] = present | (okbits << 8) | ((l3bit ? o3 : 0u) << 16) | ((l4 ? o4 : 0u) << 24);
-    p.r[22] = detect_word(w0, len);
+    const uint32_t meta = present | (okbits << 8) | ((l3bit ? o3 : 0u) << 16) | ((l4 ? o4 : 0u) << 24);
+    const uint32_t det = detect_word(w0, len);
+    // IPv6 (ProtocolRegistry.cpp:180-192) is stored the same way in both forms
+    const uint32_t v6[10] = {be32_of(w3, 0), be16_of(w3, 4) | (nh << 16) | (byte_of(w3, 7) << 24),
+                             w3[2], w3[3], w3[4], w3[5], w3[6], w3[7], w3[8], w3[9]};
     p.r[23] = 0;
+    if constexpr (!PACKED) {
+        p.r[4] = tp0 | (tp1 << 16);
+        p.r[5] = tc0 | (tc1 << 16);
+        p.r[6] = meta;
+        // IPv4 (ProtocolRegistry.cpp:161-178) in bt_rec's padded layout: L3 union at 28
+        const uint32_t v4[10] = {b0 | (b0 << 8) | (byte_of(w3, 1) << 16) | (byte_of(w3, 8) << 24),
+                                 proto | (be16_of(w3, 2) << 16), be16_of(w3, 4) | (be16_of(w3, 6) << 16),
+                                 be16_of(w3, 10), w3[3], w3[4], 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 10; ++k) p.r[7 + k] = v4ok ? v4[k] : (v6ok ? v6[k] : 0u);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) p.r[17 + k] = l4v[k];
+        p.r[22] = det;
+        return BT_REC_SLABS;
+    } else {
+        p.r[4] = meta;
+        p.r[5] = tc0 | (tp1 << 16);   // tpid0 is the ethertype
+        p.r[6] = tc1 | (det << 16);
+        p.r[7] = (det >> 16) & 0xFFu;
+        // IPv4 without bt_rec's pads and its duplicate version byte: 5 dwords
+        const uint32_t v4[5] = {b0 | (byte_of(w3, 1) << 8) | (byte_of(w3, 8) << 16) | (proto << 24),
+                                be16_of(w3, 2) | (be16_of(w3, 4) << 16), be16_of(w3, 6) | (be16_of(w3, 10) << 16),
+                                w3[3], w3[4]};
+#pragma unroll
+        for (int j = 0; j < 10; ++j) p.r[8 + j] = v4ok ? (j < 5 ? v4[j] : l4v[j - 5]) : (v6ok ? v6[j] : 0u);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) p.r[18 + j] = v6ok ? l4v[j] : 0u;
+        const uint32_t nd = 8u + (v4ok ? 5u : v6ok ? 10u : 0u) + (tcp_ok ? 5u : (udp_ok || icmp_ok) ? 2u : 0u);
+        return (nd + 3u) >> 2;
+    }
 }
 
 // One filter slot on one packet: 1 pass, 0 reject, 2 throw, 3 host.
@@ -548,19 +574,21 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 
         if (REC != kRecNone && live) {
             Parsed p;
-            parse_packet(row, s, len, w0, p);
-            if (REC == kRecPlanes) {
-                uint4* planes = reinterpret_cast<uint4*>(a.records);
+            if (REC == kRecPlanes || REC == kRecTiled) {
+                // packed device record: its first `ns` slabs (2..6) hold every parsed field
+                const uint32_t ns = parse_packet<true>(row, s, len, w0, p);
+                uint4* dst = reinterpret_cast<uint4*>(a.records) +
+                             (REC == kRecTiled ? (uint64_t)t * (BT_REC_SLABS * 64) + lane : (uint64_t)my);
+                const uint64_t kstride = REC == kRecTiled ? 64ull : (uint64_t)a.n_cap;
+                // Slab k is stored by the whole wave when any lane needs it (the other
+                // lanes' dwords there are 0), so every store covers whole 128-B lines.
 #pragma unroll
-                for (int k = 0; k < BT_REC_SLABS; ++k)
-                    st16(planes + (uint64_t)k * a.n_cap + my, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
-            } else if (REC == kRecTiled) {
-                // [tile][slab][lane]: the tile's six 1-KiB slab stores land back to back
-                uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
-#pragma unroll
-                for (int k = 0; k < BT_REC_SLABS; ++k)
-                    st16(tile + k * 64 + lane, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
+                for (uint32_t k = 0; k < BT_REC_SLABS; ++k)
+                    if (k < 2u || __ballot(k < ns) != 0ull)   // [tile][slab][lane]: 1 KiB per slab and wave
+                        st16(dst + k * kstride, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]),
+                             a.nt & 1u);
             } else {
+                parse_packet<false>(row, s, len, w0, p);
                 uint4* rec = reinterpret_cast<uint4*>(a.records + (uint64_t)my * BT_REC_BYTES);
 #pragma unroll
                 for (int k = 0; k < BT_REC_SLABS; ++k)

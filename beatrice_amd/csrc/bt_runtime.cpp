@@ -746,18 +746,95 @@ int bt_synchronize(bt_ctx* c) {
     return BT_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Unpacks the packed device record (bt_kernels.hip pack_record; layout in
+// beatrice_gpu.h) into a bt_rec. `slab(k)` returns the k-th 16-B slab; only the slabs
+// the record holds are read.
+template <class Slab>
+void unpack_record(Slab slab, bt_rec* out) {
+    uint32_t c[24] = {};
+    std::memcpy(c, slab(0), 16);
+    std::memcpy(c + 4, slab(1), 16);
+    const uint32_t ok = (c[4] >> 8) & 0xFFu;
+    const bool ok4 = ok & BT_L_IPV4, ok6 = ok & BT_L_IPV6;
+    const uint32_t l4d = (ok & BT_L_TCP) ? 5u : (ok & (BT_L_UDP | BT_L_ICMP)) ? 2u : 0u;
+    const uint32_t nd = 8u + (ok4 ? 5u : ok6 ? 10u : 0u) + l4d;
+    for (uint32_t k = 2; 4 * k < nd; ++k) std::memcpy(c + 4 * k, slab(k), 16);
+    uint32_t r[24] = {};
+    r[0] = c[0]; r[1] = c[1]; r[2] = c[2]; r[3] = c[3];
+    r[4] = ((ok & BT_L_VLAN0) ? (c[3] & 0xFFFFu) : 0u) | (c[5] & 0xFFFF0000u);   // tpid0 == ethertype
+    r[5] = (c[5] & 0xFFFFu) | (c[6] << 16);
+    r[6] = c[4];
+    const uint32_t* l4 = nullptr;
+    if (ok4) {
+        const uint32_t b0 = c[8] & 0xFFu, tos = (c[8] >> 8) & 0xFFu, ttl = (c[8] >> 16) & 0xFFu, proto = c[8] >> 24;
+        r[7] = b0 | (b0 << 8) | (tos << 16) | (ttl << 24);
+        r[8] = proto | (c[9] << 16);
+        r[9] = (c[9] >> 16) | (c[10] << 16);
+        r[10] = c[10] >> 16;
+        r[11] = c[11];
+        r[12] = c[12];
+        l4 = c + 13;
+    } else if (ok6) {
+        for (int j = 0; j < 10; ++j) r[7 + j] = c[8 + j];
+        l4 = c + 18;
+    }
+    if (l4)
+        for (uint32_t j = 0; j < l4d; ++j) r[17 + j] = l4[j];
+    r[22] = (c[6] >> 16) | ((c[7] & 0xFFu) << 16);
+    std::memcpy(out, r, sizeof(r));
+}
+
+}  // namespace
+
+extern "C" {
+
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out) {
     const uint8_t* p = static_cast<const uint8_t*>(records);
-    uint8_t* o = reinterpret_cast<uint8_t*>(out);
-    for (int k = 0; k < BT_REC_SLABS; ++k)
-        std::memcpy(o + 16 * k, p + (((size_t)(i / 64) * BT_REC_SLABS + k) * 64 + (i % 64)) * 16, 16);
+    unpack_record([&](uint32_t k) { return p + (((size_t)(i / 64) * BT_REC_SLABS + k) * 64 + (i % 64)) * 16; }, out);
     (void)n_cap;
 }
 
 void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out) {
     const uint8_t* p = static_cast<const uint8_t*>(planes);
-    uint8_t* o = reinterpret_cast<uint8_t*>(out);
-    for (int k = 0; k < BT_REC_SLABS; ++k) std::memcpy(o + 16 * k, p + ((size_t)k * n_cap + i) * 16, 16);
+    unpack_record([&](uint32_t k) { return p + ((size_t)k * n_cap + i) * 16; }, out);
+}
+
+int bt_record_unpack(bt_ctx* ctx, const void* records, uint32_t n_cap, uint32_t n, uint32_t planes, bt_rec* out,
+                     uint64_t* slabs) {
+    if ((!records || (!out && !slabs)) && n) return fail(BT_E_INVALID_ARGUMENT, "null records / out");
+    std::atomic<uint64_t> total{0};
+    const uint8_t* p = static_cast<const uint8_t*>(records);
+    host_parallel(ctx, [&](unsigned w, unsigned T) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * w / T), hi = (uint32_t)((uint64_t)n * (w + 1) / T);
+        uint64_t cnt = 0;
+        bt_rec r;
+        for (uint32_t i = lo; i < hi; ++i) {
+            if (out) {
+                if (planes) bt_record_gather_planes(records, n_cap, i, out + i);
+                else bt_record_gather(records, n_cap, i, out + i);
+                if (slabs) cnt += bt_record_slabs(out + i);
+            } else {   // count only: the ok byte sits in slab 1
+                const uint8_t* s1 = planes ? p + ((size_t)n_cap + i) * 16
+                                           : p + (((size_t)(i / 64) * BT_REC_SLABS + 1) * 64 + (i % 64)) * 16;
+                r.ok = s1[1];
+                cnt += bt_record_slabs(&r);
+            }
+        }
+        total += cnt;
+    });
+    if (slabs) *slabs = total.load();
+    return BT_OK;
+}
+
+uint32_t bt_record_slabs(const bt_rec* r) {
+    const uint32_t ok = r->ok;
+    const uint32_t nd = 8u + ((ok & BT_L_IPV4) ? 5u : (ok & BT_L_IPV6) ? 10u : 0u) +
+                        ((ok & BT_L_TCP) ? 5u : (ok & (BT_L_UDP | BT_L_ICMP)) ? 2u : 0u);
+    return (nd + 3u) >> 2;
 }
 
 }  // extern "C"

@@ -6,7 +6,8 @@
 
 A step = one bt_parse_filter_device() pass over one synthetic 16M-packet batch that
 is already resident in HBM. Default workload (N=1): BASELINE.json configs[1] — C2,
-16,777,216 fixed 64 B Eth/IPv4/UDP frames, parse-only (96-B bt_rec per packet).
+16,777,216 fixed 64 B Eth/IPv4/UDP frames, parse-only (one packed record per packet:
+64 B on the device for Eth/IPv4/UDP, unpacked to the 96-B bt_rec by the host).
 `--config c3` runs configs[2] (IMIX parse + 5-tuple PacketFilter + ordered
 compaction). Multi-GPU is weak scaling: every rank owns its own 16M-packet batch on
 its own device (packet batches shard with no collective; the only cross-rank traffic
@@ -65,9 +66,10 @@ def payload_extra_bytes(data: np.ndarray, desc: np.ndarray) -> float:
     return float(extra.sum())
 
 
-def algorithmic_bytes(desc: np.ndarray, fixed: bool, parse: bool, filt: bool, n_pass: int) -> float:
-    """Bytes the main kernel must move per launch (SURVEY.md §8(d) formula):
-    min(len,128) header read + 8 B descriptor (0 for fixed stride) + 96 B record
+def algorithmic_bytes(desc: np.ndarray, fixed: bool, rec_bytes: float, filt: bool) -> float:
+    """Bytes the main kernel must move per launch (SURVEY.md §8(d) formula, R = the
+    packed record's stored slabs, counted from this run's records):
+    min(len,128) header read + 8 B descriptor (0 for fixed stride) + R
     + 1 B decision + 1/8 B verdict bit (the ordered pass-index list is written by the
     compaction kernels and is not counted here)."""
     n = len(desc)
@@ -75,8 +77,7 @@ def algorithmic_bytes(desc: np.ndarray, fixed: bool, parse: bool, filt: bool, n_
     b = float(np.minimum(lens, 128).sum())
     if not fixed:
         b += 8.0 * n
-    if parse:
-        b += 96.0 * n
+    b += rec_bytes
     if filt:
         b += n * (1.0 + 1.0 / 8.0)
     return b
@@ -165,6 +166,7 @@ def main():
         run.run()
     ctx.time_device(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
     n_pass = run.n_pass() if filt else 0
+    rec_bytes = 16.0 * run.record_slabs() if wl["parse"] else 0.0   # packed records: slabs stored
     # Two more untimed steps right before the timed region: an idle GPU (host-side work
     # between warm-up and t0) was measured to start the first timed kernel up to ~27 ms
     # late in 3 of 8 processes, with the device-side span unchanged.
@@ -194,7 +196,7 @@ def main():
     total_pkts = n * world
     value = total_pkts / step_s / 1e6
 
-    algo = algorithmic_bytes(desc, wl["fixed"], wl["parse"], filt, n_pass)
+    algo = algorithmic_bytes(desc, wl["fixed"], rec_bytes, filt)
     if args.payload is not None:
         algo += payload_extra_bytes(data, desc)
     achieved = algo / (main_ms * 1e-3) / 1e9
@@ -234,6 +236,7 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": "bt_parse_filter_main", "kernel_ms": round(main_ms, 4),
                          "algorithmic_bytes_per_packet": round(algo / n, 2),
+                         "record_bytes_per_packet": round(rec_bytes / n, 2),
                          "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),
                          "gpu_span_ms_per_step": round(ms_iter, 4)},
             "cpu_baseline": cpu,

@@ -52,19 +52,34 @@ def test_compile_rejects_more_than_64_enabled_filters():
     assert len(abi.compile_host(fs)) == 64
 
 
-def test_record_gather_matches_untile():
-    """bt_record_gather (C) and abi.untile_records (numpy) agree on the tiled layout."""
+def test_packed_records_round_trip():
+    """The packed device record (include/beatrice_gpu.h): the numpy restatement of the
+    kernel's pack_record, placed in the tiled and plane-major layouts with random bytes
+    in the slabs a record does not store, unpacks (bt_record_gather / _planes /
+    bt_record_unpack) to the reference's bt_rec on every golden capture."""
     import numpy as np
-    n = 200
-    nt = (n + 63) // 64
-    buf = (np.arange(nt * 6144, dtype=np.uint32) * 2654435761 >> 13).astype(np.uint8)
-    aos = abi.untile_records(buf, n)
-    out = np.zeros(96, np.uint8)
-    for i in (0, 1, 63, 64, 130, 199):
-        abi.lib().bt_record_gather(buf.ctypes.data, n, i, out.ctypes.data)
-        assert np.array_equal(out, aos[i])
-    planes = buf[: 6 * n * 16]
-    aos_p = abi.untile_records(planes, n, planes=True)
-    for i in (0, 77, 199):
-        abi.lib().bt_record_gather_planes(planes.ctypes.data, n, i, out.ctypes.data)
-        assert np.array_equal(out, aos_p[i])
+    from conftest import load_golden
+    for cap in ("edge", "fuzz", "c3", "c4", "http"):
+        g, _ = load_golden(cap)
+        rec = g["rec"]
+        n = len(rec)
+        c = abi.pack_records(rec)
+        ns = abi.record_slabs(rec)
+        assert ns.min() >= 2 and ns.max() <= 6
+        # every dword past a record's stored slabs is zero (nothing is lost by not storing it)
+        assert not np.any(c[np.arange(24)[None, :] >= 4 * ns[:, None]])
+        assert all(abi.lib().bt_record_slabs(rec[i].ctypes.data) == ns[i] for i in range(0, n, 97))
+        tiled = abi.tile_packed(c, ns)
+        assert np.array_equal(abi.untile_records(tiled, n), rec), cap
+        planes = abi.tile_packed(c, ns, planes=True)
+        assert np.array_equal(abi.untile_records(planes, n, planes=True), rec), cap
+        out = np.zeros(96, np.uint8)
+        for i in (0, 1, 63, 64, n - 1):
+            abi.lib().bt_record_gather(tiled.ctypes.data, n, i, out.ctypes.data)
+            assert np.array_equal(out, rec[i])
+            abi.lib().bt_record_gather_planes(planes.ctypes.data, n, i, out.ctypes.data)
+            assert np.array_equal(out, rec[i])
+        tot = abi.ctypes.c_uint64(0)
+        buf = np.zeros_like(rec)
+        assert abi.lib().bt_record_unpack(None, tiled.ctypes.data, n, n, 0, buf.ctypes.data, abi.ctypes.byref(tot)) == 0
+        assert tot.value == int(ns.sum()) and np.array_equal(buf, rec)

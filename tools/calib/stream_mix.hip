@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void k_write(uint4* __restrict__ out, size_t n
     }
 }
 
-template <bool NT>
+template <bool NT, int SLABS = 6>
 __global__ __launch_bounds__(256) void k_mix(const uint4* __restrict__ in, uint4* __restrict__ rec, uint32_t ntiles) {
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint32_t W = gridDim.x * 4u;
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void k_mix(const uint4* __restrict__ in, uint4
         for (int j = 0; j < 4; ++j) v[j] = src[j * 64 + lane];
         uint4* dst = rec + (size_t)t * 384;        // 6 KiB
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < SLABS; ++k) {
             const uint4 a = v[k & 3];
             const u32x4 x = {a.x ^ (uint32_t)k, a.y, a.z, a.w};
             if (NT) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst + k * 64 + lane));
@@ -111,6 +111,8 @@ int main() {
         snprintf(nm, sizeof nm, "mix def %2d blocks/CU", per_cu);
         timeit(nm, 160.0 * n, [&] { hipLaunchKernelGGL(k_mix<false>, dim3(cus * per_cu), dim3(256), 0, 0, in, rec, ntiles); });
     }
+    timeit("mix nt 4 slabs (64 B rec)", 128.0 * n, [&] { hipLaunchKernelGGL((k_mix<true, 4>), dim3(cus * 4), dim3(256), 0, 0, in, rec, ntiles); });
+    timeit("mix nt 5 slabs (80 B rec)", 144.0 * n, [&] { hipLaunchKernelGGL((k_mix<true, 5>), dim3(cus * 4), dim3(256), 0, 0, in, rec, ntiles); });
     timeit("mix nt  1 tile/wave", 160.0 * n, [&] { hipLaunchKernelGGL(k_mix<true>, dim3(ntiles / 4), dim3(256), 0, 0, in, rec, ntiles); });
     return 0;
 }
