@@ -21,6 +21,8 @@
 // src/PacketFilter.cpp:57-372 (see DESIGN.md for the line-by-line mapping).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "bt_device.h"
 
 namespace bt {
@@ -713,6 +715,17 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
     }
 }
 
+int cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                  ? prop.multiProcessorCount : 256;
+    }
+    return cus;
+}
+
 // One residency wave of blocks: the persistent grid-stride loop then has no tail of
 // late blocks (measured: 2x residency cost C3 11 %).
 template <class K>
@@ -745,6 +758,10 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
     auto go = [&](auto kernel) {
         const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
         int g = grid > 0 ? grid : resident_grid(kernel, dyn);
+        // Fixed stride: two blocks (8 waves) per CU. C2 measured 0.416 ms at the
+        // residency (7 blocks/CU), 0.403 at 3, 0.387 at 2, 0.56 at 1 (4 processes each):
+        // fewer concurrent read and write streams suit HBM better here.
+        if (FL >= 0 && grid <= 0) g = std::min(g, 2 * cu_count());
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
         hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
     };
