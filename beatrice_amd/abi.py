@@ -403,29 +403,42 @@ def untile_records(buf: np.ndarray, n: int, planes: bool = False, ctx: "Context 
 def record_slabs(rec: np.ndarray) -> np.ndarray:
     """Slabs the packed device form of each bt_rec occupies (bt_record_slabs)."""
     ok = np.ascontiguousarray(rec).view(np.uint8).reshape(-1, BT_REC_BYTES)[:, 25].astype(np.int64)
-    nd = 8 + np.where(ok & L_IPV4, 5, np.where(ok & L_IPV6, 10, 0)) + \
+    nd = 5 + ((ok & L_VLAN0) != 0) + ((ok & L_VLAN1) != 0) + \
+        np.where(ok & L_IPV4, 5, np.where(ok & L_IPV6, 10, 0)) + \
         np.where(ok & L_TCP, 5, np.where(ok & (L_UDP | L_ICMP), 2, 0))
     return (nd + 3) // 4
 
 
 def pack_records(rec: np.ndarray) -> np.ndarray:
-    """numpy restatement of the kernel's pack_record (test helper): bt_rec[n] -> [n, 24]
-    packed dwords, zero past each record's stored slabs."""
+    """numpy restatement of the kernel's packed record (parse_packet<true>; test helper):
+    bt_rec[n] -> [n, 24] packed dwords, zero past each record's stored slabs."""
     r = np.ascontiguousarray(rec).view(np.uint8).reshape(-1, BT_REC_BYTES).view("<u4").astype(np.uint64)
     n = len(r)
-    ok = (r[:, 6] >> 8) & 0xFF
+    present, ok = r[:, 6] & 0xFF, (r[:, 6] >> 8) & 0xFF
+    det = r[:, 22]
     ok4, ok6 = (ok & L_IPV4) != 0, (ok & L_IPV6) != 0
     c = np.zeros((n, 24), np.uint64)
     c[:, 0:4] = r[:, 0:4]
-    c[:, 4] = r[:, 6]
-    c[:, 5] = (r[:, 5] & 0xFFFF) | (r[:, 4] & 0xFFFF0000)
-    c[:, 6] = (r[:, 5] >> 16) | ((r[:, 22] << 16) & 0xFFFF0000)
-    c[:, 7] = (r[:, 22] >> 16) & 0xFF
+    c[:, 4] = present | (ok << 8) | ((det & 7) << 16) | (((det >> 8) & 0xFF) << 19) | (((det >> 16) & 7) << 27)
+    ne = ((ok & L_VLAN0) != 0).astype(np.int64) + ((ok & L_VLAN1) != 0)
+    x0 = (r[:, 5] & 0xFFFF) | (r[:, 4] & 0xFFFF0000)
+    x1 = r[:, 5] >> 16
     v4 = np.stack([(r[:, 7] & 0xFF) | ((r[:, 7] >> 8) & 0xFF00) | ((r[:, 7] >> 8) & 0xFF0000) | ((r[:, 8] & 0xFF) << 24),
                    (r[:, 8] >> 16) | ((r[:, 9] & 0xFFFF) << 16), (r[:, 9] >> 16) | ((r[:, 10] & 0xFFFF) << 16),
-                   r[:, 11], r[:, 12], r[:, 17], r[:, 18], r[:, 19], r[:, 20], r[:, 21]], axis=1)
-    c[:, 8:18] = np.where(ok4[:, None], v4, np.where(ok6[:, None], r[:, 7:17], 0))
-    c[:, 18:23] = np.where(ok6[:, None], r[:, 17:22], 0)
+                   r[:, 11], r[:, 12]], axis=1)
+    l4 = r[:, 17:22]
+    L = np.zeros((n, 15), np.uint64)
+    L[ok4, 0:5] = v4[ok4]
+    L[ok4, 5:10] = l4[ok4]
+    L[ok6, 0:10] = r[ok6, 7:17]
+    L[ok6, 10:15] = l4[ok6]
+    for e in (0, 1, 2):
+        m = ne == e
+        if e >= 1:
+            c[m, 5] = x0[m]
+        if e == 2:
+            c[m, 6] = x1[m]
+        c[m, 5 + e:20 + e] = L[m]
     return c.astype(np.uint32)
 
 

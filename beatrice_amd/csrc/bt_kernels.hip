@@ -114,8 +114,8 @@ __device__ __forceinline__ uint32_t detect_word(const uint32_t* w0, uint32_t len
 // big-endian decode, all-or-nothing per layer (ProtocolParser.cpp:244-247).
 // PACKED = false: p.r is the 96-B bt_rec (host AoS path); returns 6.
 // PACKED = true:  p.r is the packed device record (include/beatrice_gpu.h): the fields
-// of the layers that parsed, L4 right after L3, so an Eth/IPv4/UDP packet fills 4
-// slabs instead of 6; returns the slab count (2..6). Dwords past it are 0, because
+// of the layers that parsed, each right after the previous, so an Eth/IPv4/UDP packet
+// fills 3 slabs instead of 6; returns the slab count (2..6). Dwords past it are 0, because
 // every field of a layer that did not parse is 0. Both forms come from the same
 // branch-free selects, so the packed form costs no registers beyond bt_rec's.
 template <bool PACKED>
@@ -205,19 +205,30 @@ __device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s
         p.r[22] = det;
         return BT_REC_SLABS;
     } else {
-        p.r[4] = meta;
-        p.r[5] = tc0 | (tp1 << 16);   // tpid0 is the ethertype
-        p.r[6] = tc1 | (det << 16);
-        p.r[7] = (det >> 16) & 0xFFu;
-        // IPv4 without bt_rec's pads and its duplicate version byte: 5 dwords
+        // present | ok | detector (3 + 8 + 3 bits); l3_off / l4_off follow from present
+        // and the IPv4 IHL, so they are not stored
+        p.r[4] = present | (okbits << 8) | ((det & 7u) << 16) | (((det >> 8) & 0xFFu) << 19) |
+                 (((det >> 16) & 7u) << 27);
+        // VLAN extension, one dword per tag that parsed (tpid0 is the ethertype)
+        const uint32_t ne = (v0ok ? 1u : 0u) + (v1ok ? 1u : 0u);
+        const uint32_t x0 = tc0 | (tp1 << 16), x1 = tc1;
+        // L3 then L4: IPv4 without bt_rec's pads and its duplicate version byte (5 dwords)
+        // or IPv6 (10), then TCP (5) or UDP / ICMP (2)
         const uint32_t v4[5] = {b0 | (byte_of(w3, 1) << 8) | (byte_of(w3, 8) << 16) | (proto << 24),
                                 be16_of(w3, 2) | (be16_of(w3, 4) << 16), be16_of(w3, 6) | (be16_of(w3, 10) << 16),
                                 w3[3], w3[4]};
+        uint32_t L[15];
 #pragma unroll
-        for (int j = 0; j < 10; ++j) p.r[8 + j] = v4ok ? (j < 5 ? v4[j] : l4v[j - 5]) : (v6ok ? v6[j] : 0u);
+        for (int j = 0; j < 15; ++j)
+            L[j] = v4ok ? (j < 5 ? v4[j] : j < 10 ? l4v[j - 5] : 0u) : v6ok ? (j < 10 ? v6[j] : l4v[j - 10]) : 0u;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) p.r[18 + j] = v6ok ? l4v[j] : 0u;
-        const uint32_t nd = 8u + (v4ok ? 5u : v6ok ? 10u : 0u) + (tcp_ok ? 5u : (udp_ok || icmp_ok) ? 2u : 0u);
+        for (int j = 0; j < 19; ++j) {
+            const uint32_t e0 = j < 15 ? L[j] : 0u;
+            const uint32_t e1 = j == 0 ? x0 : (j - 1 < 15 ? L[j - 1] : 0u);
+            const uint32_t e2 = j == 0 ? x0 : j == 1 ? x1 : (j - 2 < 15 ? L[j - 2] : 0u);
+            p.r[5 + j] = ne == 0u ? e0 : ne == 1u ? e1 : e2;
+        }
+        const uint32_t nd = 5u + ne + (v4ok ? 5u : v6ok ? 10u : 0u) + (tcp_ok ? 5u : (udp_ok || icmp_ok) ? 2u : 0u);
         return (nd + 3u) >> 2;
     }
 }

@@ -758,33 +758,42 @@ void unpack_record(Slab slab, bt_rec* out) {
     uint32_t c[24] = {};
     std::memcpy(c, slab(0), 16);
     std::memcpy(c + 4, slab(1), 16);
-    const uint32_t ok = (c[4] >> 8) & 0xFFu;
+    const uint32_t present = c[4] & 0xFFu, ok = (c[4] >> 8) & 0xFFu;
+    const uint32_t ne = ((ok & BT_L_VLAN0) ? 1u : 0u) + ((ok & BT_L_VLAN1) ? 1u : 0u);
     const bool ok4 = ok & BT_L_IPV4, ok6 = ok & BT_L_IPV6;
     const uint32_t l4d = (ok & BT_L_TCP) ? 5u : (ok & (BT_L_UDP | BT_L_ICMP)) ? 2u : 0u;
-    const uint32_t nd = 8u + (ok4 ? 5u : ok6 ? 10u : 0u) + l4d;
+    const uint32_t nd = 5u + ne + (ok4 ? 5u : ok6 ? 10u : 0u) + l4d;
     for (uint32_t k = 2; 4 * k < nd; ++k) std::memcpy(c + 4 * k, slab(k), 16);
+    const uint32_t x0 = ne >= 1 ? c[5] : 0u, x1 = ne >= 2 ? c[6] : 0u;
+    const uint32_t* L = c + 5 + ne;
     uint32_t r[24] = {};
     r[0] = c[0]; r[1] = c[1]; r[2] = c[2]; r[3] = c[3];
-    r[4] = ((ok & BT_L_VLAN0) ? (c[3] & 0xFFFFu) : 0u) | (c[5] & 0xFFFF0000u);   // tpid0 == ethertype
-    r[5] = (c[5] & 0xFFFFu) | (c[6] << 16);
-    r[6] = c[4];
+    r[4] = ((ok & BT_L_VLAN0) ? (c[3] & 0xFFFFu) : 0u) | (x0 & 0xFFFF0000u);   // tpid0 == ethertype
+    r[5] = (x0 & 0xFFFFu) | (x1 << 16);
+    // the walk's offsets (R-WALK): L3 after the tags the walk attempted; L4 after the
+    // IPv4 header (IHL) or the fixed 40-B IPv6 header
+    const uint32_t o3 = 14u + ((present & BT_L_VLAN0) ? 4u : 0u) + ((present & BT_L_VLAN1) ? 4u : 0u);
+    uint32_t l3_off = (present & (BT_L_IPV4 | BT_L_IPV6)) ? o3 : 0u, l4_off = 0;
     const uint32_t* l4 = nullptr;
     if (ok4) {
-        const uint32_t b0 = c[8] & 0xFFu, tos = (c[8] >> 8) & 0xFFu, ttl = (c[8] >> 16) & 0xFFu, proto = c[8] >> 24;
+        const uint32_t b0 = L[0] & 0xFFu, tos = (L[0] >> 8) & 0xFFu, ttl = (L[0] >> 16) & 0xFFu, proto = L[0] >> 24;
         r[7] = b0 | (b0 << 8) | (tos << 16) | (ttl << 24);
-        r[8] = proto | (c[9] << 16);
-        r[9] = (c[9] >> 16) | (c[10] << 16);
-        r[10] = c[10] >> 16;
-        r[11] = c[11];
-        r[12] = c[12];
-        l4 = c + 13;
+        r[8] = proto | (L[1] << 16);
+        r[9] = (L[1] >> 16) | (L[2] << 16);
+        r[10] = L[2] >> 16;
+        r[11] = L[3];
+        r[12] = L[4];
+        l4 = L + 5;
+        if (present & (BT_L_TCP | BT_L_UDP | BT_L_ICMP)) l4_off = o3 + 4u * (b0 & 0x0Fu);
     } else if (ok6) {
-        for (int j = 0; j < 10; ++j) r[7 + j] = c[8 + j];
-        l4 = c + 18;
+        for (int j = 0; j < 10; ++j) r[7 + j] = L[j];
+        l4 = L + 10;
+        if (present & (BT_L_TCP | BT_L_UDP)) l4_off = o3 + 40u;
     }
+    r[6] = present | (ok << 8) | (l3_off << 16) | (l4_off << 24);
     if (l4)
         for (uint32_t j = 0; j < l4d; ++j) r[17 + j] = l4[j];
-    r[22] = (c[6] >> 16) | ((c[7] & 0xFFu) << 16);
+    r[22] = ((c[4] >> 16) & 7u) | (((c[4] >> 19) & 0xFFu) << 8) | (((c[4] >> 27) & 7u) << 16);
     std::memcpy(out, r, sizeof(r));
 }
 
@@ -832,7 +841,8 @@ int bt_record_unpack(bt_ctx* ctx, const void* records, uint32_t n_cap, uint32_t 
 
 uint32_t bt_record_slabs(const bt_rec* r) {
     const uint32_t ok = r->ok;
-    const uint32_t nd = 8u + ((ok & BT_L_IPV4) ? 5u : (ok & BT_L_IPV6) ? 10u : 0u) +
+    const uint32_t nd = 5u + ((ok & BT_L_VLAN0) ? 1u : 0u) + ((ok & BT_L_VLAN1) ? 1u : 0u) +
+                        ((ok & BT_L_IPV4) ? 5u : (ok & BT_L_IPV6) ? 10u : 0u) +
                         ((ok & BT_L_TCP) ? 5u : (ok & (BT_L_UDP | BT_L_ICMP)) ? 2u : 0u);
     return (nd + 3u) >> 2;
 }

@@ -41,21 +41,21 @@
  * so each wavefront store instruction writes 1 KiB contiguously. The buffer needs
  * ceil(n / 64) * 6144 bytes. BT_OPT_RECORDS_PLANES selects plane-major slabs instead:
  * (k * n_cap + i) * 16. A packed record holds only the fields of the layers that
- * parsed (bt_rec.ok), L4 right after L3, as 24 little-endian dwords c[0..23]:
+ * parsed (bt_rec.ok), each right after the previous one, as 24 little-endian dwords c[]:
  *   c0..c3  = bt_rec bytes 0..15 (Ethernet, pkt_len)
- *   c4      = present | ok << 8 | l3_off << 16 | l4_off << 24
- *   c5      = vlan_tci[0] | vlan_tpid[1] << 16   (vlan_tpid[0] is the ethertype)
- *   c6      = vlan_tci[1] | detect_code << 16 | detect_is << 24
- *   c7      = detect_is2
- *   IPv4 at c8: b0 | tos << 8 | ttl << 16 | protocol << 24, total_length | id << 16,
- *               flags | checksum << 16, source_ip, destination_ip (version == ihl == b0)
- *   IPv6 at c8: bt_rec bytes 28..67 as they are
- *   L4 after L3 (c13 / c18): TCP 5 dwords, UDP / ICMP 2 dwords, as bt_rec bytes 68..
- * Only its first BT_REC_PACKED_SLABS(ok) = ceil(dwords / 4) slabs are written (Eth/IPv4/
- * UDP: 4, IPv4/TCP or IPv6/UDP: 5, IPv6/TCP: 6, no IP: 2); the rest of the 96 B are left
- * as they were. bt_record_gather() / bt_record_unpack() rebuild the bt_rec, which is the
- * parity unit. (Measured with tools/calib/stream_mix.hip: the C2 byte mix moves in
- * 0.40 ms with 64-B records against 0.48 ms with 96-B ones.)
+ *   c4      = present | ok << 8 | detect_code << 16 (3 bits) | detect_is << 19 (8 bits)
+ *             | detect_is2 << 27 (3 bits); l3_off / l4_off are implied by present (+ IHL)
+ *   then, per VLAN tag that parsed: vlan_tci[0] | vlan_tpid[1] << 16, then vlan_tci[1]
+ *             (vlan_tpid[0] is the ethertype)
+ *   then L3: IPv4 b0 | tos << 8 | ttl << 16 | protocol << 24, total_length | id << 16,
+ *            flags | checksum << 16, source_ip, destination_ip (version == ihl == b0);
+ *            or IPv6 as bt_rec bytes 28..67
+ *   then L4: TCP 5 dwords / UDP, ICMP 2 dwords, as bt_rec bytes 68..
+ * A record needs ceil(dwords / 4) slabs (bt_record_slabs): untagged Eth/IPv4/UDP 3,
+ * IPv4/TCP or one tag 4, IPv6/TCP + QinQ 6, no IP 2. Slab k of a tile is written by the
+ * whole wavefront when any of its packets needs it (zeros for the others); slabs none
+ * needs are left as they were. bt_record_gather() / bt_record_unpack() rebuild the
+ * bt_rec, which is the parity unit.
  */
 #ifndef BEATRICE_GPU_H
 #define BEATRICE_GPU_H
