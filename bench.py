@@ -149,7 +149,9 @@ def main():
     data, desc = synth.capture(wl["cfg"], n, seed=synth.SEEDS[wl["cfg"]] + rank)
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
     flags |= abi.OPT_SPIN_SYNC   # the timed region's end is not delayed by a sleeping host thread
-    ctx = abi.Context(local, grid_waves=args.grid_waves, flags=flags)
+    # BT_BENCH_DEVICE: put every rank on one device (multi-rank rehearsal on a 1-GPU box)
+    device = int(os.environ.get("BT_BENCH_DEVICE", local))
+    ctx = abi.Context(device, grid_waves=args.grid_waves, flags=flags)
     if args.payload is not None:
         if not wl["filters"]:
             sys.exit("--payload needs a filtering workload (c3 / c4)")
