@@ -99,7 +99,8 @@ EXPORTS = [
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
-    "bt_payload_dfa_compile", "bt_payload_dfa_search", "bt_payload_dfa_eval", "bt_format_records",
+    "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
+    "bt_format_records",
     "bt_record_unpack", "bt_record_slabs",
 ]
 

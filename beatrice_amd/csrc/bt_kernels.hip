@@ -305,7 +305,40 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
     const uint8_t* cls = endacc + ((K + 3u) & ~3u);
     const uint8_t* next = C == 256u ? cls : cls + 256;
     const uint32_t dw = staged_sh >> 2, sh8 = (staged_sh & 3u) * 8u;
-    for (uint32_t i = 0; i < L; i += 4u) {
+    uint32_t i = 0;
+    if (blob[6]) {
+        // Two-byte table: the classes of four bytes are independent of q and issued
+        // first, then two dependent reads cover them (half the chain of one per byte).
+        const uint32_t P = blob[7];
+        const uint8_t* clsp = blob + ((((uint32_t)(next - blob) + K * C) + 3u) & ~3u);
+        const uint8_t* pair = clsp + 256;
+        for (; i + 4u <= L; i += 4u) {
+            const uint32_t lo = row[dw + (i >> 2)], hi = row[dw + (i >> 2) + 1u];
+            const uint32_t w = sh8 ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh8) : lo;
+            const uint32_t c0 = clsp[w & 0xFFu], c1 = clsp[(w >> 8) & 0xFFu];
+            const uint32_t c2 = clsp[(w >> 16) & 0xFFu], c3 = clsp[w >> 24];
+            q = pair[(q * P + c0) * P + c1];
+            if (q >= K) return q == K ? 1u : 0u;
+            q = pair[(q * P + c2) * P + c3];
+            if (q >= K) return q == K ? 1u : 0u;
+        }
+        // the last 1..3 bytes: one more pair if two remain, then the one-byte table
+        if (i + 2u <= L) {
+            const uint32_t lo = row[dw + (i >> 2)], hi = row[dw + (i >> 2) + 1u];
+            const uint32_t w = sh8 ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh8) : lo;
+            q = pair[(q * P + clsp[w & 0xFFu]) * P + clsp[(w >> 8) & 0xFFu]];
+            if (q >= K) return q == K ? 1u : 0u;
+            i += 2u;
+        }
+        if (i < L) {   // one byte left: payload byte i sits at row byte staged_sh + i
+            const uint32_t at = staged_sh + i;
+            const uint32_t b = (row[at >> 2] >> (8u * (at & 3u))) & 0xFFu;
+            q = next[q * C + (C == 256u ? b : (uint32_t)cls[b])];
+            if (q >= K) return q == K ? 1u : 0u;
+        }
+        return endacc[q];
+    }
+    for (; i < L; i += 4u) {
         // four payload bytes from two aligned row dwords (independent of q: issued early)
         const uint32_t lo = row[dw + (i >> 2)], hi = row[dw + (i >> 2) + 1u];
         const uint32_t w = sh8 ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh8) : lo;

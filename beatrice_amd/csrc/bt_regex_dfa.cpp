@@ -30,10 +30,13 @@
 //   u16 K, u16 C          C = 256: `next` is indexed by the byte itself (one dependent
 //                         LDS read per byte); otherwise C byte classes via cls[]
 //   u8  init, u8 empty    init state (may be a sink); empty = match on the empty input
-//   u16 pad
+//   u8  pairs, u8 P       pairs = 1: a two-byte table follows (P byte classes)
 //   u8  endacc[K] (pad 4) 1 = a match completes if the input ends in this state
 //   u8  cls[256]          only when C != 256
-//   u8  next[K * C]
+//   u8  next[K * C]       (pad 4)
+//   u8  clsp[256]         pairs only: byte -> class of the two-byte table
+//   u8  pair[K * P * P]   pairs only: the state after two bytes (a sink after the first
+//                         stays), so the walk's dependent chain is half as long
 #include <algorithm>
 #include <bitset>
 #include <cstring>
@@ -559,13 +562,15 @@ Dfa build_dfa(const std::string& pattern) {
 
 // Live states, sinks and table shape of the serialized DFA.
 struct Packed {
-    int K = 0, C = 0, init = 0, empty = 0;
-    std::vector<uint8_t> endacc, cls, next;
+    int K = 0, C = 0, init = 0, empty = 0, P = 0;
+    std::vector<uint8_t> endacc, cls, next, clsp, pair;
 };
+
+constexpr int kPairTableMax = 4096;       // K * P * P bytes: the two-byte table is optional
 
 constexpr int kByteTableMaxStates = 32;   // K * 256 <= 8 KiB: index by the byte, skip cls[]
 
-Packed pack(const Dfa& d) {
+Packed pack(const Dfa& d, bool pairs) {
     const int S = (int)d.acc.size();
     // live = neither "match complete" (absorbing true) nor "no match possible"
     std::vector<int> id(S, -1);
@@ -592,11 +597,29 @@ Packed pack(const Dfa& d) {
             p.next[(size_t)id[q] * p.C + c] = (uint8_t)map(d.next[(size_t)q * d.n_classes + cl]);
         }
     }
+    const int P = d.n_classes;
+    if (pairs && K > 0 && (size_t)K * P * P <= (size_t)kPairTableMax) {
+        p.P = P;
+        p.clsp.assign(d.cls, d.cls + 256);
+        p.pair.assign((size_t)K * P * P, 0);
+        for (int q = 0; q < S; ++q) {
+            if (id[q] < 0) continue;
+            for (int c0 = 0; c0 < P; ++c0) {
+                const int t = d.next[(size_t)q * P + c0];
+                for (int c1 = 0; c1 < P; ++c1) {
+                    const int to = map(t) >= K ? map(t) : map(d.next[(size_t)t * P + c1]);
+                    p.pair[((size_t)id[q] * P + c0) * P + c1] = (uint8_t)to;
+                }
+            }
+        }
+    }
     return p;
 }
 
 uint32_t blob_size(const Packed& p) {
-    return 8 + ((p.K + 3) & ~3) + (p.C == 256 ? 0 : 256) + (uint32_t)p.K * p.C;
+    uint32_t n = 8 + ((p.K + 3) & ~3) + (p.C == 256 ? 0 : 256) + (uint32_t)p.K * p.C;
+    if (p.P) n = ((n + 3) & ~3u) + 256 + (uint32_t)p.K * p.P * p.P;
+    return n;
 }
 
 }  // namespace
@@ -604,6 +627,10 @@ uint32_t blob_size(const Packed& p) {
 extern "C" {
 
 int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size) {
+    return bt_payload_dfa_compile_ex(expression, 0, blob, cap, size);
+}
+
+int bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob, uint32_t cap, uint32_t* size) {
     if (!expression || !size) return BT_E_INVALID_ARGUMENT;
     const std::string e(expression);
     try {
@@ -613,7 +640,7 @@ int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uin
     }
     Packed pk;
     try {
-        pk = pack(build_dfa(e));
+        pk = pack(build_dfa(e), !(flags & BT_DFA_NO_PAIRS));
     } catch (const Unsupported&) {
         return BT_E_NOT_IMPLEMENTED;
     }
@@ -627,6 +654,8 @@ int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uin
     std::memcpy(p + 2, &c16, 2);
     p[4] = (uint8_t)pk.init;
     p[5] = (uint8_t)pk.empty;
+    p[6] = pk.P ? 1 : 0;
+    p[7] = (uint8_t)pk.P;
     uint8_t* q = p + 8;
     if (pk.K) std::memcpy(q, pk.endacc.data(), pk.K);
     q += (pk.K + 3) & ~3;
@@ -635,6 +664,12 @@ int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uin
         q += 256;
     }
     if (!pk.next.empty()) std::memcpy(q, pk.next.data(), pk.next.size());
+    q += pk.next.size();
+    if (pk.P) {
+        q = p + (((size_t)(q - p) + 3) & ~(size_t)3);
+        std::memcpy(q, pk.clsp.data(), 256);
+        std::memcpy(q + 256, pk.pair.data(), pk.pair.size());
+    }
     return BT_OK;
 }
 
@@ -649,7 +684,18 @@ int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n) {
     uint32_t q = p[4];
     if (n == 0) return p[5];
     if (q >= K) return q == K;
-    for (uint32_t i = 0; i < n; ++i) {
+    uint32_t i = 0;
+    if (p[6]) {   // two bytes per dependent step, as the kernel walks it
+        const uint32_t P = p[7];
+        const size_t at = ((size_t)(next + (size_t)K * C - p) + 3) & ~(size_t)3;
+        const uint8_t* clsp = p + at;
+        const uint8_t* pair = clsp + 256;
+        for (; i + 2 <= n; i += 2) {
+            q = pair[(q * P + clsp[s[i]]) * P + clsp[s[i + 1]]];
+            if (q >= K) return q == K;
+        }
+    }
+    for (; i < n; ++i) {
         q = next[q * C + (C == 256 ? s[i] : cls[s[i]])];
         if (q >= K) return q == K;
     }

@@ -411,12 +411,16 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
         for (auto& s : slots) {
             const bt_filter_desc& d = f[s.source_index];
             if (s.kind != BT_K_HOST || d.type != BT_FILTER_PAYLOAD || !d.expression) continue;
-            uint32_t size = 0;
-            if (bt_payload_dfa_compile(d.expression, nullptr, 0, &size) != BT_OK) continue;
+            uint32_t size = 0, fl = 0;
+            if (bt_payload_dfa_compile_ex(d.expression, fl, nullptr, 0, &size) != BT_OK) continue;
             const size_t at = (pool.size() + 15) & ~(size_t)15;
-            if (at + size > kDfaPoolMax) continue;
+            if (at + size > kDfaPoolMax) {   // retry without the optional two-byte table
+                fl = BT_DFA_NO_PAIRS;
+                if (bt_payload_dfa_compile_ex(d.expression, fl, nullptr, 0, &size) != BT_OK || at + size > kDfaPoolMax)
+                    continue;
+            }
             pool.resize(at + size);
-            if (bt_payload_dfa_compile(d.expression, pool.data() + at, size, &size) != BT_OK) {
+            if (bt_payload_dfa_compile_ex(d.expression, fl, pool.data() + at, size, &size) != BT_OK) {
                 pool.resize(at);
                 continue;
             }

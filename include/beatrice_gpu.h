@@ -372,6 +372,11 @@ int  bt_host_unregister(bt_ctx* ctx, void* host);
  *   bt_payload_dfa_search   regex_search(string(s, n), regex(expr)) for a compiled expr
  *   bt_payload_dfa_eval     applyPayloadFilter(frame, len) for a non-empty expression */
 int  bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size);
+/* The same with options: BT_DFA_NO_PAIRS leaves out the optional two-byte table (the
+ * compiler adds it when it is <= 4 KiB; the filter compiler drops it when a program's
+ * tables would not fit the 16 KiB pool otherwise). */
+#define BT_DFA_NO_PAIRS 0x1u
+int  bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob, uint32_t cap, uint32_t* size);
 int  bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);
 int  bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len);
 
