@@ -451,12 +451,22 @@ def tile_packed(c: np.ndarray, nslab: np.ndarray, planes: bool = False, seed: in
     rng = np.random.default_rng(seed)
     slabs = c.reshape(n, 6, 16 // 4).view(np.uint8).reshape(n, 6, 16).copy()
     keep = np.arange(6)[None, :] < nslab[:, None]
-    slabs[~keep] = rng.integers(0, 256, size=(int((~keep).sum()), 16), dtype=np.uint8)
-    if planes:
+    if planes:   # whole-wave slabs, one slot per packet
+        slabs[~keep] = rng.integers(0, 256, size=(int((~keep).sum()), 16), dtype=np.uint8)
         return np.ascontiguousarray(slabs.transpose(1, 0, 2)).reshape(-1)
-    t = np.zeros((nt * 64, 6, 16), np.uint8)
-    t[:n] = slabs
-    return np.ascontiguousarray(t.reshape(nt, 64, 6, 16).transpose(0, 2, 1, 3)).reshape(-1)
+    # tiled: slabs 0..1 at the packet's slot (zeros for a last tile's unused slots), slab
+    # k >= 2 packed in packet order to the front of the tile's slab-k region
+    t = rng.integers(0, 256, size=(nt, 6, 64, 16), dtype=np.uint8)
+    t[:, 0:2] = 0
+    for i in range(n):
+        tt, lane = divmod(i, 64)
+        t[tt, 0:2, lane] = slabs[i, 0:2]
+    for tt in range(nt):
+        idx = np.arange(tt * 64, min(n, tt * 64 + 64))
+        for k in range(2, 6):
+            sel = idx[nslab[idx] > k]
+            t[tt, k, :len(sel)] = slabs[sel, k]
+    return t.reshape(-1)
 
 
 class DeviceRun:

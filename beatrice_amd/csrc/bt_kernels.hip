@@ -623,16 +623,31 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             if (REC == kRecPlanes || REC == kRecTiled) {
                 // packed device record: its first `ns` slabs (2..6) hold every parsed field
                 const uint32_t ns = parse_packet<true>(row, s, len, w0, p);
-                uint4* dst = reinterpret_cast<uint4*>(a.records) +
-                             (REC == kRecTiled ? (uint64_t)t * (BT_REC_SLABS * 64) + lane : (uint64_t)my);
-                const uint64_t kstride = REC == kRecTiled ? 64ull : (uint64_t)a.n_cap;
-                // Slab k is stored by the whole wave when any lane needs it (the other
-                // lanes' dwords there are 0), so every store covers whole 128-B lines.
+                if (REC == kRecTiled) {
+                    // [tile][slab][slot]: slabs 0 and 1 at the lane's slot; slab k >= 2 only
+                    // for the lanes that need it, packed to the front of the tile's slab-k
+                    // region in lane order, so the stores fill whole 128-B lines except the
+                    // last one of each region.
+                    uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
+                    const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-                for (uint32_t k = 0; k < BT_REC_SLABS; ++k)
-                    if (k < 2u || __ballot(k < ns) != 0ull)   // [tile][slab][lane]: 1 KiB per slab and wave
-                        st16(dst + k * kstride, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]),
-                             a.nt & 1u);
+                    for (uint32_t k = 0; k < BT_REC_SLABS; ++k) {
+                        const uint64_t mk = __ballot(k < ns);
+                        if (mk == 0ull) break;   // ns only falls: no lane needs a later slab
+                        if (k < ns)
+                            st16(tile + k * 64 + (k < 2u ? lane : (uint32_t)__popcll(mk & below)),
+                                 make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
+                    }
+                } else {
+                    // plane-major: slab k is stored by the whole wave when any lane needs it
+                    // (the other lanes' dwords there are 0)
+                    uint4* dst = reinterpret_cast<uint4*>(a.records) + (uint64_t)my;
+#pragma unroll
+                    for (uint32_t k = 0; k < BT_REC_SLABS; ++k)
+                        if (k < 2u || __ballot(k < ns) != 0ull)
+                            st16(dst + (uint64_t)k * a.n_cap,
+                                 make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
+                }
             } else {
                 parse_packet<false>(row, s, len, w0, p);
                 uint4* rec = reinterpret_cast<uint4*>(a.records + (uint64_t)my * BT_REC_BYTES);
@@ -640,6 +655,14 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                 for (int k = 0; k < BT_REC_SLABS; ++k)
                     rec[k] = make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]);
             }
+        }
+
+        if (REC == kRecTiled && !live) {
+            // the last tile's unused slots: a zero slab 1 reads as a 2-slab record, so a
+            // reader can rebuild the slab-k packing of the tile without knowing n
+            uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
+            st16(tile + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
+            st16(tile + 64 + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
         }
 
         // ---- 3. FILTER ------------------------------------------------------

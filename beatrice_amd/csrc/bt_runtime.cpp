@@ -805,9 +805,34 @@ void unpack_record(Slab slab, bt_rec* out) {
 
 extern "C" {
 
+// Tiled layout: slab k >= 2 of a record sits at its rank among the tile's records that
+// need slab k. ns[] = the tile's slab counts, read from the full slab-1 region.
+static void tile_slab_counts(const uint8_t* tile, uint32_t* ns) {
+    for (uint32_t j = 0; j < 64; ++j) {
+        uint32_t c4;
+        std::memcpy(&c4, tile + (64 + j) * 16, 4);
+        bt_rec r;
+        r.ok = (uint8_t)(c4 >> 8);
+        ns[j] = bt_record_slabs(&r);
+    }
+}
+
+static void gather_tiled(const uint8_t* tile, const uint32_t* ns, uint32_t lane, bt_rec* out) {
+    unpack_record([&](uint32_t k) {
+        uint32_t slot = lane;
+        if (k >= 2) {
+            slot = 0;
+            for (uint32_t j = 0; j < lane; ++j) slot += ns[j] > k;
+        }
+        return tile + ((size_t)k * 64 + slot) * 16;
+    }, out);
+}
+
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out) {
-    const uint8_t* p = static_cast<const uint8_t*>(records);
-    unpack_record([&](uint32_t k) { return p + (((size_t)(i / 64) * BT_REC_SLABS + k) * 64 + (i % 64)) * 16; }, out);
+    const uint8_t* tile = static_cast<const uint8_t*>(records) + (size_t)(i / 64) * BT_REC_SLABS * 64 * 16;
+    uint32_t ns[64];
+    tile_slab_counts(tile, ns);
+    gather_tiled(tile, ns, i % 64, out);
     (void)n_cap;
 }
 
@@ -825,10 +850,17 @@ int bt_record_unpack(bt_ctx* ctx, const void* records, uint32_t n_cap, uint32_t 
         const uint32_t lo = (uint32_t)((uint64_t)n * w / T), hi = (uint32_t)((uint64_t)n * (w + 1) / T);
         uint64_t cnt = 0;
         bt_rec r;
+        uint32_t ns[64];
+        uint32_t ns_tile = ~0u;
         for (uint32_t i = lo; i < hi; ++i) {
             if (out) {
-                if (planes) bt_record_gather_planes(records, n_cap, i, out + i);
-                else bt_record_gather(records, n_cap, i, out + i);
+                if (planes) {
+                    bt_record_gather_planes(records, n_cap, i, out + i);
+                } else {
+                    const uint8_t* tile = p + (size_t)(i / 64) * BT_REC_SLABS * 64 * 16;
+                    if (ns_tile != i / 64) { tile_slab_counts(tile, ns); ns_tile = i / 64; }
+                    gather_tiled(tile, ns, i % 64, out + i);
+                }
                 if (slabs) cnt += bt_record_slabs(out + i);
             } else {   // count only: the ok byte sits in slab 1
                 const uint8_t* s1 = planes ? p + ((size_t)n_cap + i) * 16

@@ -52,10 +52,13 @@
  *            or IPv6 as bt_rec bytes 28..67
  *   then L4: TCP 5 dwords / UDP, ICMP 2 dwords, as bt_rec bytes 68..
  * A record needs ceil(dwords / 4) slabs (bt_record_slabs): untagged Eth/IPv4/UDP 3,
- * IPv4/TCP or one tag 4, IPv6/TCP + QinQ 6, no IP 2. Slab k of a tile is written by the
- * whole wavefront when any of its packets needs it (zeros for the others); slabs none
- * needs are left as they were. bt_record_gather() / bt_record_unpack() rebuild the
- * bt_rec, which is the parity unit.
+ * IPv4/TCP or one tag 4, IPv6/TCP + QinQ 6, no IP 2. In the tiled layout, slabs 0 and 1
+ * of packet i are at the addresses above; slab k >= 2 is stored only by the packets that
+ * need it, packed in packet order to the front of the tile's slab-k region (a packet's
+ * slot = its rank among them; the last tile's unused slots hold a zero slab 1). In the
+ * plane-major layout slab k is at the packet's slot, written for the whole wavefront
+ * when any packet needs it. Bytes no packet needs are left as they were.
+ * bt_record_gather() / bt_record_unpack() rebuild the bt_rec, which is the parity unit.
  */
 #ifndef BEATRICE_GPU_H
 #define BEATRICE_GPU_H
