@@ -504,8 +504,11 @@ class DeviceRun:
         out = {}
         self.ctx.synchronize()
         if self.d_rec:
-            out["records"] = untile_records(self.d_rec.download(np.zeros(self.d_rec.nbytes, np.uint8)), n,
-                                            planes=bool(self.ctx.flags & OPT_RECORDS_PLANES))
+            buf = self.d_rec.download(np.zeros(self.d_rec.nbytes, np.uint8))
+            if self.ctx.flags & OPT_RECORDS_AOS:   # bt_rec as is
+                out["records"] = buf[: n * BT_REC_BYTES].reshape(n, BT_REC_BYTES)
+            else:
+                out["records"] = untile_records(buf, n, planes=bool(self.ctx.flags & OPT_RECORDS_PLANES))
         if self.d_dec:
             out["decide"] = self.d_dec.download(np.zeros(n, dtype=np.uint8))
         if self.d_ver:
@@ -524,6 +527,8 @@ class DeviceRun:
             return 6 * self.n
         self.ctx.synchronize()
         buf = self.d_rec.download(np.zeros(self.d_rec.nbytes, np.uint8))
+        if self.ctx.flags & OPT_RECORDS_AOS:   # bt_rec as is: what the packed form would need
+            return int(record_slabs(buf[: self.n * BT_REC_BYTES].reshape(self.n, BT_REC_BYTES)).sum())
         tot = ctypes.c_uint64(0)
         _check(lib().bt_record_unpack(self.ctx.h, buf.ctypes.data, self.n, self.n,
                                       int(bool(self.ctx.flags & OPT_RECORDS_PLANES)), None, ctypes.byref(tot)))

@@ -264,3 +264,24 @@ def test_zero_copy_outputs(gpu_ctx):
     assert np.array_equal(h_dec, dec)
     bits = np.unpackbits(h_ver.view(np.uint8), bitorder="little")[:n].astype(bool)
     assert np.array_equal(bits, (dec >> 6) == 0)
+
+
+@pytest.mark.parametrize("layout", ["tiled", "planes", "aos"])
+@pytest.mark.parametrize("cap", ["c4", "fuzz", "edge"])
+def test_record_layouts(cap, layout):
+    """Every device record layout (packed tiled, packed plane-major, bt_rec AoS) rebuilds
+    the reference's records, with and without a filter program."""
+    flags = {"tiled": 0, "planes": abi.OPT_RECORDS_PLANES, "aos": abi.OPT_RECORDS_AOS}[layout]
+    g, man = load_golden(cap)
+    n = len(g["desc"])
+    ctx = abi.Context(0, flags=flags)
+    try:
+        for filters in ([], man["filter_sets"]["c3"]):
+            ctx.compile(filters)
+            out = run_dev(ctx, g["data"], g["desc"], n, records=True, filt=bool(filters))
+            bad = np.nonzero((out["records"] != g["rec"]).any(axis=1))[0]
+            assert len(bad) == 0, f"{cap}/{layout}: {len(bad)} records differ; first {bad[:5]}"
+            if filters:
+                compare_decisions(out["decide"], g["code__c3"], g["src__c3"], filters, where=f"{cap}/{layout}")
+    finally:
+        ctx.close()
