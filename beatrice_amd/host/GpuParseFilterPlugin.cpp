@@ -29,6 +29,7 @@ namespace gpu {
 class GpuParseFilterPlugin : public IPacketPlugin {
 public:
     void onStart() override {
+        std::lock_guard<std::mutex> g(gpu_mu_);
         std::lock_guard<std::mutex> lk(mu_);
         const int device = env_int("BEATRICE_GPU_DEVICE", 0);
         batch_ = (size_t)env_int("BEATRICE_GPU_BATCH", 65536);
@@ -39,18 +40,30 @@ public:
     }
 
     void onStop() override {
-        std::lock_guard<std::mutex> lk(mu_);
-        flushLocked();
+        flush();
+        std::lock_guard<std::mutex> g(gpu_mu_);
         filter_.reset();
     }
 
+    // onPacket may run on several context threads at once (src/BeatriceContext.cpp:215-278).
+    // A full batch is swapped out under mu_ and classified outside it, so the other
+    // threads keep appending to a fresh batch while the GPU works; gpu_mu_ sends the
+    // batches to the device one at a time.
     void onPacket(Packet& packet) override {
         if (!enabled_) return;
-        std::lock_guard<std::mutex> lk(mu_);   // onPacket may run on several context threads
-        if (pending_.empty()) first_ = std::chrono::steady_clock::now();
-        pending_.push_back(packet);            // shares the immutable bytes, no copy
-        const auto age = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - first_);
-        if (pending_.size() >= batch_ || age.count() >= flush_us_) flushLocked();
+        std::vector<Packet> full;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (pending_.empty()) first_ = std::chrono::steady_clock::now();
+            pending_.push_back(packet);        // shares the immutable bytes, no copy
+            const auto age =
+                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - first_);
+            if (pending_.size() >= batch_ || age.count() >= flush_us_) {
+                full.swap(pending_);
+                pending_.reserve(batch_);
+            }
+        }
+        if (!full.empty()) classifyBatch(full);
     }
 
     std::string getName() const override { return "gpu_parse_filter"; }
@@ -64,13 +77,17 @@ public:
     uint64_t getErrorCount() const override { return errors_; }
     void resetStatistics() override {
         processed_ = passed_ = errors_ = 0;
-        std::lock_guard<std::mutex> lk(mu_);
+        std::lock_guard<std::mutex> g(gpu_mu_);
         if (filter_) filter_->resetStats();
     }
 
     void flush() {
-        std::lock_guard<std::mutex> lk(mu_);
-        flushLocked();
+        std::vector<Packet> full;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            full.swap(pending_);
+        }
+        if (!full.empty()) classifyBatch(full);
     }
     uint64_t passed() const { return passed_; }
     GpuPacketFilter* filter() { return filter_.get(); }
@@ -105,20 +122,21 @@ private:
         }
     }
 
-    void flushLocked() {
-        if (pending_.empty() || !filter_) return;
+    void classifyBatch(const std::vector<Packet>& batch) {
+        std::lock_guard<std::mutex> g(gpu_mu_);
+        if (!filter_) return;
         try {
-            auto v = filter_->classify(pending_);
-            processed_ += pending_.size();
+            auto v = filter_->classify(batch);
+            processed_ += batch.size();
             passed_ += v.pass_idx.size();
         } catch (const std::exception&) {
             // a filter expression the reference would throw on: count the batch as errors
-            errors_ += pending_.size();
+            errors_ += batch.size();
         }
-        pending_.clear();
     }
 
-    std::mutex mu_;
+    std::mutex mu_;        // pending_, first_
+    std::mutex gpu_mu_;    // filter_ (one batch on the device at a time)
     std::unique_ptr<GpuPacketFilter> filter_;
     std::vector<Packet> pending_;
     std::chrono::steady_clock::time_point first_;

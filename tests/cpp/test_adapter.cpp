@@ -20,6 +20,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "beatrice/IPacketPlugin.hpp"
@@ -250,7 +251,15 @@ static bool plugin_case(const Capture& cap, const char* so) {
     CHECK(create && flush && passed, "plugin symbols missing");
     std::unique_ptr<beatrice::IPacketPlugin> p(create());
     p->onStart();
-    for (const auto& pk : cap.packets) p->onPacket(const_cast<Packet&>(pk));
+    // four context threads call onPacket at once (src/BeatriceContext.cpp:215-278)
+    {
+        std::vector<std::thread> th;
+        for (int w = 0; w < 4; ++w)
+            th.emplace_back([&, w] {
+                for (size_t i = w; i < cap.packets.size(); i += 4) p->onPacket(const_cast<Packet&>(cap.packets[i]));
+            });
+        for (auto& x : th) x.join();
+    }
     flush(p.get());
     PacketFilter ref;
     install(ref, {{"proto", PacketFilter::FilterType::PROTOCOL, "udp", 3, true, 0},
@@ -266,7 +275,7 @@ static bool plugin_case(const Capture& cap, const char* so) {
     p->onStop();
     p.reset();
     dlclose(h);
-    std::printf("ok   plugin  createPlugin/onStart/onPacket x%zu/onStop, %lu passed\n", cap.packets.size(),
+    std::printf("ok   plugin  createPlugin/onStart/onPacket x%zu on 4 threads/onStop, %lu passed\n", cap.packets.size(),
                 (unsigned long)want);
     return true;
 }
