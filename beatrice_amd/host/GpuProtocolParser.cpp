@@ -264,9 +264,50 @@ void GpuProtocolParser::run(GpuParsedBatch& b) {
     const uint32_t n = (uint32_t)b.frames_.size();
     b.recs_.resize(n);
     b.ctx_ = ctx_;
+    const auto t0 = std::chrono::steady_clock::now();
     if (n && bt_parse_filter_ptrs(ctx_, b.frames_.data(), b.lens_.data(), n, b.recs_.data(), nullptr, nullptr,
                                   nullptr, nullptr) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    // updateStats (src/parser/ProtocolParser.cpp:482-506) for every walked layer
+    static const char* kName[8] = {"ethernet", "vlan", "vlan", "ipv4", "ipv6", "tcp", "udp", "icmp"};
+    uint64_t ok = 0, bad = 0, per[8] = {};
+    for (const bt_rec& r : b.recs_) {
+        for (int k = 0; k < 8; ++k) {
+            if (!(r.present & (1u << k))) continue;
+            ++per[k];
+            if (r.ok & (1u << k)) ++ok; else ++bad;
+        }
+    }
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    const uint64_t layers = ok + bad;
+    if (!layers) return;
+    auto& st = stats_;
+    st.totalPacketsParsed += layers;
+    st.successfulParses += ok;
+    st.failedParses += bad;
+    const double each = us / (double)layers;
+    time_carry_us_ += us;
+    const auto total = std::chrono::microseconds((int64_t)time_carry_us_);
+    st.totalParseTime += total;
+    time_carry_us_ -= (double)total.count();
+    const auto per_layer = std::chrono::microseconds((int64_t)each);
+    if (per_layer < st.minParseTime) st.minParseTime = per_layer;
+    if (per_layer > st.maxParseTime) st.maxParseTime = per_layer;
+    if (st.successfulParses) st.averageParseTime = std::chrono::microseconds(st.totalParseTime.count() / st.successfulParses);
+    for (int k = 0; k < 8; ++k)
+        if (per[k]) st.protocolUsageCount[kName[k]] += per[k];
+}
+
+parser::ProtocolParser::ParserStats GpuProtocolParser::getStats() const {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    return stats_;
+}
+
+void GpuProtocolParser::resetStats() {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_ = parser::ProtocolParser::ParserStats{};
+    time_carry_us_ = 0.0;
 }
 
 GpuParsedBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets) {

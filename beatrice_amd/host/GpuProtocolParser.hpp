@@ -18,12 +18,14 @@
 #pragma once
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "beatrice/Packet.hpp"
 #include "beatrice_gpu.h"
 #include "parser/ParserResult.hpp"
+#include "parser/ProtocolParser.hpp"
 #include "parser/ProtocolRegistry.hpp"
 
 namespace beatrice {
@@ -78,9 +80,22 @@ public:
     // borrows `base` for the lifetime of the returned batch
     GpuParsedBatch parseBatch(const uint8_t* base, const bt_pkt_desc* desc, uint32_t n);
 
+    // ProtocolParser::getStats / resetStats (include/parser/ProtocolParser.hpp:40-54,
+    // src/parser/ProtocolParser.cpp:174-182, updateStats :482-506): every walked layer of
+    // every batch counts as one parsePacket call, with the same totalPacketsParsed /
+    // successfulParses / failedParses / protocolUsageCount. Times are the batch's wall
+    // time spread evenly over its layers, in whole microseconds as the reference keeps
+    // them. The reference divides by successfulParses and raises SIGFPE when the first
+    // parse on an instance fails; here the averages stay 0 until a parse succeeds.
+    parser::ProtocolParser::ParserStats getStats() const;
+    void resetStats();
+
 private:
     void run(GpuParsedBatch& b);
     bt_ctx* ctx_ = nullptr;
+    mutable std::mutex stats_mu_;
+    parser::ProtocolParser::ParserStats stats_;
+    double time_carry_us_ = 0.0;   // sub-microsecond remainder of the amortised time
 };
 
 }  // namespace gpu

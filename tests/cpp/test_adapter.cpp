@@ -234,7 +234,35 @@ static bool parser_case(const char* label, const Capture& cap) {
             CHECK(is_ref[b] == batch.is(i, 1u << b), "%s: packet %zu predicate bit %d", label, i, b);
         CHECK(ProtocolDetector::isARP(v) == batch.isARP(i), "%s: packet %zu isARP", label, i);
     }
-    std::printf("ok   parser  %-22s %zu packets, %zu layer results, detector\n", label, cap.packets.size(), nlayers);
+    // getStats: a reference parser with performance metrics on (its default), fed the same
+    // layers, counts the same (times are wall clock: not compared)
+    {
+        ProtocolParser counted;   // default ParserConfig: enablePerformanceMetrics = true
+        for (auto p : {BuiltinProtocols::createEthernetProtocol(), BuiltinProtocols::createVLANProtocol(),
+                       BuiltinProtocols::createIPv4Protocol(), BuiltinProtocols::createIPv6Protocol(),
+                       BuiltinProtocols::createTCPProtocol(), BuiltinProtocols::createUDPProtocol(),
+                       BuiltinProtocols::createICMPProtocol()})
+            counted.registerProtocol(p);
+        gpu.resetStats();
+        auto b2 = gpu.parseBatch(cap.packets);
+        // a failed first parse makes the reference divide by zero (SIGFPE): compare only
+        // captures whose first frame holds an Ethernet header
+        const bool first_ok = !cap.packets.empty() && cap.packets[0].length() >= 14;
+        for (size_t i = 0; first_ok && i < cap.packets.size(); ++i) {
+            const uint8_t* f = cap.packets[i].data();
+            const size_t len = cap.packets[i].length();
+            for (const auto& L : b2.layers(i)) (void)counted.parsePacket(std::vector<uint8_t>(f + L.offset, f + len), L.name);
+        }
+        const auto want = counted.getStats();
+        const auto got = gpu.getStats();
+        CHECK(!first_ok || (want.totalPacketsParsed == got.totalPacketsParsed && want.successfulParses == got.successfulParses &&
+                  want.failedParses == got.failedParses && want.protocolUsageCount == got.protocolUsageCount),
+              "%s: parser stats differ: total %lu/%lu ok %lu/%lu failed %lu/%lu", label,
+              (unsigned long)want.totalPacketsParsed, (unsigned long)got.totalPacketsParsed,
+              (unsigned long)want.successfulParses, (unsigned long)got.successfulParses,
+              (unsigned long)want.failedParses, (unsigned long)got.failedParses);
+    }
+    std::printf("ok   parser  %-22s %zu packets, %zu layer results, detector, stats\n", label, cap.packets.size(), nlayers);
     return true;
 }
 
