@@ -488,14 +488,12 @@ __device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32
 
 // Upper bound of the frame bytes the walk + filters will read, from round A's 64 B
 // (everything it looks at — EtherTypes at 12/16/20, IHL at L3+0 — sits below byte 49).
-__device__ __forceinline__ uint32_t header_end(const uint32_t* row, uint32_t s, uint32_t len, uint32_t floor_) {
-    uint32_t w[6];
-    window<6>(row, s, w);
-    const uint32_t et0 = be16_of(w, 12), et1 = be16_of(w, 16), et2 = be16_of(w, 20);
+// `w0` = the packet's first 40 bytes (window<10> at its start); only bytes < 28 are used.
+__device__ __forceinline__ uint32_t header_end(const uint32_t* w0, uint32_t len, uint32_t floor_) {
+    const uint32_t et0 = be16_of(w0, 12), et1 = be16_of(w0, 16), et2 = be16_of(w0, 20);
     uint32_t o3 = 14, et = et0;
     if (is_vlan(et0)) { o3 = 18; et = et1; if (is_vlan(et1)) { o3 = 22; et = et2; } }
-    const uint32_t a = s + o3;
-    const uint32_t ihl = (row[a >> 2] >> (8 * (a & 3u))) & 0x0Fu;
+    const uint32_t ihl = (o3 == 14u ? byte_of(w0, 14) : o3 == 18u ? byte_of(w0, 18) : byte_of(w0, 22)) & 0x0Fu;
     uint32_t end = o3;
     if (et == 0x0800u) end = o3 + 20u + (ihl > 5 ? 4u * ihl - 20u : 0u) + 20u;
     else if (et == 0x86DDu) end = o3 + 60u;
@@ -588,16 +586,21 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         wave_lds_sync();
         const bool this_wide = FIXED_LOG2 < 0 && st.wide;
         if (PREFETCH && t + step < t_end) issue_loads<FIXED_LOG2>(a, t + step, lane, st, wide, need_max);
+        // the packet's first 40 bytes; read once here (round A's chunks hold them) and
+        // again only if round B rewrote the row
+        const uint32_t s = (FIXED_LOG2 >= 0) ? 0u : ((uint32_t)my_off & 15u);
+        uint32_t w0[10];
+        window<10>(row, s, w0);
         if constexpr (FIXED_LOG2 < 0) {
             if (REC != kRecNone) {   // filter-only needs <= 38 B: round A always suffices
-                const uint32_t s0 = (uint32_t)my_off & 15u;
+                const uint32_t s0 = s;
                 // bytes from a0 that round A read, and whether they hold what header_end reads;
                 // the floor of 38 B covers the PacketFilter gates and the detector column
                 const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s0, my_len, need_max)
                                                  : min(64u, s0 + my_len);
                 const bool cov = a_end >= s0 + min(my_len, 28u);
                 const uint32_t end = !live ? 0u
-                                   : cov ? s0 + header_end(row, s0, my_len, kNeedFilter)
+                                   : cov ? s0 + header_end(w0, my_len, kNeedFilter)
                                          : s0 + min(my_len, need_max);
                 const uint32_t lo = (a_end + 15u) >> 4;   // first chunk round A did not read
                 const bool my_nb = end > 16u * lo;
@@ -606,6 +609,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                     const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
                     load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
                     wave_lds_sync();
+                    window<10>(row, s, w0);
                 }
                 wide = __popcll(__ballot(end > 64u)) > 32;   // decides the wave's next issue
                 if (a.nt & 12u) wide = (a.nt & 8u) != 0u;   // A/B knobs
@@ -613,10 +617,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         }
 
         // ---- 2. PARSE -------------------------------------------------------
-        const uint32_t s = (FIXED_LOG2 >= 0) ? 0u : ((uint32_t)my_off & 15u);
         const uint32_t len = live ? my_len : 0u;
-        uint32_t w0[10];
-        window<10>(row, s, w0);
 
         if (REC != kRecNone && live) {
             Parsed p;
