@@ -37,6 +37,7 @@ struct MainArgs {
                                // bit2 / bit3 force two-round / wide loads (A/B)
     const uint8_t* dfa;        // PAYLOAD DFA pool (device), copied to dynamic LDS per block
     uint32_t dfa_bytes;        // 0: the program has no BT_K_PAYLOAD slot
+    uint32_t prefixes;         // BT_BATCH_PREFIXES: base holds header prefixes only
 };
 
 constexpr uint32_t kDfaPoolMax = 16384;   // bytes of DFA tables per program (LDS budget)

@@ -683,7 +683,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                 if (__ballot(open) == 0ull) break;
                 uint32_t r;
                 if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
-                    r = open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0,
+                    r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
+                      : open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0,
                                             staged_sh)
                              : 0u;
                 else

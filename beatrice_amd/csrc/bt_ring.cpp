@@ -15,10 +15,12 @@
 //                  tp_mac, tp_net, ... }, MAC header at frame + tp_mac.
 // num_pkts is in the block header, so a prefix over the taken blocks places every
 // block's descriptors before any frame is read and the blocks are walked in parallel.
+#include <emmintrin.h>
 #include <linux/if_packet.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <vector>
 
 #include "bt_host.h"
@@ -53,10 +55,57 @@ struct Chain {
     uint32_t j, n, delay;
     bt_pkt_desc* out;
     int64_t block;
+    uint64_t first;            // global index of the block's first frame (slot numbering)
+    const uint8_t* pend;       // gather: frame whose prefix is copied on the next visit
+    uint32_t pend_len;
+    uint8_t* pend_slot;
 };
 
+inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+
+// The bytes the layer walk and the built-in filters read (the kernel's header_end,
+// bt_kernels.hip): EtherTypes at 12/16/20, IHL at L3, at least 38 (filter gates and the
+// detector), rounded up to 16 and capped at the frame.
+inline uint32_t prefix_len(const uint8_t* f, uint32_t len) {
+    uint32_t end = 38;
+    if (len >= 24) {
+        uint32_t o3 = 14, et = be16(f + 12);
+        if (et == 0x8100u || et == 0x88A8u) {
+            o3 = 18;
+            et = be16(f + 16);
+            if (et == 0x8100u || et == 0x88A8u) { o3 = 22; et = be16(f + 20); }
+        }
+        if (et == 0x0800u && len > o3) {
+            const uint32_t ihl = f[o3] & 0x0Fu;
+            end = o3 + 20u + (ihl > 5 ? 4u * ihl - 20u : 0u) + 20u;
+        } else if (et == 0x86DDu) {
+            end = o3 + 60u;
+        }
+        end = end > 38u ? end : 38u;
+    }
+    end = (end + 15u) & ~15u;
+    if (end > BT_PREFIX_SLOT) end = BT_PREFIX_SLOT;
+    return end < len ? end : len;
+}
+
+// Non-temporal 16-B stores into the (16-B-aligned) slot: the slot lines are not read
+// for ownership first, and they do not evict the ring lines the chains still walk.
+inline void copy_prefix(Chain& ch) {
+    const uint32_t m = prefix_len(ch.pend, ch.pend_len);
+    if (((uintptr_t)ch.pend_slot & 15u) == 0) {
+        for (uint32_t k = 0; k < m; k += 16) {
+            const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k), v);
+        }
+    } else {
+        std::memcpy(ch.pend_slot, ch.pend, m);
+    }
+    ch.pend = nullptr;
+}
+
+template <bool GATHER>
 int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_t* start, uint32_t count,
-                    bt_pkt_desc* desc) {
+                    bt_pkt_desc* desc, uint8_t* slots) {
     const uint64_t bs = r->block_size;
     for (uint32_t g0 = 0; g0 < count; g0 += kChains) {
         Chain c[kChains];
@@ -72,6 +121,8 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
             ch.j = 0;
             ch.out = desc + start[k];
             ch.block = b;
+            ch.first = start[k];
+            ch.pend = nullptr;
             if (ch.n) {
                 __builtin_prefetch(ch.blk + ch.off);
                 ++live;
@@ -86,13 +137,25 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                     ++g;
                     continue;
                 }
+                if (GATHER && ch.pend) copy_prefix(ch);   // its lines were prefetched a round ago
                 if (ch.off + sizeof(tpacket3_hdr) > bs) return ch.block;
                 const tpacket3_hdr* h = reinterpret_cast<const tpacket3_hdr*>(ch.blk + ch.off);
                 const uint64_t mac = ch.off + h->tp_mac;
                 const uint32_t snap = h->tp_snaplen, next = h->tp_next_offset;
                 if (mac + snap > bs) return ch.block;
-                ch.out[ch.j] = BT_DESC(ch.base_off + mac, std::min<uint32_t>(snap, kDescLenMax));
+                if (GATHER) {
+                    const uint64_t i = ch.first + ch.j;
+                    ch.out[ch.j] = BT_DESC(i * BT_PREFIX_SLOT, std::min<uint32_t>(snap, kDescLenMax));
+                    ch.pend = ch.blk + mac;
+                    ch.pend_len = snap;
+                    ch.pend_slot = slots + i * BT_PREFIX_SLOT;
+                    __builtin_prefetch(ch.pend);
+                    __builtin_prefetch(ch.pend + 63);
+                } else {
+                    ch.out[ch.j] = BT_DESC(ch.base_off + mac, std::min<uint32_t>(snap, kDescLenMax));
+                }
                 if (++ch.j == ch.n) {          // chain done: swap in the last live one
+                    if (GATHER && ch.pend) copy_prefix(ch);
                     c[g] = c[--live];
                     continue;
                 }
@@ -110,8 +173,10 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
 
 extern "C" {
 
-int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
-                      bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
+namespace {
+
+int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks, uint8_t* slots,
+              bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
     if (!ring || !ring->base || !n_desc || !n_blocks_taken || (cap && !desc))
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3: null argument");
     if (!ring->n_blocks || ring->block_size < sizeof(tpacket_block_desc) || first_block >= ring->n_blocks)
@@ -141,7 +206,9 @@ int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_bloc
     auto work = [&](unsigned w, unsigned T) {
         const uint32_t a = (uint32_t)((uint64_t)nb * w / T), b = (uint32_t)((uint64_t)nb * (w + 1) / T);
         if (a >= b) return;
-        const int64_t e = walk_blocks(ring, blocks.data() + a, start.data() + a, b - a, desc);
+        const int64_t e = slots ? walk_blocks<true>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
+                                : walk_blocks<false>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr);
+        if (slots) _mm_sfence();   // this worker's streaming stores land before the join
         if (e >= 0) bad.store(e);
     };
     if (total >= 4096 && nb > 1) bt::host_parallel(ctx, work);
@@ -152,6 +219,20 @@ int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_bloc
     *n_desc = (uint32_t)total;
     *n_blocks_taken = nb;
     return BT_OK;
+}
+
+}  // namespace
+
+int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                      bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
+    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, desc, cap, n_desc, n_blocks_taken);
+}
+
+int bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                        uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
+                        uint32_t* n_blocks_taken) {
+    if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_tpv3: null slots");
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, desc, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count) {

@@ -230,6 +230,7 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.base = b->base;
     a.desc = static_cast<const uint64_t*>(b->desc);
     a.desc_words = b->desc_format == BT_DESC_XDP ? 2u : 1u;
+    a.prefixes = (b->flags & BT_BATCH_PREFIXES) ? 1u : 0u;
     a.stride = b->stride;
     a.n = b->n;
     a.ntiles = (b->n + 63) / 64;

@@ -301,8 +301,13 @@ typedef struct bt_batch {          /* input; device memory or host memory mapped
     uint32_t n;                    /* packets                                           */
     uint64_t bytes;                /* size of the base buffer (bounds check)            */
     uint32_t desc_format;          /* BT_DESC_PACKED / BT_DESC_XDP                      */
-    uint32_t reserved;
+    uint32_t flags;                /* BT_BATCH_*                                        */
 } bt_batch;
+
+/* bt_batch.flags */
+#define BT_BATCH_PREFIXES 0x1u     /* base holds header prefixes (bt_ring_gather_tpv3), not
+                                      whole frames: PAYLOAD slots, which read past the
+                                      headers, are left to the host (BT_DECIDE_HOST)     */
 
 typedef struct bt_outputs {        /* any pointer may be NULL = not produced            */
     void*     records;             /* ceil(n/64) * 6144 bytes, tiled slabs (see above)  */
@@ -410,6 +415,18 @@ typedef struct bt_tpv3_ring {
 int  bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block,
                        uint32_t max_blocks, bt_pkt_desc* desc, uint32_t cap,
                        uint32_t* n_desc, uint32_t* n_blocks_taken);
+/* The same walk, and each frame's header prefix is also copied into slot i of `slots`
+ * (BT_PREFIX_SLOT bytes per frame, slot i at i * BT_PREFIX_SLOT): the bytes the layer walk
+ * and the built-in filters read, i.e. max(38, the walked header end) rounded up to 16, at
+ * most the frame. desc[i] = BT_DESC(i * BT_PREFIX_SLOT, min(tp_snaplen, 65535)). A batch
+ * over `slots` (registered, or copied to the device) with flags = BT_BATCH_PREFIXES then
+ * reads one aligned 64-B host line per packet over PCIe for headers up to 64 B, instead
+ * of a window straddling the ring's 2-mod-16 frame starts. The walker copies while its
+ * chains are in flight, one frame behind each chain's header read. */
+#define BT_PREFIX_SLOT 128u
+int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                         uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
+                         uint32_t* n_blocks_taken);
 /* Hands `count` blocks starting at first_block back to the kernel (TP_STATUS_KERNEL,
  * release-ordered). Call it once the device has finished reading them. */
 int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);

@@ -95,3 +95,66 @@ def test_cpp_stage_synthetic_ring():
     r = subprocess.run([CAPTURE_BIN, "stage-synth"], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def _run_gathered(ctx, ring, bs, nb, filters):
+    """bt_ring_gather_tpv3 -> device run over the 128-B prefix slots (BT_BATCH_PREFIXES),
+    slots and outputs in registered host memory."""
+    wdesc, _ = abi.ring_walk_tpv3(ring, bs, nb, ctx=ctx)
+    n = len(wdesc)
+    slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)   # poison past each prefix
+    gd = np.zeros(n, np.uint64)
+    desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx)
+    assert taken == nb and len(desc) == n
+    tiles = (n + 63) // 64
+    h_rec = np.zeros(tiles * 6144, np.uint8)
+    h_dec = np.zeros(tiles * 64, np.uint8)
+    h_ver = np.zeros(tiles, np.uint64)
+    ctx.compile(filters)
+    held = [slots, gd, h_dec, h_ver, h_rec]
+    dev = [ctx.register(a) for a in held]
+    try:
+        batch = abi.Batch(dev[0], dev[1], 0, n, slots.nbytes, abi.DESC_PACKED, abi.BATCH_PREFIXES)
+        ctx.run_device(batch, abi.Outputs(dev[4], n, dev[3], dev[2], None, None))
+        ctx.synchronize()
+    finally:
+        for a in held:
+            ctx.unregister(a)
+    return wdesc, abi.untile_records(h_rec, n), h_dec[:n]
+
+
+def test_gathered_prefixes_match_reference(gpu_ctx):
+    """Header prefixes gathered by the walker give the kernels the reference's records
+    and decisions on the kernel-written ring; a PAYLOAD slot is left to the host."""
+    g = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    bs, nb = (int(x) for x in g["geometry"])
+    for s in man["rings"]["ring_lo"]["filter_sets"]:
+        filters = man["filter_sets"][s]
+        if any(f["type"] == abi.PAYLOAD for f in filters):
+            continue
+        desc, rec, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, filters)
+        assert np.array_equal(desc, g["desc"])
+        assert np.array_equal(rec, g["rec"])
+        compare_decisions(dec, g[f"code__{s}"], g[f"src__{s}"], filters, where=f"ring_lo/{s} gathered")
+    pay = [{"type": abi.PROTOCOL, "expr": "tcp", "priority": 3}, {"type": abi.PAYLOAD, "expr": "GET", "priority": 2}]
+    _, _, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, pay)
+    _, _, dref, _ = _run_ring(gpu_ctx, g["ring"].copy(), bs, nb, pay, records=False)
+    code, slot = dec >> 6, dec & 63
+    reached = ((dref >> 6) != 1) | ((dref & 63) == 1)   # packets the PAYLOAD slot decides
+    assert np.all(code[reached] == 3) and np.array_equal(dec[~reached], dref[~reached])
+
+
+@pytest.mark.parametrize("cfg", [synth.C3, synth.C4, synth.FUZZ])
+def test_gathered_prefixes_1m_match_oracle(gpu_ctx, cfg):
+    data, desc0 = synth.capture(cfg, 1 << 20, seed=23)
+    ring, _, used = synth.tpv3_ring(data, desc0)
+    desc, rec, dec = _run_gathered(gpu_ctx, ring, synth.TPV3_BLOCK, used, C3_SET)
+    orec, odec, _ = ol.oracle_run(ring, desc, len(desc), C3_SET)
+    assert np.array_equal(rec, orec)
+    assert np.array_equal(dec, odec)
+
+
+C3_SET = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+          {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+          {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]

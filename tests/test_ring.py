@@ -166,3 +166,36 @@ def test_cpp_backend_on_loopback():
     r = subprocess.run([CAPTURE_BIN, "backend"], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("which", ["kernel_ring", "c2", "c3", "c4", "fuzz"])
+def test_gather_prefixes_hold_every_byte_the_walk_reads(which):
+    """bt_ring_gather_tpv3: the header prefixes in their 128-B slots (rest of each slot
+    poisoned) give the oracle the same records and filter decisions as the whole frames
+    in the ring, for every built-in filter set; descriptors keep the real lengths."""
+    import json
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    if which == "kernel_ring":
+        g, bs, nb = _fixture()
+        ring, used = g["ring"].copy(), nb
+    else:
+        cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4, "fuzz": synth.FUZZ}[which]
+        data, desc = synth.capture(cfg, 6000, seed=11)
+        bs = 1 << 16
+        ring, _, used = synth.tpv3_ring(data, desc, block_size=bs)
+    wdesc, taken = abi.ring_walk_tpv3(ring, bs, used)
+    n = len(wdesc)
+    slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)
+    out = np.zeros(n, np.uint64)
+    gdesc, gtaken = abi.ring_gather_tpv3(ring, bs, used, slots, out)
+    assert gtaken == taken and len(gdesc) == n
+    assert np.array_equal(synth.desc_len(gdesc), synth.desc_len(wdesc))
+    assert np.array_equal(synth.desc_off(gdesc), np.arange(n, dtype=np.uint64) * abi.PREFIX_SLOT)
+    rec_w, _, _ = ol.oracle_run(ring, wdesc, n, None, parse=True)
+    rec_g, _, _ = ol.oracle_run(slots, gdesc, n, None, parse=True)
+    assert np.array_equal(rec_g, rec_w)
+    for s in ("c3", "mixed", "throw_after", "bpf_1", "port_range_1", "ip_range_1"):
+        filters = man["filter_sets"][s]
+        _, dw, _ = ol.oracle_run(ring, wdesc, n, filters, parse=False)
+        _, dg, _ = ol.oracle_run(slots, gdesc, n, filters, parse=False)
+        assert np.array_equal(dg, dw), s

@@ -25,6 +25,9 @@ ap.add_argument("--tpacket", action="store_true",
                 help="pack the capture into an AF_PACKET TPACKET_V3 ring image (kernel layout), register "
                      "it, and run ring -> walk (bt_ring_walk_tpv3, host pool) -> kernels reading frames "
                      "in place -> outputs in registered host memory, walking batch k+1 while batch k runs")
+ap.add_argument("--gather", action="store_true",
+                help="with --tpacket: the walker also copies each frame's header prefix into 128-B pinned "
+                     "slots (bt_ring_gather_tpv3) and the kernels read the slots (BT_BATCH_PREFIXES)")
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
 ap.add_argument("--host-threads", type=int, default=0)
 a = ap.parse_args()
@@ -44,6 +47,9 @@ if a.tpacket:
     d_ring = ctx.register(ring)
     h_desc = np.zeros(n + 64, np.uint64)
     d_desc = ctx.register(h_desc)
+    if a.gather:
+        slots = np.zeros((n + 64) * abi.PREFIX_SLOT, np.uint8)
+        d_slots = ctx.register(slots)
     for mode in ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
         tiles = (n + 63) // 64 + nbat + 1          # each batch starts its outputs on a fresh tile
@@ -58,7 +64,13 @@ if a.tpacket:
         def one_pass(walk=True):
             start, tile = 0, 0
             for k in range(nbat):
-                if walk:
+                if walk and a.gather:
+                    got, taken = abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B,
+                                                      max_blocks=min(B, used - k * B), ctx=ctx, slot_base=start)
+                    cnt = len(got)
+                    if len(counts) < nbat:
+                        counts.append(cnt)
+                elif walk:
                     got, taken = abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B),
                                                     ctx=ctx, out=h_desc[start:])
                     cnt = len(got)
@@ -66,7 +78,11 @@ if a.tpacket:
                         counts.append(cnt)
                 else:
                     cnt = counts[k]
-                batch = abi.Batch(d_ring, d_desc + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
+                if a.gather:
+                    batch = abi.Batch(d_slots + abi.PREFIX_SLOT * start, d_desc + 8 * start, 0, cnt,
+                                      abi.PREFIX_SLOT * cnt, abi.DESC_PACKED, abi.BATCH_PREFIXES)
+                else:
+                    batch = abi.Batch(d_ring, d_desc + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
                 outs = abi.Outputs(d_rec + 6144 * tile if rec else None, cnt, d_ver + 8 * tile, d_dec + 64 * tile,
                                    None, None)
                 ctx.run_device(batch, outs)      # async: the next walk overlaps this batch
@@ -88,12 +104,18 @@ if a.tpacket:
             kbest = min(kbest, time.perf_counter() - t0)
         t0 = time.perf_counter()
         for k in range(nbat):
-            abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
-                               out=h_desc[:])
+            if a.gather:
+                abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B, max_blocks=min(B, used - k * B),
+                                     ctx=ctx)
+            else:
+                abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
+                                   out=h_desc[:])
         walk = time.perf_counter() - t0
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
-        print(json.dumps({"config": a.config, "mode": "tpacket_v3 ring, zero-copy, " + mode, "packets": n,
+        how = "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
+            "tpacket_v3 ring, zero-copy, "
+        print(json.dumps({"config": a.config, "mode": how + mode, "packets": n,
                           "ring_blocks": used, "block_bytes": bs, "batch_blocks": B, "seconds": round(best, 4),
                           "mpps": round(n / best / 1e6, 1), "walk_only_mpps": round(n / walk / 1e6, 1),
                           "kernels_only_mpps": round(n / kbest / 1e6, 1),
@@ -103,6 +125,8 @@ if a.tpacket:
             ctx.unregister(h)
     ctx.unregister(h_desc)
     ctx.unregister(ring)
+    if a.gather:
+        ctx.unregister(slots)
     sys.exit(0)
 
 if a.zero_copy:
