@@ -217,6 +217,25 @@ __device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s
         const uint32_t v4[5] = {b0 | (byte_of(w3, 1) << 8) | (byte_of(w3, 8) << 16) | (proto << 24),
                                 be16_of(w3, 2) | (be16_of(w3, 4) << 16), be16_of(w3, 6) | (be16_of(w3, 10) << 16),
                                 w3[3], w3[4]};
+#ifndef BT_NO_SIMPLE_WAVES
+        // Wave-uniform fast path: no lane of the wave parsed IPv6 or a second tag (every
+        // C2/C3 wave). Then ne <= 1 and L is IPv4 + L4 or nothing: one select per dword
+        // instead of three.
+        if (__ballot(v6ok || v1ok) == 0ull) {
+            // l4v is 0 unless v4ok here, so only the IPv4 dwords need the v4ok select
+            uint32_t Ls[11];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) Ls[j] = v4ok ? v4[j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) Ls[5 + j] = l4v[j];
+            Ls[10] = 0u;
+#pragma unroll
+            for (int j = 0; j < 19; ++j)
+                p.r[5 + j] = j > 10 ? 0u : v0ok ? (j == 0 ? x0 : Ls[j > 0 ? j - 1 : 0]) : Ls[j <= 10 ? j : 0];
+            const uint32_t nd = 5u + ne + (v4ok ? 5u : 0u) + (tcp_ok ? 5u : (udp_ok || icmp_ok) ? 2u : 0u);
+            return (nd + 3u) >> 2;
+        }
+#endif
         uint32_t L[15];
 #pragma unroll
         for (int j = 0; j < 15; ++j)

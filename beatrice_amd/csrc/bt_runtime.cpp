@@ -755,50 +755,42 @@ int bt_synchronize(bt_ctx* c) {
 
 namespace {
 
-// Unpacks the packed device record (bt_kernels.hip pack_record; layout in
-// beatrice_gpu.h) into a bt_rec. `slab(k)` returns the k-th 16-B slab; only the slabs
-// the record holds are read.
+// Unpacks the packed device record (bt_kernels.hip parse_packet<true>; layout in
+// beatrice_gpu.h) into a bt_rec. `slab(k)` returns the k-th 16-B slab; all six are read
+// (every layout keeps slab k of a record in bounds) and the dwords past the record's own
+// are masked off, so the unpack has no data-dependent branches: a capture's random mix
+// of tags / L3 / L4 costs no mispredictions.
 template <class Slab>
-void unpack_record(Slab slab, bt_rec* out) {
-    uint32_t c[24] = {};
-    std::memcpy(c, slab(0), 16);
-    std::memcpy(c + 4, slab(1), 16);
+inline void unpack_record(Slab slab, bt_rec* out) {
+    uint32_t c[24];
+    for (uint32_t k = 0; k < BT_REC_SLABS; ++k) std::memcpy(c + 4 * k, slab(k), 16);
     const uint32_t present = c[4] & 0xFFu, ok = (c[4] >> 8) & 0xFFu;
-    const uint32_t ne = ((ok & BT_L_VLAN0) ? 1u : 0u) + ((ok & BT_L_VLAN1) ? 1u : 0u);
-    const bool ok4 = ok & BT_L_IPV4, ok6 = ok & BT_L_IPV6;
+    const uint32_t v0 = (ok & BT_L_VLAN0) ? 1u : 0u, v1 = (ok & BT_L_VLAN1) ? 1u : 0u, ne = v0 + v1;
+    const uint32_t m4 = (ok & BT_L_IPV4) ? ~0u : 0u, m6 = (ok & BT_L_IPV6) && !m4 ? ~0u : 0u;
     const uint32_t l4d = (ok & BT_L_TCP) ? 5u : (ok & (BT_L_UDP | BT_L_ICMP)) ? 2u : 0u;
-    const uint32_t nd = 5u + ne + (ok4 ? 5u : ok6 ? 10u : 0u) + l4d;
-    for (uint32_t k = 2; 4 * k < nd; ++k) std::memcpy(c + 4 * k, slab(k), 16);
-    const uint32_t x0 = ne >= 1 ? c[5] : 0u, x1 = ne >= 2 ? c[6] : 0u;
-    const uint32_t* L = c + 5 + ne;
-    uint32_t r[24] = {};
+    const uint32_t x0 = v0 ? c[5] : 0u, x1 = v1 ? c[6] : 0u;
+    const uint32_t* L = c + 5 + ne;   // <= c + 7: L[0..16] stays inside c
+    uint32_t r[24];
     r[0] = c[0]; r[1] = c[1]; r[2] = c[2]; r[3] = c[3];
-    r[4] = ((ok & BT_L_VLAN0) ? (c[3] & 0xFFFFu) : 0u) | (x0 & 0xFFFF0000u);   // tpid0 == ethertype
+    r[4] = (v0 ? (c[3] & 0xFFFFu) : 0u) | (x0 & 0xFFFF0000u);   // tpid0 == ethertype
     r[5] = (x0 & 0xFFFFu) | (x1 << 16);
     // the walk's offsets (R-WALK): L3 after the tags the walk attempted; L4 after the
     // IPv4 header (IHL) or the fixed 40-B IPv6 header
     const uint32_t o3 = 14u + ((present & BT_L_VLAN0) ? 4u : 0u) + ((present & BT_L_VLAN1) ? 4u : 0u);
-    uint32_t l3_off = (present & (BT_L_IPV4 | BT_L_IPV6)) ? o3 : 0u, l4_off = 0;
-    const uint32_t* l4 = nullptr;
-    if (ok4) {
-        const uint32_t b0 = L[0] & 0xFFu, tos = (L[0] >> 8) & 0xFFu, ttl = (L[0] >> 16) & 0xFFu, proto = L[0] >> 24;
-        r[7] = b0 | (b0 << 8) | (tos << 16) | (ttl << 24);
-        r[8] = proto | (L[1] << 16);
-        r[9] = (L[1] >> 16) | (L[2] << 16);
-        r[10] = L[2] >> 16;
-        r[11] = L[3];
-        r[12] = L[4];
-        l4 = L + 5;
-        if (present & (BT_L_TCP | BT_L_UDP | BT_L_ICMP)) l4_off = o3 + 4u * (b0 & 0x0Fu);
-    } else if (ok6) {
-        for (int j = 0; j < 10; ++j) r[7 + j] = L[j];
-        l4 = L + 10;
-        if (present & (BT_L_TCP | BT_L_UDP)) l4_off = o3 + 40u;
-    }
+    const uint32_t l3_off = (present & (BT_L_IPV4 | BT_L_IPV6)) ? o3 : 0u;
+    const uint32_t b0 = L[0] & 0xFFu;
+    const uint32_t l4_off = (m4 && (present & (BT_L_TCP | BT_L_UDP | BT_L_ICMP))) ? o3 + 4u * (b0 & 0x0Fu)
+                          : (m6 && (present & (BT_L_TCP | BT_L_UDP))) ? o3 + 40u : 0u;
     r[6] = present | (ok << 8) | (l3_off << 16) | (l4_off << 24);
-    if (l4)
-        for (uint32_t j = 0; j < l4d; ++j) r[17 + j] = l4[j];
+    // IPv4 in bt_rec's padded layout, or IPv6 as stored, or nothing
+    const uint32_t v4[10] = {b0 | (b0 << 8) | (((L[0] >> 8) & 0xFFu) << 16) | (((L[0] >> 16) & 0xFFu) << 24),
+                             (L[0] >> 24) | (L[1] << 16), (L[1] >> 16) | (L[2] << 16), L[2] >> 16, L[3], L[4],
+                             0u, 0u, 0u, 0u};
+    for (int j = 0; j < 10; ++j) r[7 + j] = (v4[j] & m4) | (L[j] & m6);
+    const uint32_t* l4 = L + ((m4 & 5u) | (m6 & 10u));
+    for (uint32_t j = 0; j < 5; ++j) r[17 + j] = j < l4d ? l4[j] : 0u;
     r[22] = ((c[4] >> 16) & 7u) | (((c[4] >> 19) & 0xFFu) << 8) | (((c[4] >> 27) & 7u) << 16);
+    r[23] = 0;
     std::memcpy(out, r, sizeof(r));
 }
 
@@ -810,10 +802,8 @@ extern "C" {
 // need slab k. ns[] = the tile's slab counts, read from the full slab-1 region.
 static void tile_slab_counts(const uint8_t* tile, uint32_t* ns) {
     for (uint32_t j = 0; j < 64; ++j) {
-        uint32_t c4;
-        std::memcpy(&c4, tile + (64 + j) * 16, 4);
         bt_rec r;
-        r.ok = (uint8_t)(c4 >> 8);
+        r.ok = tile[(64 + j) * 16 + 1];   // slab 1, dword 0, byte 1
         ns[j] = bt_record_slabs(&r);
     }
 }
@@ -827,6 +817,20 @@ static void gather_tiled(const uint8_t* tile, const uint32_t* ns, uint32_t lane,
         }
         return tile + ((size_t)k * 64 + slot) * 16;
     }, out);
+}
+
+// Records [lo, hi) of one tile (lane order): the slab-k ranks are running counts, so a
+// whole tile unpacks in one pass.
+static void unpack_tile(const uint8_t* tile, uint32_t lo, uint32_t hi, bt_rec* out) {
+    uint32_t rank[BT_REC_SLABS] = {};
+    for (uint32_t j = 0; j < hi; ++j) {
+        bt_rec r;
+        r.ok = tile[(64 + j) * 16 + 1];
+        const uint32_t ns = bt_record_slabs(&r);
+        uint32_t at[BT_REC_SLABS] = {j, j, rank[2], rank[3], rank[4], rank[5]};
+        for (uint32_t k = 2; k < ns; ++k) ++rank[k];
+        if (j >= lo) unpack_record([&](uint32_t k) { return tile + ((size_t)k * 64 + at[k]) * 16; }, out + j);
+    }
 }
 
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out) {
@@ -851,16 +855,17 @@ int bt_record_unpack(bt_ctx* ctx, const void* records, uint32_t n_cap, uint32_t 
         const uint32_t lo = (uint32_t)((uint64_t)n * w / T), hi = (uint32_t)((uint64_t)n * (w + 1) / T);
         uint64_t cnt = 0;
         bt_rec r;
-        uint32_t ns[64];
-        uint32_t ns_tile = ~0u;
         for (uint32_t i = lo; i < hi; ++i) {
             if (out) {
                 if (planes) {
                     bt_record_gather_planes(records, n_cap, i, out + i);
-                } else {
-                    const uint8_t* tile = p + (size_t)(i / 64) * BT_REC_SLABS * 64 * 16;
-                    if (ns_tile != i / 64) { tile_slab_counts(tile, ns); ns_tile = i / 64; }
-                    gather_tiled(tile, ns, i % 64, out + i);
+                } else {   // the rest of i's tile in one pass
+                    const uint32_t t = i / 64, e = std::min(hi, t * 64 + 64);
+                    unpack_tile(p + (size_t)t * BT_REC_SLABS * 64 * 16, i % 64, e - t * 64, out + t * 64);
+                    if (slabs)
+                        for (uint32_t j = i; j < e; ++j) cnt += bt_record_slabs(out + j);
+                    i = e - 1;
+                    continue;
                 }
                 if (slabs) cnt += bt_record_slabs(out + i);
             } else {   // count only: the ok byte sits in slab 1

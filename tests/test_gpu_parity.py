@@ -98,13 +98,16 @@ def test_seeded_captures_match_oracle(gpu_ctx, cfg, n):
     check_filter_outputs(out, n)
 
 
-@pytest.mark.parametrize("cap", ["c3", "c4", "fuzz", "edge"])
-def test_host_batch_path(cap):
+@pytest.mark.parametrize("cap,layout", [("c3", "tiled"), ("c4", "tiled"), ("fuzz", "tiled"), ("edge", "tiled"),
+                                        ("c4", "planes"), ("edge", "aos")])
+def test_host_batch_path(cap, layout):
     """bt_parse_filter: host buffers, prefix gather into pinned staging, multi-chunk
-    double-buffered pipeline (chunk 1024 packets)."""
+    double-buffered pipeline (chunk 1024 packets). The pipeline copies bt_rec AoS back
+    whatever record layout the context's flags select for device batches."""
     g, man = load_golden(cap)
     n = len(g["desc"])
-    ctx = abi.Context(0, host_chunk_packets=1000)
+    flags = {"tiled": 0, "planes": abi.OPT_RECORDS_PLANES, "aos": abi.OPT_RECORDS_AOS}[layout]
+    ctx = abi.Context(0, host_chunk_packets=1000, flags=flags)
     try:
         filters = man["filter_sets"]["c3"]
         ctx.compile(filters)
