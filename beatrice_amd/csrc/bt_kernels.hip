@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 
 #include "bt_device.h"
 
@@ -725,6 +727,264 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     }
 }
 
+// ---- descriptor-mode pipeline with counted waits ------------------------------
+// gfx950 has one vmcnt counter for loads AND stores, retired in issue order. In
+// bt_parse_filter_main the loop top waits for the prefetched header loads, and because
+// some paths between the prefetch and that wait issue fewer stores (exec-skipped
+// blocks, the early `break` of the slab loop, null outputs), the compiler can only
+// emit vmcnt(0) there: every tile waited for its predecessor's record stores to be
+// acknowledged, and for the next tile's descriptor load right after. Here every store
+// of a tile is an unconditional buffer store (lanes that must not write get an
+// offset past the descriptor's range, which the hardware drops), the header loads of
+// lanes with nothing to read load a zero line instead of being skipped, and the
+// descriptors are loaded one tile ahead. Every path then issues the same operations,
+// so the wait for the next tile's headers is vmcnt(K) with K = this tile's stores:
+// the stores retire in the background.
+__device__ uint4 g_zero16[8];                    // source of the loads that read nothing
+constexpr uint32_t kOob = 0x80000000u;           // buffer offset past every range: dropped / reads 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// This lane's descriptor of tile t (0 past n or when !valid): one buffer load either way.
+// DW = descriptor words (1 bt_pkt_desc, 2 xdp_desc), a template argument so that no
+// register is written on one format's path and loaded on the other's.
+template <int DW>
+__device__ __forceinline__ void load_desc_pipe(const MainArgs& a, uint32_t t, bool valid, uint32_t lane,
+                                               uint32_t (&dw)[DW + 1]) {
+    const uint32_t p0 = t * 64u;
+    const uint32_t cnt = valid && p0 < a.n ? min(64u, a.n - p0) : 0u;
+    if constexpr (DW == 1) {
+        const auto r = rsrc_of(a.desc + (valid ? p0 : 0u), cnt * 8u);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, 0);
+        dw[0] = v.x; dw[1] = v.y;
+    } else {
+        const auto r = rsrc_of(a.desc + (valid ? 2ull * p0 : 0ull), cnt * 16u);
+        typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(lane * 16u), 0, 0);
+        dw[0] = v.x; dw[1] = v.y; dw[2] = v.z;
+    }
+}
+
+// Round A of tile t from descriptor words already in registers (issue_loads' loads,
+// with the zero line standing in for the skipped ones).
+template <int DW>
+__device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t t, bool valid, uint32_t lane,
+                                                   const uint32_t (&dw)[DW + 1], Stage<-1>& st, bool wide,
+                                                   uint32_t need_max) {
+    const uint32_t p0 = t * 64u;
+    const bool live = valid && p0 + lane < a.n;
+    if constexpr (DW == 1) {
+        st.off = ((uint64_t)(dw[1] & 0xFFFFu) << 32) | dw[0];
+        st.len = dw[1] >> 16;
+    } else {
+        st.off = ((uint64_t)dw[1] << 32) | dw[0];
+        st.len = dw[DW] > 0xFFFFu ? 0xFFFFu : dw[DW];
+    }
+    if (!live) { st.off = 0; st.len = 0; }
+    const uint32_t off_lo = (uint32_t)st.off, off_hi = (uint32_t)(st.off >> 32);
+    const uint32_t c = lane & 3u;
+    st.wide = wide;
+    const bool ntl = (a.nt & 2u) && !wide;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t q = j * 16u + (lane >> 2);
+        const uint64_t qo = ((uint64_t)(uint32_t)__shfl((int)off_hi, (int)q) << 32) |
+                            (uint32_t)__shfl((int)off_lo, (int)q);
+        const uint32_t ql = (uint32_t)__shfl((int)st.len, (int)q);
+        const uint64_t a0 = qo & ~15ull;
+        const uint64_t addr = a0 + 16u * c;
+        const uint32_t sq = (uint32_t)qo & 15u;
+        st.qa0[j] = a0;
+        const bool live_q = valid && p0 + q < a.n;
+        const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
+        const bool ok = live_q && (16u * c < a_end) && (addr + 16u <= a.bytes);
+        st.v[j] = ld16(ok ? a.base + addr : zero, ntl);
+        if (wide) {
+            const bool okb = live_q && (16u * (c + 4u) < a_end) && (addr + 64u + 16u <= a.bytes);
+            st.v[4 + j] = ld16(okb ? a.base + addr + 64u : zero, false);
+        }
+    }
+}
+
+// The stores of one tile, all unconditional (see above): K = 6 slab stores (tiled
+// records) + 3 filter outputs. Record stores are always non-temporal here (a runtime
+// choice of policy would be a branch, and a path that skips both stores).
+template <bool NT>
+__device__ __forceinline__ void st_b128(const __amdgpu_buffer_rsrc_t& r, uint32_t off, uint4 v) {
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, NT ? 2 : 0);
+}
+
+template <int REC, bool FILTER>
+__device__ __forceinline__ void pad_stores() {   // the prologue's stand-ins for a tile's stores
+    const auto r = rsrc_of(g_zero16, 0u);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    // distinct offsets, or the compiler merges them (the range is empty: all are dropped)
+    if (REC == kRecTiled)
+#pragma unroll
+        for (int k = 0; k < BT_REC_SLABS; ++k) __builtin_amdgcn_raw_buffer_store_b128(z, r, 16 * k, 0, 0);
+    if (FILTER)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, r, 256 + 16 * k, 0, 0);
+}
+
+template <int REC, bool FILTER, int DW>
+__global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevProgram prog) {
+    static_assert(REC == kRecTiled || REC == kRecNone, "pipe variant: tiled records or none");
+    constexpr uint32_t kRow = kRowDwords;
+    __shared__ uint32_t lds_all[kWavesPerBlock * kWave * kRow + 32];   // + tail pad for over-reads
+    extern __shared__ uint4 dyn_lds[];   // PAYLOAD DFA pool (a.dfa_bytes), else empty
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
+    uint32_t* img = lds_all + wid * (kWave * kRow);
+    const uint32_t* row = img + lane * kRow;
+    if (FILTER && a.dfa_bytes) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
+        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
+        __syncthreads();
+    }
+    const uint8_t* dfa_lds = reinterpret_cast<const uint8_t*>(dyn_lds);
+
+    const uint32_t total_waves = gridDim.x * kWavesPerBlock;
+    const uint32_t gw = blockIdx.x * kWavesPerBlock + wid;
+    uint32_t t, t_end, step;
+    if (a.blocked) {
+        const uint32_t per = (a.ntiles + total_waves - 1) / total_waves;
+        t = gw * per;
+        t_end = min(a.ntiles, t + per);
+        step = 1;
+    } else {
+        t = gw;
+        t_end = a.ntiles;
+        step = total_waves;
+    }
+    if (t >= t_end) return;   // wave-uniform; no block barrier follows
+    const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
+    bool wide = false;
+
+    // prologue: descriptors of t and t + step, round A of t (waited), then stand-ins for
+    // a tile's stores so the first iteration's waits count like every later one's
+    Stage<-1> st;
+    uint32_t dn[DW + 1];
+    load_desc_pipe<DW>(a, t, true, lane, dn);
+    issue_round_a_pipe<DW>(a, t, true, lane, dn, st, wide, need_max);
+    load_desc_pipe<DW>(a, t + step, t + step < t_end, lane, dn);
+    pad_stores<REC, FILTER>();
+    stage_to_lds<-1>(st, img, lane);
+    wave_lds_sync();
+
+    for (;;) {
+        const uint32_t p0 = t * 64u;
+        const uint32_t my = p0 + lane;
+        const bool live = my < a.n;
+        const uint64_t my_off = st.off;
+        const uint32_t my_len = st.len;
+        uint64_t qa0[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qa0[j] = st.qa0[j];
+        const bool this_wide = st.wide;
+        const uint32_t s = (uint32_t)my_off & 15u;
+        uint32_t w0[10];
+        window<10>(row, s, w0);
+        if (REC != kRecNone) {   // round B (same as bt_parse_filter_main), before the next tile's loads
+            const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s, my_len, need_max)
+                                             : min(64u, s + my_len);
+            const bool cov = a_end >= s + min(my_len, 28u);
+            const uint32_t end = !live ? 0u
+                               : cov ? s + header_end(w0, my_len, kNeedFilter)
+                                     : s + min(my_len, need_max);
+            const uint32_t lo = (a_end + 15u) >> 4;
+            const bool my_nb = end > 16u * lo;
+            if (__ballot(my_nb) != 0ull) {
+                const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
+                load_round_b<-1>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
+                wave_lds_sync();
+                window<10>(row, s, w0);
+            }
+            wide = __popcll(__ballot(end > 64u)) > 32;
+            if (a.nt & 12u) wide = (a.nt & 8u) != 0u;
+        }
+
+        // next tile: round A from the descriptors loaded one tile ago, then the
+        // descriptors of the tile after it
+        const uint32_t tn = t + step;
+        const bool more = tn < t_end;
+        issue_round_a_pipe<DW>(a, tn, more, lane, dn, st, wide, need_max);
+        load_desc_pipe<DW>(a, tn + step, more && tn + step < t_end, lane, dn);
+
+        // ---- PARSE + tiled record stores ----
+        const uint32_t len = live ? my_len : 0u;
+        if (REC == kRecTiled) {
+            Parsed p;
+            uint32_t ns = parse_packet<true>(row, s, len, w0, p);
+            if (!live) {   // the last tile's unused slots: zero slabs 0-1 (a 2-slab record)
+                ns = 2u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) p.r[k] = 0u;
+            }
+            const auto r = rsrc_of(a.records + (uint64_t)t * (BT_REC_SLABS * 64 * 16), BT_REC_SLABS * 64 * 16);
+            const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+            for (uint32_t k = 0; k < BT_REC_SLABS; ++k) {
+                const uint64_t mk = __ballot(k < ns);
+                const uint32_t off = k < 2u ? (k * 64u + lane) * 16u
+                                   : k < ns ? (k * 64u + (uint32_t)__popcll(mk & below)) * 16u : kOob;
+                st_b128<true>(r, off, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]));
+            }
+        }
+
+        // ---- FILTER ----
+        if (FILTER) {
+            FilterIn x;
+            x.gate = len >= 34 && be16_of(w0, 12) == 0x0800u;
+            x.proto = byte_of(w0, 23);
+            x.src = be32_of(w0, 26);
+            x.dst = be32_of(w0, 30);
+            x.sport = be16_of(w0, 34);
+            x.dport = be16_of(w0, 36);
+            x.l4_ok = (x.proto == 6 && len >= 54) || (x.proto == 17 && len >= 42);
+            uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
+            bool open = live;
+            uint32_t staged_sh = ~0u;
+            for (uint32_t f = 0; f < prog.n; ++f) {
+                if (__ballot(open) == 0ull) break;
+                uint32_t rr;
+                if (prog.f[f].kind == BT_K_PAYLOAD)
+                    rr = a.prefixes ? 3u
+                       : open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0, staged_sh)
+                              : 0u;
+                else
+                    rr = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
+                if (open && rr != 1u) {
+                    code = rr == 0u ? BT_DECIDE_REJECT : rr == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+                    slot = f;
+                    open = false;
+                }
+            }
+            const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
+            const uint32_t cnt = min(64u, a.n - p0);
+            const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
+            const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict ? 8u : 0u);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
+            const auto rt = rsrc_of(a.tile_pass ? a.tile_pass + t : nullptr, a.tile_pass ? 4u : 0u);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)__popcll(pass), rt, lane == 0 ? 0 : (int)kOob, 0, 0);
+        }
+
+        wave_lds_sync();   // this tile's LDS reads are done
+        if (!more) break;
+        stage_to_lds<-1>(st, img, lane);
+        wave_lds_sync();
+        t = tn;
+    }
+}
+
 // ---- ordered compaction of passing packet indices ---------------------------------
 // K2: chunk_sums[c] = sum of tile_pass over chunk c (kChunkTiles = 256 tiles, one per
 // thread).
@@ -815,21 +1075,24 @@ int cu_count() {
 }
 
 // One residency wave of blocks: the persistent grid-stride loop then has no tail of
-// late blocks (measured: 2x residency cost C3 11 %).
-template <class K>
-int resident_grid(K kernel, uint32_t dyn) {
-    static int blocks = 0;   // per kernel instantiation, no dynamic LDS
+// late blocks (measured: 2x residency cost C3 11 %). Cached per kernel instantiation
+// (the template argument), and for PAYLOAD programs per dynamic-LDS size.
+template <auto Kernel>
+int resident_grid(uint32_t dyn) {
+    static int blocks = 0;
+    static uint32_t last_dyn = ~0u;
+    static int last_blocks = 0;
+    static std::mutex mu;
     auto query = [&](uint32_t bytes) {
         int dev = 0, per_cu = 0;
         hipDeviceProp_t prop;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, bytes) != hipSuccess || per_cu < 1)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, Kernel, kBlock, bytes) != hipSuccess || per_cu < 1)
             return 1024;
         return prop.multiProcessorCount * per_cu;
     };
+    std::lock_guard<std::mutex> lk(mu);
     if (dyn) {   // a PAYLOAD program: occupancy depends on its DFA pool size
-        static uint32_t last_dyn = 0;
-        static int last_blocks = 0;
         if (dyn != last_dyn) {
             last_blocks = query(dyn);
             last_dyn = dyn;
@@ -840,12 +1103,23 @@ int resident_grid(K kernel, uint32_t dyn) {
     return blocks;
 }
 
+// The counted-wait pipeline (bt_parse_filter_pipe) serves descriptor mode with tiled
+// records or none; BT_NO_PIPE=1 in the environment selects bt_parse_filter_main
+// instead (A/B).
+bool use_pipe() {
+    static const bool on = [] {
+        const char* e = getenv("BT_NO_PIPE");
+        return !(e && *e && *e != '0');
+    }();
+    return on;
+}
+
 template <int FL, int REC, bool F>
 void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st) {
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    auto go = [&](auto kernel) {
-        const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
-        int g = grid > 0 ? grid : resident_grid(kernel, dyn);
+    const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
+    auto go = [&](auto kernel, int resident) {
+        int g = grid > 0 ? grid : resident;
         // Fixed stride: two blocks (8 waves) per CU. C2 measured 0.416 ms at the
         // residency (7 blocks/CU), 0.403 at 3, 0.387 at 2, 0.56 at 1 (4 processes each):
         // fewer concurrent read and write streams suit HBM better here.
@@ -853,8 +1127,17 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
         hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
     };
-    if (pf) go(bt_parse_filter_main<FL, REC, F, true>);
-    else go(bt_parse_filter_main<FL, REC, F, false>);
+    if constexpr (FL < 0 && (REC == kRecTiled || REC == kRecNone)) {
+        if (pf && a.desc && (a.nt & 1u) && use_pipe()) {
+            if (a.desc_words == 1)
+                go(bt_parse_filter_pipe<REC, F, 1>, grid > 0 ? 0 : resident_grid<bt_parse_filter_pipe<REC, F, 1>>(dyn));
+            else
+                go(bt_parse_filter_pipe<REC, F, 2>, grid > 0 ? 0 : resident_grid<bt_parse_filter_pipe<REC, F, 2>>(dyn));
+            return;
+        }
+    }
+    if (pf) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
+    else go(bt_parse_filter_main<FL, REC, F, false>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn));
 }
 
 template <int FL>

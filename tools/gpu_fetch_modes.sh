@@ -11,7 +11,7 @@ fl = sys.argv[1]
 per = {}
 for f in glob.glob(f"gpurun_out/fm_fetch_{fl}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "parse_filter_main" in r.get("Kernel_Name", "") and r.get("Counter_Name") == "FETCH_SIZE":
+        if "parse_filter_" in r.get("Kernel_Name", "") and r.get("Counter_Name") == "FETCH_SIZE":
             k = (f, r.get("Dispatch_Id"))
             per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
 vals = sorted(per.values())

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of bt_parse_filter_main from rocprofv3 PMC passes.
+"""Per-launch HBM traffic of the main kernel (bt_parse_filter_main / _pipe) from rocprofv3 PMC passes.
 
     python tools/pmc_traffic.py --fetch DIR_FETCH --write DIR_WRITE --config c2 \
         [--out profiles/traffic.json]
@@ -17,7 +17,7 @@ import glob
 import json
 import os
 
-KERNEL = "bt_parse_filter_main"
+KERNEL = "bt_parse_filter_"   # bt_parse_filter_main (fixed stride) or bt_parse_filter_pipe (descriptors)
 
 
 def per_dispatch(d, counter):
