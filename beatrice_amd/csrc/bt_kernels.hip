@@ -94,20 +94,22 @@ struct Parsed {
 __device__ __forceinline__ uint32_t detect_word(const uint32_t* w0, uint32_t len) {
     const uint32_t et = be16_of(w0, 12), b0 = byte_of(w0, 0), pr = byte_of(w0, 23);
     const uint32_t ports = be16_of(w0, 34) | (be16_of(w0, 36) << 16);
-    const bool eth = len >= 14 && (et == 0x0800u || et == 0x86DDu || et == 0x0806u);
+    // bitwise & / | throughout: short-circuit forms became exec-mask branches
+    const bool eth = (len >= 14) & ((et == 0x0800u) | (et == 0x86DDu) | (et == 0x0806u));
     const bool l34 = len >= 34;
-    uint32_t code = len < 14 ? BT_DET_UNKNOWN : eth ? BT_DET_ETHERNET : BT_DET_NONE;
-    if (eth && l34) code = pr == 6 ? BT_DET_TCP : pr == 17 ? BT_DET_UDP : pr == 1 ? BT_DET_ICMP : code;
-    const bool v4 = l34 && (b0 >> 4) == 4u;
-    const bool tcp = v4 && pr == 6, udp = v4 && pr == 17;
-    const bool p80 = (ports & 0xFFFFu) == 80u || (ports >> 16) == 80u;
-    const bool p53 = (ports & 0xFFFFu) == 53u || (ports >> 16) == 53u;
+    const uint32_t code0 = len < 14 ? BT_DET_UNKNOWN : eth ? BT_DET_ETHERNET : BT_DET_NONE;
+    const uint32_t l4code = pr == 6 ? BT_DET_TCP : pr == 17 ? BT_DET_UDP : pr == 1 ? BT_DET_ICMP : 0u;
+    const uint32_t code = (eth & l34 & (l4code != 0u)) ? l4code : code0;
+    const bool v4 = l34 & ((b0 >> 4) == 4u);
+    const bool tcp = v4 & (pr == 6), udp = v4 & (pr == 17);
+    const bool p80 = ((ports & 0xFFFFu) == 80u) | ((ports >> 16) == 80u);
+    const bool p53 = ((ports & 0xFFFFu) == 53u) | ((ports >> 16) == 53u);
     const uint32_t is = (eth ? BT_IS_ETHERNET : 0u) | (v4 ? BT_IS_IPV4 : 0u) |
-                        (len >= 54 && (b0 >> 4) == 6u ? BT_IS_IPV6 : 0u) | (tcp ? BT_IS_TCP : 0u) |
-                        (udp ? BT_IS_UDP : 0u) | (v4 && pr == 1 ? BT_IS_ICMP : 0u) |
-                        (tcp && len >= 54 && p80 ? BT_IS_HTTP : 0u) | (udp && len >= 42 && p53 ? BT_IS_DNS : 0u);
-    const uint32_t is2 = (len >= 28 && et == 0x0806u ? BT_IS2_ARP : 0u) | (l34 && pr == 6 ? BT_IS2_MULTI_TCP : 0u) |
-                         (l34 && pr == 17 ? BT_IS2_MULTI_UDP : 0u);
+                        (((len >= 54) & ((b0 >> 4) == 6u)) ? BT_IS_IPV6 : 0u) | (tcp ? BT_IS_TCP : 0u) |
+                        (udp ? BT_IS_UDP : 0u) | ((v4 & (pr == 1)) ? BT_IS_ICMP : 0u) |
+                        ((tcp & (len >= 54) & p80) ? BT_IS_HTTP : 0u) | ((udp & (len >= 42) & p53) ? BT_IS_DNS : 0u);
+    const uint32_t is2 = (((len >= 28) & (et == 0x0806u)) ? BT_IS2_ARP : 0u) |
+                         ((l34 & (pr == 6)) ? BT_IS2_MULTI_TCP : 0u) | ((l34 & (pr == 17)) ? BT_IS2_MULTI_UDP : 0u);
     return code | (is << 8) | (is2 << 16);
 }
 
@@ -159,9 +161,9 @@ __device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s
     const uint32_t b0 = byte_of(w3, 0);
     const uint32_t proto = byte_of(w3, 9), nh = byte_of(w3, 6);
     uint32_t o4 = is4 ? o3 + 4u * (b0 & 0x0Fu) : o3 + 40u;
-    uint32_t l4 = 0;
-    if (v4ok && o4 <= len) l4 = proto == 6 ? BT_L_TCP : proto == 17 ? BT_L_UDP : proto == 1 ? BT_L_ICMP : 0u;
-    if (v6ok) l4 = nh == 6 ? BT_L_TCP : nh == 17 ? BT_L_UDP : 0u;
+    const uint32_t l4v4 = proto == 6 ? BT_L_TCP : proto == 17 ? BT_L_UDP : proto == 1 ? BT_L_ICMP : 0u;
+    const uint32_t l4v6 = nh == 6 ? BT_L_TCP : nh == 17 ? BT_L_UDP : 0u;
+    const uint32_t l4 = v6ok ? l4v6 : (v4ok & (o4 <= len)) ? l4v4 : 0u;
 
     // L4 fields (bt_rec dwords 17..21): TCP :194-209, UDP :211-221, ICMP :223-234
     uint32_t w4[5];
@@ -511,13 +513,14 @@ __device__ __forceinline__ void stage_to_lds(const Stage<FIXED_LOG2>& st, uint32
 // (everything it looks at — EtherTypes at 12/16/20, IHL at L3+0 — sits below byte 49).
 // `w0` = the packet's first 40 bytes (window<10> at its start); only bytes < 28 are used.
 __device__ __forceinline__ uint32_t header_end(const uint32_t* w0, uint32_t len, uint32_t floor_) {
+    // branch-free: the walk's tag / EtherType / IHL choice as selects
     const uint32_t et0 = be16_of(w0, 12), et1 = be16_of(w0, 16), et2 = be16_of(w0, 20);
-    uint32_t o3 = 14, et = et0;
-    if (is_vlan(et0)) { o3 = 18; et = et1; if (is_vlan(et1)) { o3 = 22; et = et2; } }
-    const uint32_t ihl = (o3 == 14u ? byte_of(w0, 14) : o3 == 18u ? byte_of(w0, 18) : byte_of(w0, 22)) & 0x0Fu;
-    uint32_t end = o3;
-    if (et == 0x0800u) end = o3 + 20u + (ihl > 5 ? 4u * ihl - 20u : 0u) + 20u;
-    else if (et == 0x86DDu) end = o3 + 60u;
+    const bool t0 = is_vlan(et0), t1 = t0 & is_vlan(et1);
+    const uint32_t o3 = 14u + (t0 ? 4u : 0u) + (t1 ? 4u : 0u);
+    const uint32_t et = t1 ? et2 : t0 ? et1 : et0;
+    const uint32_t ihl = (t1 ? byte_of(w0, 22) : t0 ? byte_of(w0, 18) : byte_of(w0, 14)) & 0x0Fu;
+    const uint32_t v4end = o3 + 40u + (ihl > 5u ? 4u * ihl - 20u : 0u);
+    uint32_t end = et == 0x0800u ? v4end : et == 0x86DDu ? o3 + 60u : o3;
     end = end > floor_ ? end : floor_;
     return end < len ? end : len;
 }
@@ -799,12 +802,13 @@ __device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t t
         const uint64_t addr = a0 + 16u * c;
         const uint32_t sq = (uint32_t)qo & 15u;
         st.qa0[j] = a0;
-        const bool live_q = valid && p0 + q < a.n;
+        // a packet that is not live has off = len = 0, so a_end = 0 and nothing is read;
+        // bitwise & keeps the conditions branch-free (&& made exec-mask branches)
         const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
-        const bool ok = live_q && (16u * c < a_end) && (addr + 16u <= a.bytes);
+        const bool ok = (16u * c < a_end) & (addr + 16u <= a.bytes);
         st.v[j] = ld16(ok ? a.base + addr : zero, ntl);
         if (wide) {
-            const bool okb = live_q && (16u * (c + 4u) < a_end) && (addr + 64u + 16u <= a.bytes);
+            const bool okb = (16u * (c + 4u) < a_end) & (addr + 64u + 16u <= a.bytes);
             st.v[4 + j] = ld16(okb ? a.base + addr + 64u : zero, false);
         }
     }
