@@ -271,14 +271,15 @@ __device__ __forceinline__ uint32_t eval_slot(uint32_t kind, uint32_t a, uint32_
     case BT_K_TRUE: return 1;
     case BT_K_FALSE: return 0;
     case BT_K_BPF:
-        return x.gate && (((a & 1u) && x.proto == 6) || ((a & 2u) && x.proto == 17) || ((a & 4u) && x.proto == 1));
-    case BT_K_PROTO_EQ: return x.gate && x.proto == a;
-    case BT_K_PROTO_NZ: return x.gate && x.proto != 0;
-    case BT_K_IP_MASK: return x.gate && (((x.src & b) == a) || ((x.dst & b) == a));
+        return x.gate & ((((a & 1u) != 0u) & (x.proto == 6)) | (((a & 2u) != 0u) & (x.proto == 17)) |
+                         (((a & 4u) != 0u) & (x.proto == 1)));
+    case BT_K_PROTO_EQ: return x.gate & (x.proto == a);
+    case BT_K_PROTO_NZ: return x.gate & (x.proto != 0);
+    case BT_K_IP_MASK: return x.gate & (((x.src & b) == a) | ((x.dst & b) == a));
     case BT_K_PORT:
-        return x.gate && x.l4_ok && ((x.sport >= a && x.sport <= b) || (x.dport >= a && x.dport <= b));
+        return x.gate & x.l4_ok & (((x.sport >= a) & (x.sport <= b)) | ((x.dport >= a) & (x.dport <= b)));
     case BT_K_IP_THROW: return x.gate ? 2u : 0u;
-    case BT_K_PORT_THROW: return (x.gate && x.l4_ok) ? 2u : 0u;
+    case BT_K_PORT_THROW: return (x.gate & x.l4_ok) ? 2u : 0u;
     default: return 3;   // BT_K_HOST
     }
 }
@@ -693,13 +694,13 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
             FilterIn x;
-            x.gate = len >= 34 && be16_of(w0, 12) == 0x0800u;
+            x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
             x.proto = byte_of(w0, 23);
             x.src = be32_of(w0, 26);
             x.dst = be32_of(w0, 30);
             x.sport = be16_of(w0, 34);
             x.dport = be16_of(w0, 36);
-            x.l4_ok = (x.proto == 6 && len >= 54) || (x.proto == 17 && len >= 42);
+            x.l4_ok = ((x.proto == 6) & (len >= 54)) | ((x.proto == 17) & (len >= 42));
             uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
             bool open = live;
             uint32_t staged_sh = ~0u;   // payload window not staged yet
@@ -944,13 +945,13 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             FilterIn x;
-            x.gate = len >= 34 && be16_of(w0, 12) == 0x0800u;
+            x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
             x.proto = byte_of(w0, 23);
             x.src = be32_of(w0, 26);
             x.dst = be32_of(w0, 30);
             x.sport = be16_of(w0, 34);
             x.dport = be16_of(w0, 36);
-            x.l4_ok = (x.proto == 6 && len >= 54) || (x.proto == 17 && len >= 42);
+            x.l4_ok = ((x.proto == 6) & (len >= 54)) | ((x.proto == 17) & (len >= 42));
             uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
             bool open = live;
             uint32_t staged_sh = ~0u;

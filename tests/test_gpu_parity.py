@@ -288,3 +288,45 @@ def test_record_layouts(cap, layout):
                 compare_decisions(out["decide"], g["code__c3"], g["src__c3"], filters, where=f"{cap}/{layout}")
     finally:
         ctx.close()
+
+
+# Every form of the main kernel launch_main can pick, on one ragged capture: the
+# counted-wait pipeline (default in descriptor mode; a deep per-wave loop with 4 waves;
+# blocked tile order; forced wide / two-round loads) and bt_parse_filter_main (no
+# prefetch; default cache policy). Parse+filter, parse-only and filter-only, at batch
+# sizes 1, 63, 65 and 20,037 (not a multiple of the 64-packet tile).
+KERNEL_FORMS = {
+    "pipe": dict(flags=0),
+    "pipe_4_waves": dict(flags=0, grid_waves=4),
+    "pipe_blocked": dict(flags=abi.OPT_TILE_BLOCKED, grid_waves=64),
+    "pipe_wide_always": dict(flags=abi.OPT_WIDE_ALWAYS),
+    "pipe_wide_never": dict(flags=abi.OPT_WIDE_NEVER),
+    "main_no_prefetch": dict(flags=abi.OPT_NO_PREFETCH),
+    "main_cache_default": dict(flags=abi.OPT_CACHE_DEFAULT, grid_waves=8),
+}
+
+
+@pytest.mark.parametrize("form", list(KERNEL_FORMS))
+def test_kernel_forms_agree(form):
+    data, desc = synth.capture(synth.FUZZ, 20037, seed=11)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    ctx = abi.Context(0, **KERNEL_FORMS[form])
+    try:
+        ctx.compile(filters)
+        for n in (1, 63, 65, len(desc)):
+            d = np.ascontiguousarray(desc[:n])
+            rec, dec, npass = ol.oracle_run(data, d, n, filters)
+            out = run_dev(ctx, data, d, n)
+            assert np.array_equal(out["records"], rec), f"{form} n={n}: records"
+            assert np.array_equal(out["decide"], dec), f"{form} n={n}: decisions"
+            assert out["n_pass"] == npass
+            check_filter_outputs(out, n)
+            out = run_dev(ctx, data, d, n, filt=False)
+            assert np.array_equal(out["records"], rec), f"{form} n={n}: parse-only records"
+            out = run_dev(ctx, data, d, n, records=False)
+            assert np.array_equal(out["decide"], dec), f"{form} n={n}: filter-only decisions"
+            check_filter_outputs(out, n)
+    finally:
+        ctx.close()
