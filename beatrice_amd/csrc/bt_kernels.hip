@@ -751,59 +751,78 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-// This lane's descriptor of tile t (0 past n or when !valid): one buffer load either way.
-// DW = descriptor words (1 bt_pkt_desc, 2 xdp_desc), a template argument so that no
-// register is written on one format's path and loaded on the other's.
+// The descriptors of tile t as the wave needs them: `me` = this lane's packet (the
+// parse), q[j] = packet j*16 + lane/4 (round A: four lanes per packet). Both are buffer
+// loads of the same 512-B tile slice (the q loads hit the lines the `me` load brings
+// in), zero past n or when !valid; loading q directly replaces three ds_bpermute
+// shuffles per round-A instruction. DW = descriptor words (1 bt_pkt_desc, 2 xdp_desc), a
+// template argument so that no register is written on one format's path and loaded on
+// the other's.
+template <int DW>
+struct TileDesc {
+    uint32_t me[DW + 1];
+    uint32_t q[4][DW + 1];
+};
+
 template <int DW>
 __device__ __forceinline__ void load_desc_pipe(const MainArgs& a, uint32_t t, bool valid, uint32_t lane,
-                                               uint32_t (&dw)[DW + 1]) {
+                                               TileDesc<DW>& d) {
     const uint32_t p0 = t * 64u;
     const uint32_t cnt = valid && p0 < a.n ? min(64u, a.n - p0) : 0u;
+    const auto r = rsrc_of(a.desc + (valid ? (uint64_t)DW * p0 : 0ull), cnt * 8u * DW);
+    const uint32_t qoff = (lane >> 2) * 8u * DW;
     if constexpr (DW == 1) {
-        const auto r = rsrc_of(a.desc + (valid ? p0 : 0u), cnt * 8u);
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, 0);
-        dw[0] = v.x; dw[1] = v.y;
+        d.me[0] = v.x; d.me[1] = v.y;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(qoff + j * 128u), 0, 0);
+            d.q[j][0] = w.x; d.q[j][1] = w.y;
+        }
     } else {
-        const auto r = rsrc_of(a.desc + (valid ? 2ull * p0 : 0ull), cnt * 16u);
         typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
         const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(lane * 16u), 0, 0);
-        dw[0] = v.x; dw[1] = v.y; dw[2] = v.z;
+        d.me[0] = v.x; d.me[1] = v.y; d.me[2] = v.z;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(qoff + j * 256u), 0, 0);
+            d.q[j][0] = w.x; d.q[j][1] = w.y; d.q[j][2] = w.z;
+        }
     }
 }
 
-// Round A of tile t from descriptor words already in registers (issue_loads' loads,
-// with the zero line standing in for the skipped ones).
 template <int DW>
-__device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t t, bool valid, uint32_t lane,
-                                                   const uint32_t (&dw)[DW + 1], Stage<-1>& st, bool wide,
-                                                   uint32_t need_max) {
-    const uint32_t p0 = t * 64u;
-    const bool live = valid && p0 + lane < a.n;
-    if constexpr (DW == 1) {
-        st.off = ((uint64_t)(dw[1] & 0xFFFFu) << 32) | dw[0];
-        st.len = dw[1] >> 16;
-    } else {
-        st.off = ((uint64_t)dw[1] << 32) | dw[0];
-        st.len = dw[DW] > 0xFFFFu ? 0xFFFFu : dw[DW];
+__device__ __forceinline__ void decode_desc(const uint32_t (&w)[DW + 1], uint64_t& off, uint32_t& len) {
+    if constexpr (DW == 1) {   // bt_pkt_desc: off in bits 0..47, len in 48..63
+        off = ((uint64_t)(w[1] & 0xFFFFu) << 32) | w[0];
+        len = w[1] >> 16;
+    } else {                   // xdp_desc {u64 addr; u32 len; u32 options}
+        off = ((uint64_t)w[1] << 32) | w[0];
+        len = w[2] > 0xFFFFu ? 0xFFFFu : w[2];
     }
-    if (!live) { st.off = 0; st.len = 0; }
-    const uint32_t off_lo = (uint32_t)st.off, off_hi = (uint32_t)(st.off >> 32);
+}
+
+// Round A of tile t from descriptors already in registers (issue_loads' loads, with the
+// zero line standing in for the skipped ones). A packet past n has an all-zero
+// descriptor: off = len = 0, so nothing of it is read.
+template <int DW>
+__device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t lane, const TileDesc<DW>& d,
+                                                   Stage<-1>& st, bool wide, uint32_t need_max) {
+    decode_desc<DW>(d.me, st.off, st.len);
     const uint32_t c = lane & 3u;
     st.wide = wide;
     const bool ntl = (a.nt & 2u) && !wide;
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t q = j * 16u + (lane >> 2);
-        const uint64_t qo = ((uint64_t)(uint32_t)__shfl((int)off_hi, (int)q) << 32) |
-                            (uint32_t)__shfl((int)off_lo, (int)q);
-        const uint32_t ql = (uint32_t)__shfl((int)st.len, (int)q);
+        uint64_t qo;
+        uint32_t ql;
+        decode_desc<DW>(d.q[j], qo, ql);
         const uint64_t a0 = qo & ~15ull;
         const uint64_t addr = a0 + 16u * c;
         const uint32_t sq = (uint32_t)qo & 15u;
         st.qa0[j] = a0;
-        // a packet that is not live has off = len = 0, so a_end = 0 and nothing is read;
         // bitwise & keeps the conditions branch-free (&& made exec-mask branches)
         const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
         const bool ok = (16u * c < a_end) & (addr + 16u <= a.bytes);
@@ -874,9 +893,9 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     // prologue: descriptors of t and t + step, round A of t (waited), then stand-ins for
     // a tile's stores so the first iteration's waits count like every later one's
     Stage<-1> st;
-    uint32_t dn[DW + 1];
+    TileDesc<DW> dn;
     load_desc_pipe<DW>(a, t, true, lane, dn);
-    issue_round_a_pipe<DW>(a, t, true, lane, dn, st, wide, need_max);
+    issue_round_a_pipe<DW>(a, lane, dn, st, wide, need_max);
     load_desc_pipe<DW>(a, t + step, t + step < t_end, lane, dn);
     pad_stores<REC, FILTER>();
     stage_to_lds<-1>(st, img, lane);
@@ -918,7 +937,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // descriptors of the tile after it
         const uint32_t tn = t + step;
         const bool more = tn < t_end;
-        issue_round_a_pipe<DW>(a, tn, more, lane, dn, st, wide, need_max);
+        issue_round_a_pipe<DW>(a, lane, dn, st, wide, need_max);
         load_desc_pipe<DW>(a, tn + step, more && tn + step < t_end, lane, dn);
 
         // ---- PARSE + tiled record stores ----
