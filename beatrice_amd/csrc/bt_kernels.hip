@@ -379,6 +379,42 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
     return endacc[q];
 }
 
+// The compiled PacketFilter program on this lane's packet: the reference's AND chain in
+// priority order with early exit (src/PacketFilter.cpp:57-119), wave-uniform slot by slot
+// until every lane has decided. Returns the decision code (BT_DECIDE_*) and the deciding
+// slot. `lrow` = the lane's LDS row, reused to stage a PAYLOAD window after the parse.
+__device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const uint8_t* dfa_lds,
+                                                  uint32_t* lrow, uint64_t my_off, uint32_t len,
+                                                  const uint32_t* w0, bool live, uint32_t& slot) {
+    FilterIn x;
+    x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
+    x.proto = byte_of(w0, 23);
+    x.src = be32_of(w0, 26);
+    x.dst = be32_of(w0, 30);
+    x.sport = be16_of(w0, 34);
+    x.dport = be16_of(w0, 36);
+    x.l4_ok = ((x.proto == 6) & (len >= 54)) | ((x.proto == 17) & (len >= 42));
+    uint32_t code = BT_DECIDE_PASS;
+    slot = prog.n ? prog.n - 1u : 0u;
+    bool open = live;
+    uint32_t staged_sh = ~0u;   // payload window not staged yet
+    for (uint32_t f = 0; f < prog.n; ++f) {
+        if (__ballot(open) == 0ull) break;
+        uint32_t r;
+        if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
+            r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
+              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh) : 0u;
+        else
+            r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
+        if (open && r != 1u) {
+            code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+            slot = f;
+            open = false;
+        }
+    }
+    return code;
+}
+
 // Header windows of one 64-packet tile in flight in registers (LOAD stage).
 //  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
 //  descriptors:  round A = the first 64 B (chunks 0..3) of every packet's 16-B-aligned
@@ -558,6 +594,35 @@ __device__ __forceinline__ void load_round_b(const MainArgs& a, uint32_t t, uint
     }
 }
 
+// Descriptor mode after round A: where this lane's walked headers end (header_end, with
+// a floor of 38 B for the PacketFilter gates and the detector column), round B for the
+// chunks round A did not read (wave-uniform: only if some lane needs it; then the row
+// and `w0` are refreshed), and the wave's load mode for its next tile (wide when most
+// packets needed more than 64 B; nt bits 2/3 force it, A/B). Returns that mode.
+__device__ __forceinline__ bool round_b(const MainArgs& a, uint32_t t, uint32_t lane, const uint64_t* qa0,
+                                       uint32_t* img, const uint32_t* row, uint32_t s, uint64_t my_off,
+                                       uint32_t my_len, bool live, bool this_wide, uint32_t need_max,
+                                       uint32_t* w0) {
+    // bytes from a0 that round A read, and whether they hold what header_end reads
+    const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s, my_len, need_max)
+                                     : min(64u, s + my_len);
+    const bool cov = a_end >= s + min(my_len, 28u);
+    const uint32_t end = !live ? 0u
+                       : cov ? s + header_end(w0, my_len, kNeedFilter)
+                             : s + min(my_len, need_max);
+    const uint32_t lo = (a_end + 15u) >> 4;   // first chunk round A did not read
+    const bool my_nb = end > 16u * lo;
+    if (__ballot(my_nb) != 0ull) {
+        const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
+        load_round_b<-1>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
+        wave_lds_sync();
+        window<10>(row, s, w0);
+    }
+    bool wide = __popcll(__ballot(end > 64u)) > 32;
+    if (a.nt & 12u) wide = (a.nt & 8u) != 0u;
+    return wide;
+}
+
 template <int FIXED_LOG2, int REC, bool FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
@@ -617,28 +682,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         uint32_t w0[10];
         window<10>(row, s, w0);
         if constexpr (FIXED_LOG2 < 0) {
-            if (REC != kRecNone) {   // filter-only needs <= 38 B: round A always suffices
-                const uint32_t s0 = s;
-                // bytes from a0 that round A read, and whether they hold what header_end reads;
-                // the floor of 38 B covers the PacketFilter gates and the detector column
-                const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s0, my_len, need_max)
-                                                 : min(64u, s0 + my_len);
-                const bool cov = a_end >= s0 + min(my_len, 28u);
-                const uint32_t end = !live ? 0u
-                                   : cov ? s0 + header_end(w0, my_len, kNeedFilter)
-                                         : s0 + min(my_len, need_max);
-                const uint32_t lo = (a_end + 15u) >> 4;   // first chunk round A did not read
-                const bool my_nb = end > 16u * lo;
-                const uint64_t needs_b = __ballot(my_nb);
-                if (needs_b != 0ull) {
-                    const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
-                    load_round_b<FIXED_LOG2>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
-                    wave_lds_sync();
-                    window<10>(row, s, w0);
-                }
-                wide = __popcll(__ballot(end > 64u)) > 32;   // decides the wave's next issue
-                if (a.nt & 12u) wide = (a.nt & 8u) != 0u;   // A/B knobs
-            }
+            if (REC != kRecNone)   // filter-only needs <= 38 B: round A always suffices
+                wide = round_b(a, t, lane, qa0, img, row, s, my_off, my_len, live, this_wide, need_max, w0);
         }
 
         // ---- 2. PARSE -------------------------------------------------------
@@ -693,33 +738,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
-            FilterIn x;
-            x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
-            x.proto = byte_of(w0, 23);
-            x.src = be32_of(w0, 26);
-            x.dst = be32_of(w0, 30);
-            x.sport = be16_of(w0, 34);
-            x.dport = be16_of(w0, 36);
-            x.l4_ok = ((x.proto == 6) & (len >= 54)) | ((x.proto == 17) & (len >= 42));
-            uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
-            bool open = live;
-            uint32_t staged_sh = ~0u;   // payload window not staged yet
-            for (uint32_t f = 0; f < prog.n; ++f) {
-                if (__ballot(open) == 0ull) break;
-                uint32_t r;
-                if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
-                    r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
-                      : open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0,
-                                            staged_sh)
-                             : 0u;
-                else
-                    r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
-                if (open && r != 1u) {
-                    code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
-                    slot = f;
-                    open = false;
-                }
-            }
+            uint32_t slot;
+            const uint32_t code = filter_packet(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
             if (lane == 0) {
@@ -856,6 +876,10 @@ __device__ __forceinline__ void pad_stores() {   // the prologue's stand-ins for
         for (int k = 0; k < 3; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, r, 256 + 16 * k, 0, 0);
 }
 
+// Descriptor mode only. A fixed-stride form (contiguous 1-KiB loads, prefetched) was
+// measured slower on C2 (0.369 against 0.340 ms for bt_parse_filter_main without
+// prefetch, at 1-4 blocks/CU): there, a wave's loads in flight during its record stores
+// cost more HBM efficiency than the hidden latency gains.
 template <int REC, bool FILTER, int DW>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevProgram prog) {
     static_assert(REC == kRecTiled || REC == kRecNone, "pipe variant: tiled records or none");
@@ -907,31 +931,11 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         const bool live = my < a.n;
         const uint64_t my_off = st.off;
         const uint32_t my_len = st.len;
-        uint64_t qa0[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) qa0[j] = st.qa0[j];
-        const bool this_wide = st.wide;
         const uint32_t s = (uint32_t)my_off & 15u;
         uint32_t w0[10];
         window<10>(row, s, w0);
-        if (REC != kRecNone) {   // round B (same as bt_parse_filter_main), before the next tile's loads
-            const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s, my_len, need_max)
-                                             : min(64u, s + my_len);
-            const bool cov = a_end >= s + min(my_len, 28u);
-            const uint32_t end = !live ? 0u
-                               : cov ? s + header_end(w0, my_len, kNeedFilter)
-                                     : s + min(my_len, need_max);
-            const uint32_t lo = (a_end + 15u) >> 4;
-            const bool my_nb = end > 16u * lo;
-            if (__ballot(my_nb) != 0ull) {
-                const bool second = __ballot(my_nb && lo < 4u && end > 16u * (lo + 4u)) != 0ull;
-                load_round_b<-1>(a, t, lane, qa0, my_nb ? (lo | (end << 8)) : 0u, img, second);
-                wave_lds_sync();
-                window<10>(row, s, w0);
-            }
-            wide = __popcll(__ballot(end > 64u)) > 32;
-            if (a.nt & 12u) wide = (a.nt & 8u) != 0u;
-        }
+        if (REC != kRecNone)   // round B, before the next tile's loads
+            wide = round_b(a, t, lane, st.qa0, img, row, s, my_off, my_len, live, st.wide, need_max, w0);
 
         // next tile: round A from the descriptors loaded one tile ago, then the
         // descriptors of the tile after it
@@ -963,32 +967,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
 
         // ---- FILTER ----
         if (FILTER) {
-            FilterIn x;
-            x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
-            x.proto = byte_of(w0, 23);
-            x.src = be32_of(w0, 26);
-            x.dst = be32_of(w0, 30);
-            x.sport = be16_of(w0, 34);
-            x.dport = be16_of(w0, 36);
-            x.l4_ok = ((x.proto == 6) & (len >= 54)) | ((x.proto == 17) & (len >= 42));
-            uint32_t code = BT_DECIDE_PASS, slot = prog.n ? prog.n - 1u : 0u;
-            bool open = live;
-            uint32_t staged_sh = ~0u;
-            for (uint32_t f = 0; f < prog.n; ++f) {
-                if (__ballot(open) == 0ull) break;
-                uint32_t rr;
-                if (prog.f[f].kind == BT_K_PAYLOAD)
-                    rr = a.prefixes ? 3u
-                       : open ? eval_payload(a, dfa_lds + prog.f[f].a, img + lane * kRow, my_off, len, w0, staged_sh)
-                              : 0u;
-                else
-                    rr = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
-                if (open && rr != 1u) {
-                    code = rr == 0u ? BT_DECIDE_REJECT : rr == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
-                    slot = f;
-                    open = false;
-                }
-            }
+            uint32_t slot;
+            const uint32_t code = filter_packet(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
@@ -1160,7 +1140,7 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
             return;
         }
     }
-    if (pf) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
+    if (pf && FL < 0) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
     else go(bt_parse_filter_main<FL, REC, F, false>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn));
 }
 
@@ -1190,9 +1170,9 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
         else if (a.stride == 64) fl = 2;
         else if (a.stride == 128) fl = 3;
     }
-    // Next-tile prefetch pays for descriptor mode (+3 % C3) but not for fixed stride
-    // (-16 % C2: the early loads interleave with the record stores).
-    prefetch = prefetch && fl < 0;
+    // Next-tile prefetch: the pipe kernel always prefetches (BT_OPT_NO_PREFETCH selects
+    // bt_parse_filter_main without it). In bt_parse_filter_main it pays for descriptor
+    // mode (+3 % C3) but not for fixed stride (-16 % C2); launch_t drops it there.
     switch (fl) {
     case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, prefetch, st); break;
     case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, prefetch, st); break;
