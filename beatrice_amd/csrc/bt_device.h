@@ -52,8 +52,11 @@ constexpr uint32_t kNeedFilter = 38;              // PacketFilter reads bytes 12
 
 // Launch wrappers (bt_kernels.hip). All are asynchronous on `stream`.
 enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2, kRecTiled = 3 };
+// timing_start / timing_stop (hipEvent_t, may be null): recorded by the kernel's own
+// dispatch (hipExtLaunchKernelGGL), so timing a launch adds no packets to the stream.
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
-                int grid_blocks, bool prefetch, void* stream);
+                int grid_blocks, bool prefetch, void* stream, void* timing_start = nullptr,
+                void* timing_stop = nullptr);
 int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
                    uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream);
 int device_grid_blocks(int device);

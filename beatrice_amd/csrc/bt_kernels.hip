@@ -19,6 +19,7 @@
 //               pass count feeds the ordered compaction kernels below.
 // Replaces the per-packet work of reference src/parser/ProtocolParser.cpp:238-433 and
 // src/PacketFilter.cpp:57-372 (see DESIGN.md for the line-by-line mapping).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1119,7 +1120,8 @@ bool use_pipe() {
 }
 
 template <int FL, int REC, bool F>
-void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st) {
+void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st, hipEvent_t e0,
+              hipEvent_t e1) {
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
     auto go = [&](auto kernel, int resident) {
@@ -1129,7 +1131,10 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
         // fewer concurrent read and write streams suit HBM better here.
         if (FL >= 0 && grid <= 0) g = std::min(g, 2 * cu_count());
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
-        hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
+        if (e0 || e1)
+            hipExtLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, e0, e1, 0, a, prog);
+        else
+            hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
     };
     if constexpr (FL < 0 && (REC == kRecTiled || REC == kRecNone)) {
         if (pf && a.desc && (a.nt & 1u) && use_pipe()) {
@@ -1145,23 +1150,25 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
 }
 
 template <int FL>
-void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, bool pf, hipStream_t st) {
+void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, bool pf, hipStream_t st,
+               hipEvent_t e0, hipEvent_t e1) {
     if (rec == kRecPlanes) {
-        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, pf, st); else launch_t<FL, kRecPlanes, false>(a, prog, grid, pf, st);
+        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecPlanes, false>(a, prog, grid, pf, st, e0, e1);
     } else if (rec == kRecTiled) {
-        if (f) launch_t<FL, kRecTiled, true>(a, prog, grid, pf, st); else launch_t<FL, kRecTiled, false>(a, prog, grid, pf, st);
+        if (f) launch_t<FL, kRecTiled, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecTiled, false>(a, prog, grid, pf, st, e0, e1);
     } else if (rec == kRecAoS) {
-        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, pf, st); else launch_t<FL, kRecAoS, false>(a, prog, grid, pf, st);
+        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecAoS, false>(a, prog, grid, pf, st, e0, e1);
     } else {
-        launch_t<FL, kRecNone, true>(a, prog, grid, pf, st);
+        launch_t<FL, kRecNone, true>(a, prog, grid, pf, st, e0, e1);
     }
 }
 
 }  // namespace
 
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter, int grid_blocks,
-                bool prefetch, void* stream) {
+                bool prefetch, void* stream, void* timing_start, void* timing_stop) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipEvent_t e0 = reinterpret_cast<hipEvent_t>(timing_start), e1 = reinterpret_cast<hipEvent_t>(timing_stop);
     const int grid = grid_blocks;   // <= 0: one residency wave of the chosen variant
     int fl = -1;   // fixed-stride fast path when the stride is 16/32/64/128 B
     if (!a.desc) {
@@ -1174,11 +1181,11 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
     // bt_parse_filter_main without it). In bt_parse_filter_main it pays for descriptor
     // mode (+3 % C3) but not for fixed stride (-16 % C2); launch_t drops it there.
     switch (fl) {
-    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, prefetch, st); break;
-    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, prefetch, st); break;
-    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, prefetch, st); break;
-    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, prefetch, st); break;
-    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, prefetch, st); break;
+    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
+    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
+    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
+    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
+    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
     }
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }

@@ -260,10 +260,10 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
         else if (c->opts.flags & BT_OPT_RECORDS_PLANES) rec = kRecPlanes;
         else rec = kRecTiled;
     }
-    if (e0) HIP_TRY(hipEventRecord(e0, st));
-    int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st);
+    // e0 / e1 time the main kernel from its own dispatch packet (no marker packets: a
+    // pair of hipEventRecord around the launch left the GPU idle ~6 us each, per step)
+    int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, e1);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (e1) HIP_TRY(hipEventRecord(e1, st));
     if (compact) {
         rc = launch_compact(a.verdict, c->tile_pass, a.ntiles, b->n, c->chunk_sums, o->pass_idx, o->n_pass, st);
         if (rc) return fail(rc, "compaction launch failed");

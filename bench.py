@@ -9,9 +9,11 @@ is already resident in HBM. Default workload (N=1): BASELINE.json configs[1] —
 16,777,216 fixed 64 B Eth/IPv4/UDP frames, parse-only (one packed record per packet:
 64 B on the device for Eth/IPv4/UDP, unpacked to the 96-B bt_rec by the host).
 `--config c3` runs configs[2] (IMIX parse + 5-tuple PacketFilter + ordered
-compaction). Multi-GPU is weak scaling: every rank owns its own 16M-packet batch on
-its own device (packet batches shard with no collective; the only cross-rank traffic
-is the timing barrier and the max-reduction of the step time, over gloo).
+compaction). Multi-GPU is weak scaling by default: every rank owns its own 16M-packet
+batch on its own device (packet batches shard with no collective; the only cross-rank
+traffic is the timing barrier and the max-reduction of the step time, over gloo).
+`--strong` (C5's other half) splits one --packets batch into tile-aligned,
+byte-balanced contiguous shards, one per rank.
 
 Prints ONE JSON line on rank 0 with value = packets of all ranks / max step time,
 the roofline of the main kernel (HIP events around every main-kernel launch inside the
@@ -31,7 +33,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from beatrice_amd import abi, synth  # noqa: E402
+from beatrice_amd import abi, shard, synth  # noqa: E402
 
 METRIC = "Mpps + achieved HBM GB/s, device-resident parse+filter, 64B and IMIX"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -140,6 +142,9 @@ def main():
     ap.add_argument("--payload", default=None,
                     help="c3/c4: put a PAYLOAD regex FIRST in the filter program (every IPv4 packet runs the "
                          "GPU DFA: worst case); reported in config, not the default workload")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (C5): --packets is the whole job, split across the ranks in "
+                         "tile-aligned, byte-balanced contiguous shards (beatrice_amd/shard.py)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -152,9 +157,18 @@ def main():
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
     wl = WORKLOADS[args.config]
-    n = args.packets
-
-    data, desc = synth.capture(wl["cfg"], n, seed=synth.SEEDS[wl["cfg"]] + rank)
+    n_job = args.packets * (1 if args.strong else world)
+    if args.strong:
+        # every rank generates the same capture and keeps its own shard, rebased
+        data, desc = synth.capture(wl["cfg"], args.packets, seed=synth.SEEDS[wl["cfg"]])
+        lo, hi = shard.shard_bounds(synth.desc_len(desc), world)[rank]
+        if wl["fixed"]:
+            data, desc = np.ascontiguousarray(data[lo * 64:hi * 64]), desc[lo:hi]
+        else:
+            data, desc = shard.local_batch(data, desc, lo, hi)
+    else:
+        data, desc = synth.capture(wl["cfg"], args.packets, seed=synth.SEEDS[wl["cfg"]] + rank)
+    n = len(desc)
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
     flags |= abi.OPT_SPIN_SYNC   # the timed region's end is not delayed by a sleeping host thread
     # BT_BENCH_DEVICE: put every rank on one device (multi-rank rehearsal on a 1-GPU box)
@@ -203,8 +217,7 @@ def main():
         t = torch.tensor([step_s, main_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         step_s, main_ms = float(t[0]), float(t[1])
-    total_pkts = n * world
-    value = total_pkts / step_s / 1e6
+    value = n_job / step_s / 1e6
 
     algo = algorithmic_bytes(desc, wl["fixed"], rec_bytes, filt)
     if args.payload is not None:
@@ -235,11 +248,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64)",
-            "config": {"workload": wl["name"], "packets_per_gpu": n, "parallelism": f"batch split x{world}",
+            "config": {"workload": wl["name"], "packets_per_gpu": n, "packets_total": n_job,
+                       "parallelism": f"batch split x{world}",
                        "pass_fraction": round(n_pass / n, 4) if filt else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
