@@ -1,22 +1,27 @@
 // bt_kernels.hip — gfx950 kernels for the Beatrice parse+filter stage.
 //
-// bt_parse_filter_main: one packet per lane, one 64-packet tile per wavefront,
-// persistent grid-stride over tiles. Per tile:
-//   1. LOAD   — the wave fetches the 64 header windows (<=128 B each, 16-B aligned
-//               chunks) with coalesced global_load_dwordx4: in descriptor mode 8 lanes
-//               cover one packet's window (8 packets per instruction); in fixed-stride
-//               mode the tile is one contiguous span (1 KiB per instruction).
-//               Chunks are written into a per-wave LDS image, one 132-B row per packet
-//               (33 dwords: the odd stride spreads the later per-lane reads over banks).
+// bt_parse_filter_main / bt_parse_filter_pipe: one packet per lane, one 64-packet tile
+// per wavefront, persistent grid-stride over tiles. Per tile:
+//   1. LOAD   — the wave fetches the 64 header windows (16-B aligned chunks) with
+//               coalesced 16-B loads: in descriptor mode round A reads the first 64 B
+//               of every window with 4 lanes per packet (16 packets per instruction),
+//               round B only the further chunks the walked headers need; in
+//               fixed-stride mode the tile is one contiguous span (1 KiB per
+//               instruction). Chunks go into a per-wave LDS image, one row per packet
+//               (33 dwords in descriptor mode: the odd stride spreads the per-lane reads
+//               over the banks).
 //   2. PARSE  — each lane walks its own row: Ethernet, up to two 802.1Q/802.1ad tags,
 //               IPv4/IPv6, TCP/UDP/ICMP (DESIGN.md "R-WALK"). Unaligned header windows
 //               are rebuilt from aligned ds_read_b32 pairs with v_alignbyte_b32. The
-//               96-B bt_rec is assembled in registers and written as six 16-B slab
-//               stores (plane-major: 1 KiB per wave instruction) or AoS for host copies.
+//               record is assembled in registers: the packed device form (2-6 16-B
+//               slabs, tiled per 64-packet tile, include/beatrice_gpu.h) or the 96-B
+//               bt_rec (AoS, host copies).
 //   3. FILTER — the compiled PacketFilter program (kernel argument, scalar loads) is
 //               evaluated wave-uniformly slot by slot with early exit once every lane
 //               has decided; the verdict is a wavefront __ballot word and the per-tile
 //               pass count feeds the ordered compaction kernels below.
+// bt_parse_filter_pipe is the descriptor-mode form with counted memory waits (see the
+// comment above it); bt_parse_filter_main serves fixed stride and the other layouts.
 // Replaces the per-packet work of reference src/parser/ProtocolParser.cpp:238-433 and
 // src/PacketFilter.cpp:57-372 (see DESIGN.md for the line-by-line mapping).
 #include <hip/hip_ext.h>
