@@ -1,0 +1,85 @@
+"""CPU: the bench contract and the committed evidence agree with each other.
+
+* bench.py's helpers: the algorithmic-bytes formula and the name of the
+  main-kernel variant it reports;
+* every committed bench line (profiles/r01/bench_*.json) carries the contract's keys, and
+  its roofline numbers follow from its own fields (achieved = algorithmic bytes x packets
+  / kernel time, frac = achieved / peak);
+* the rocprofv3 kernel stats committed beside it (profiles/r01/*_kernel_stats.csv) agree
+  with the bench's own event timing of the same command within 5 %, and name the kernel
+  the bench line names;
+* the PMC traffic the bench lines quote is the one in profiles/traffic.json.
+"""
+import csv
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from beatrice_amd import synth  # noqa: E402
+
+PROFILES = os.path.join(ROOT, "profiles", "r01")
+CONFIGS = ["c2", "c3", "c4"]
+
+
+def _line(path):
+    with open(path) as fh:
+        return [json.loads(x) for x in fh if x.startswith("{")][-1]
+
+
+def test_algorithmic_bytes_formula():
+    data, desc = synth.capture(synth.C3, 1000, seed=3)
+    lens = synth.desc_len(desc).astype(np.int64)
+    got = bench.algorithmic_bytes(desc, fixed=False, rec_bytes=58.0 * 1000, filt=True)
+    want = np.minimum(lens, 128).sum() + 8 * 1000 + 58.0 * 1000 + 1000 * 1.125
+    assert got == pytest.approx(want)
+    got = bench.algorithmic_bytes(desc, fixed=True, rec_bytes=0.0, filt=False)
+    assert got == pytest.approx(np.minimum(lens, 128).sum())
+
+
+def test_main_kernel_name(monkeypatch):
+    monkeypatch.delenv("BT_NO_PIPE", raising=False)
+    assert bench.main_kernel_name(bench.WORKLOADS["c2"]) == "bt_parse_filter_main"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"]) == "bt_parse_filter_pipe"
+    monkeypatch.setenv("BT_NO_PIPE", "1")
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"]) == "bt_parse_filter_main"
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_committed_bench_line_is_consistent(cfg):
+    d = _line(os.path.join(PROFILES, f"bench_{cfg}.json"))
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["n_gpus"] == 1 and d["unit"] == "Mpps" and d["higher_is_better"] is True
+    n = d["config"]["packets_per_gpu"]
+    assert d["value"] == pytest.approx(n / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    achieved = r["algorithmic_bytes_per_packet"] * n / (r["kernel_ms"] * 1e-3) / 1e9
+    assert r["achieved"] == pytest.approx(achieved, rel=2e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
+    c = d["cpu_baseline"]
+    assert c["kind"] in ("reference", "port") and c["cores"] >= 1 and c["value"] > 0
+    # the PMC traffic quoted is the committed per-launch figure
+    traffic = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[cfg]
+    assert r["traffic"] == traffic["traffic"] and traffic["packets"] == n
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_rocprof_stats_agree_with_bench_events(cfg):
+    under = _line(os.path.join(PROFILES, f"{cfg}_bench_under_rocprof.json"))
+    with open(os.path.join(PROFILES, f"{cfg}_kernel_stats.csv")) as fh:
+        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"]]
+    assert len(rows) == 1, [x["Name"] for x in rows]
+    assert under["roofline"]["kernel"] in rows[0]["Name"]
+    avg_ms = float(rows[0]["AverageNs"]) / 1e6
+    assert avg_ms == pytest.approx(under["roofline"]["kernel_ms"], rel=0.05)
