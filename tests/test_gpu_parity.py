@@ -330,3 +330,29 @@ def test_kernel_forms_agree(form):
             check_filter_outputs(out, n)
     finally:
         ctx.close()
+
+
+def test_repeated_runs_are_identical(gpu_ctx):
+    """The same 1M-packet C4 batch through the main kernel 16 times: records, decisions and
+    pass lists never change (a wait that retired too early — the counted vmcnt waits of
+    bt_parse_filter_pipe — would show up as run-to-run differences), and match the oracle."""
+    n = 1 << 20
+    data, desc = synth.capture(synth.C4, n, seed=0xBEEF)
+    filters = [{"type": abi.PROTOCOL, "expr": "tcp", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1-40000", "priority": 1}]
+    gpu_ctx.compile(filters)
+    r = abi.DeviceRun(gpu_ctx, data, desc, n)
+    try:
+        r.run()
+        first = r.fetch()
+        rec, dec, npass = ol.oracle_run(data, desc, n, filters)
+        assert np.array_equal(first["records"], rec) and np.array_equal(first["decide"], dec)
+        assert first["n_pass"] == npass
+        for _ in range(15):
+            r.run()
+            out = r.fetch()
+            for k in ("records", "decide", "verdict", "pass_idx"):
+                assert np.array_equal(out[k], first[k]), k
+            assert out["n_pass"] == first["n_pass"]
+    finally:
+        r.free()
