@@ -68,12 +68,16 @@ def payload_extra_bytes(data: np.ndarray, desc: np.ndarray) -> float:
     return float(extra.sum())
 
 
-def main_kernel_name(wl) -> str:
+def main_kernel_name(wl, flags: int = 0) -> str:
     """The main-kernel variant launch_main picks (bt_kernels.hip launch_t): descriptor
-    mode runs the counted-wait pipeline unless BT_NO_PIPE is set; fixed stride runs
-    bt_parse_filter_main."""
+    mode with packed tiled records (or none) and non-temporal record stores runs the
+    counted-wait pipeline unless BT_NO_PIPE is set or prefetch is off; everything else
+    runs bt_parse_filter_main."""
     no_pipe = os.environ.get("BT_NO_PIPE", "") not in ("", "0")
-    return "bt_parse_filter_main" if wl["fixed"] or no_pipe else "bt_parse_filter_pipe"
+    layout = flags & (abi.OPT_RECORDS_AOS | abi.OPT_RECORDS_PLANES)
+    nt_stores = not (flags & abi.OPT_CACHE_DEFAULT) or (flags & abi.OPT_NT_STORES)
+    pipe = not (wl["fixed"] or no_pipe or layout or (flags & abi.OPT_NO_PREFETCH) or not nt_stores)
+    return "bt_parse_filter_pipe" if pipe else "bt_parse_filter_main"
 
 
 def algorithmic_bytes(desc: np.ndarray, fixed: bool, rec_bytes: float, filt: bool) -> float:
@@ -258,7 +262,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": main_kernel_name(wl), "kernel_ms": round(main_ms, 4),
+                         "kernel": main_kernel_name(wl, flags), "kernel_ms": round(main_ms, 4),
                          "algorithmic_bytes_per_packet": round(algo / n, 2),
                          "record_bytes_per_packet": round(rec_bytes / n, 2),
                          "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),

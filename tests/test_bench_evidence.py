@@ -21,7 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
-from beatrice_amd import synth  # noqa: E402
+from beatrice_amd import abi, synth  # noqa: E402
 
 PROFILES = os.path.join(ROOT, "profiles", "r01")
 CONFIGS = ["c2", "c3", "c4"]
@@ -46,6 +46,11 @@ def test_main_kernel_name(monkeypatch):
     monkeypatch.delenv("BT_NO_PIPE", raising=False)
     assert bench.main_kernel_name(bench.WORKLOADS["c2"]) == "bt_parse_filter_main"
     assert bench.main_kernel_name(bench.WORKLOADS["c3"]) == "bt_parse_filter_pipe"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"], abi.OPT_NO_PREFETCH) == "bt_parse_filter_main"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"], abi.OPT_RECORDS_AOS) == "bt_parse_filter_main"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"], abi.OPT_CACHE_DEFAULT) == "bt_parse_filter_main"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3"],
+                                  abi.OPT_CACHE_DEFAULT | abi.OPT_NT_STORES) == "bt_parse_filter_pipe"
     monkeypatch.setenv("BT_NO_PIPE", "1")
     assert bench.main_kernel_name(bench.WORKLOADS["c3"]) == "bt_parse_filter_main"
 
