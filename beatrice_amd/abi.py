@@ -88,6 +88,19 @@ class Outputs(ctypes.Structure):
                 ("decide", ctypes.c_void_p), ("pass_idx", ctypes.c_void_p), ("n_pass", ctypes.c_void_p)]
 
 
+class Timing(ctypes.Structure):
+    """bt_timing (include/beatrice_gpu.h): bt_time_device_ex's breakdown."""
+    _fields_ = [("span_ms", ctypes.c_float), ("main_ms", ctypes.c_float), ("main_min_ms", ctypes.c_float),
+                ("main_max_ms", ctypes.c_float), ("lead_ms", ctypes.c_float), ("gap_ms", ctypes.c_float),
+                ("enqueue_ms", ctypes.c_double), ("first_seen_ms", ctypes.c_double),
+                ("last_seen_ms", ctypes.c_double), ("query_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
+                ("spin_rc", ctypes.c_int32), ("device_flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 6)]
+
+    def as_dict(self) -> dict:
+        return {k: (round(getattr(self, k), 4) if isinstance(getattr(self, k), float) else getattr(self, k))
+                for k, _ in self._fields_ if k != "reserved"}
+
+
 class Tpv3Ring(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("block_size", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32)]
@@ -97,7 +110,7 @@ EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_record_gather", "bt_record_gather_planes",
+    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
@@ -140,6 +153,8 @@ def lib() -> ctypes.CDLL:
         "bt_synchronize": (ctypes.c_int, [vp]),
         "bt_time_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+        "bt_time_device_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
+                                             ctypes.POINTER(Timing)]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
         "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
@@ -226,10 +241,10 @@ class DeviceBuffer:
         _check(lib().bt_dev_malloc(ctx.h, self.nbytes, ctypes.byref(p)))
         self.ptr = p.value
 
-    def upload(self, arr: np.ndarray):
+    def upload(self, arr: np.ndarray, offset: int = 0):
         arr = np.ascontiguousarray(arr)
-        assert arr.nbytes <= self.nbytes
-        _check(lib().bt_memcpy_h2d(self.ctx.h, self.ptr, arr.ctypes.data, arr.nbytes))
+        assert offset >= 0 and offset + arr.nbytes <= self.nbytes
+        _check(lib().bt_memcpy_h2d(self.ctx.h, self.ptr + offset, arr.ctypes.data, arr.nbytes))
 
     def download(self, arr: np.ndarray):
         assert arr.flags.c_contiguous and arr.nbytes <= self.nbytes
@@ -315,6 +330,11 @@ class Context:
         _check(lib().bt_time_device(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(a),
                                     ctypes.byref(b)))
         return a.value, b.value
+
+    def time_device_ex(self, batch: Batch, outs: Outputs, iters: int) -> Timing:
+        t = Timing()
+        _check(lib().bt_time_device_ex(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(t)))
+        return t
 
     def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
         """bt_parse_filter over host buffers. Returns dict of numpy outputs."""
@@ -496,17 +516,19 @@ def tile_packed(c: np.ndarray, nslab: np.ndarray, planes: bool = False, seed: in
 class DeviceRun:
     """Device-resident batch + outputs (the bench / parity path)."""
 
-    def __init__(self, ctx: Context, data: np.ndarray, desc: np.ndarray | None, n: int, stride: int = 0,
-                 records=True, decide=True, verdict=True, pass_idx=True):
+    def __init__(self, ctx: Context, data: np.ndarray | None, desc: np.ndarray | None, n: int, stride: int = 0,
+                 records=True, decide=True, verdict=True, pass_idx=True, data_bytes: int | None = None):
+        """data=None: the packet buffer (data_bytes long) is filled later with upload_data()."""
         self.ctx, self.n = ctx, n
-        self.d_data = ctx.alloc((data.nbytes + 255) // 256 * 256 + 256)
-        self.d_data.upload(data)
+        nbytes = int(data.nbytes) if data is not None else int(data_bytes)
+        self.d_data = ctx.alloc((nbytes + 255) // 256 * 256 + 256)
+        if data is not None:
+            self.d_data.upload(data)
         self.d_desc = None
         if desc is not None:
             self.d_desc = ctx.alloc(max(8, desc.nbytes))
             self.d_desc.upload(np.ascontiguousarray(desc, dtype=np.uint64))
-        self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n,
-                           int(data.nbytes))
+        self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n, nbytes)
         nt = (n + 63) // 64
         self.d_rec = ctx.alloc(max(16, nt * 64 * BT_REC_BYTES)) if records else None
         self.d_dec = ctx.alloc(max(16, n)) if decide else None
@@ -519,6 +541,10 @@ class DeviceRun:
                             self.d_pidx.ptr if self.d_pidx else None,
                             self.d_npass.ptr if self.d_npass else None)
         ctx.reserve(n)
+
+    def upload_data(self, buf: np.ndarray, offset: int):
+        """Bytes of the packet buffer from `offset` on (a capture streamed range by range)."""
+        self.d_data.upload(buf, offset)
 
     def run(self):
         self.ctx.run_device(self.batch, self.outs)

@@ -157,6 +157,8 @@ struct bt_ctx {
     bt_batch tg_batch{};
     bt_outputs tg_out{};
     uint32_t tg_iters = 0;
+    int spin_rc = -1;                  // hipSetDeviceFlags(hipDeviceScheduleSpin) result
+    unsigned device_flags = 0;
 };
 
 namespace bt {
@@ -358,12 +360,14 @@ int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
         // host waits spin instead of sleeping: no wake-up latency on a loaded host.
         // Only possible before the process's first HIP context on this device.
         (void)hipSetDevice(device);
-        (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        c->spin_rc = (int)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        (void)hipGetLastError();   // a refusal (context already active) is reported, not sticky
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(BT_E_INIT_FAILED, "hipSetDevice/hipStreamCreate failed on device %d", device);
     }
+    (void)hipGetDeviceFlags(&c->device_flags);
     (void)hipEventCreate(&c->ev0);
     (void)hipEventCreate(&c->ev1);
     c->grid = c->opts.grid_waves ? (int)((c->opts.grid_waves + kWavesPerBlock - 1) / kWavesPerBlock)
@@ -471,8 +475,7 @@ int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, vo
     return run_device(c, b, o, st, false, nullptr, nullptr);
 }
 
-int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
-                   float* main_ms) {
+int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
     if (!c || !b || !o || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
@@ -508,8 +511,9 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
         c->tg_out = *o;
         c->tg_iters = iters;
     }
-    static const bool dbg = getenv("BT_DEBUG_TIMING") != nullptr;
-    const auto h0 = std::chrono::steady_clock::now();
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    const auto h0 = clk::now();
     if (use_graph) {
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(hipGraphLaunch(c->tgraph, c->stream));
@@ -522,24 +526,65 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
         }
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
     }
-    const auto h1 = std::chrono::steady_clock::now();
-    HIP_TRY(hipEventSynchronize(c->ev1));
-    const auto h2 = std::chrono::steady_clock::now();
-    float tot = 0, k = 0;
+    const auto h1 = clk::now();
+    // Poll instead of hipEventSynchronize: a blocking wait is woken by an interrupt, whose
+    // latency would sit inside the caller's timed region.
+    auto poll = [](hipEvent_t e) -> hipError_t {
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q != hipErrorNotReady) return q;
+        }
+    };
+    HIP_TRY(poll(c->ev0));
+    const auto h2 = clk::now();
+    HIP_TRY(poll(c->ev1));
+    const auto h3 = clk::now();
+    float tot = 0, k = 0, kmin = 1e30f, kmax = 0, lead = 0, gap = 0;
     HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
     for (uint32_t i = 0; !use_graph && i < iters; ++i) {
         float x = 0;
         HIP_TRY(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
         k += x;
+        kmin = std::min(kmin, x);
+        kmax = std::max(kmax, x);
+        if (i + 1 < iters) {
+            float g = 0;
+            HIP_TRY(hipEventElapsedTime(&g, c->tev[2 * i + 1], c->tev[2 * i + 2]));
+            gap += g;
+        }
     }
-    if (ms_per_iter) *ms_per_iter = tot / iters;
-    if (main_ms) *main_ms = use_graph ? -1.0f : k / iters;
-    if (dbg) {
-        const auto h3 = std::chrono::steady_clock::now();
-        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "[bt_time_device] enqueue %.3f ms, sync %.3f ms, elapsed-queries %.3f ms, gpu span %.3f ms\n",
-                ms(h0, h1), ms(h1, h2), ms(h2, h3), tot);
+    if (!use_graph) HIP_TRY(hipEventElapsedTime(&lead, c->ev0, c->tev[0]));
+    const auto h4 = clk::now();
+    if (t) {
+        *t = bt_timing{};
+        t->span_ms = tot;
+        t->main_ms = use_graph ? -1.0f : k / iters;
+        t->main_min_ms = use_graph ? -1.0f : kmin;
+        t->main_max_ms = use_graph ? -1.0f : kmax;
+        t->lead_ms = lead;
+        t->gap_ms = gap;
+        t->enqueue_ms = ms(h0, h1);
+        t->first_seen_ms = ms(h1, h2);
+        t->last_seen_ms = ms(h2, h3);
+        t->query_ms = ms(h3, h4);
+        t->wall_ms = ms(h0, h4);
+        t->spin_rc = c->spin_rc;
+        t->device_flags = c->device_flags;
     }
+    static const bool dbg = getenv("BT_DEBUG_TIMING") != nullptr;
+    if (dbg)
+        fprintf(stderr, "[bt_time_device] enqueue %.3f ms, first-seen %.3f ms, last-seen %.3f ms, queries %.3f ms, "
+                "gpu span %.3f ms\n", ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, h4), tot);
+    return BT_OK;
+}
+
+int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
+                   float* main_ms) {
+    bt_timing t{};
+    const int rc = bt_time_device_ex(c, b, o, iters, &t);
+    if (rc) return rc;
+    if (ms_per_iter) *ms_per_iter = t.span_ms / iters;
+    if (main_ms) *main_ms = t.main_ms;
     return BT_OK;
 }
 

@@ -259,25 +259,36 @@ uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc) {
     return (off + 255) / 256 * 256;
 }
 
-// Fills the frames described by desc into data (nthreads threads).
-int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads) {
-    uint64_t nb = (n + kBlock - 1) / kBlock;
+// Fills frames [lo, hi) of the capture described by desc; frame i goes to
+// data + (offset_i - data_off). lo must be a multiple of the 65536-frame RNG block, so a
+// capture filled range by range is identical to one filled at once (bench.py streams
+// large captures to the device this way instead of holding them whole on the host).
+int bt_synth_fill_range(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint64_t lo, uint64_t hi,
+                        uint8_t* data, uint64_t data_off, int nthreads) {
+    if (lo % kBlock || hi > n || lo > hi) return 1;
+    const uint64_t b0 = lo / kBlock, b1 = (hi + kBlock - 1) / kBlock;
     if (nthreads < 1) nthreads = 1;
     std::vector<std::thread> th;
     for (int t = 0; t < nthreads; ++t) {
         th.emplace_back([=] {
-            for (uint64_t b = (uint64_t)t; b < nb; b += (uint64_t)nthreads) {
+            for (uint64_t b = b0 + (uint64_t)t; b < b1; b += (uint64_t)nthreads) {
                 Rng r(seed, b, 1);
-                uint64_t lo = b * kBlock, hi = std::min(n, lo + kBlock);
-                for (uint64_t i = lo; i < hi; ++i) {
-                    uint64_t d = desc[i];
-                    build(cfg, shape_of(cfg, seed, i), data + (d & 0xFFFFFFFFFFFFull), (uint32_t)(d >> 48), i, r);
+                const uint64_t a = b * kBlock, e = std::min(hi, a + kBlock);
+                for (uint64_t i = a; i < e; ++i) {
+                    const uint64_t d = desc[i];
+                    build(cfg, shape_of(cfg, seed, i), data + ((d & 0xFFFFFFFFFFFFull) - data_off), (uint32_t)(d >> 48),
+                          i, r);
                 }
             }
         });
     }
     for (auto& x : th) x.join();
     return 0;
+}
+
+// Fills the frames described by desc into data (nthreads threads).
+int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads) {
+    return bt_synth_fill_range(cfg, n, seed, desc, 0, n, data, 0, nthreads);
 }
 
 // Packs a capture into an AF_PACKET TPACKET_V3 RX-ring image the way the kernel lays

@@ -30,6 +30,10 @@ def lib() -> ctypes.CDLL:
         L.bt_synth_fill.restype = ctypes.c_int
         L.bt_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int]
+        L.bt_synth_fill_range.restype = ctypes.c_int
+        L.bt_synth_fill_range.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_int]
         L.bt_synth_tpv3_pack.restype = ctypes.c_uint64
         L.bt_synth_tpv3_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
@@ -49,6 +53,37 @@ def capture(cfg: int, n: int, seed: int | None = None, threads: int | None = Non
         threads = min(16, os.cpu_count() or 1)
     L.bt_synth_fill(cfg, n, seed, desc.ctypes.data, data.ctypes.data, threads)
     return data, desc
+
+
+RNG_BLOCK = 65536   # frames per RNG block of bt_synth.cpp (fill ranges start on one)
+
+
+def layout(cfg: int, n: int, seed: int | None = None):
+    """(desc, data bytes) of a capture without filling it."""
+    if seed is None:
+        seed = SEEDS[cfg]
+    desc = np.empty(n, dtype=np.uint64)
+    nbytes = lib().bt_synth_layout(cfg, n, seed, desc.ctypes.data)
+    return desc, int(nbytes)
+
+
+FILL_PAD = 128   # zero bytes fill_range leaves after the last frame (over-reads of header math)
+
+
+def fill_range(cfg: int, seed: int, desc: np.ndarray, lo: int, hi: int, threads: int | None = None):
+    """Frames [lo, hi) of a capture (lo a multiple of RNG_BLOCK), identical to the same
+    frames of capture(cfg, len(desc), seed). Returns (buf, b0, nbytes): frame i sits at
+    buf[offset_i - b0], the frames span buf[:nbytes], and FILL_PAD zero bytes follow."""
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    off = desc_off(desc)
+    b0 = int(off[lo]) if hi > lo else 0
+    b1 = int(off[hi - 1] + desc_len(desc[hi - 1:hi])[0]) if hi > lo else 0
+    buf = np.zeros(b1 - b0 + FILL_PAD, dtype=np.uint8)
+    rc = lib().bt_synth_fill_range(cfg, len(desc), seed, desc.ctypes.data, lo, hi, buf.ctypes.data, b0, threads)
+    if rc:
+        raise ValueError(f"bt_synth_fill_range({lo}, {hi}) = {rc}")
+    return buf, b0, b1 - b0
 
 
 def desc_off(desc: np.ndarray) -> np.ndarray:

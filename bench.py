@@ -1,28 +1,43 @@
 #!/usr/bin/env python3
 """Benchmark of the device-resident parse+filter hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4] [--packets P]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2f|c2|c3|c4] [--configs LIST|none]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-A step = one bt_parse_filter_device() pass over one synthetic 16M-packet batch that
-is already resident in HBM. Default workload (N=1): BASELINE.json configs[1] — C2,
-16,777,216 fixed 64 B Eth/IPv4/UDP frames, parse-only (one packed record per packet:
-64 B on the device for Eth/IPv4/UDP, unpacked to the 96-B bt_rec by the host).
-`--config c3` runs configs[2] (IMIX parse + 5-tuple PacketFilter + ordered
-compaction). Multi-GPU is weak scaling by default: every rank owns its own 16M-packet
-batch on its own device (packet batches shard with no collective; the only cross-rank
-traffic is the timing barrier and the max-reduction of the step time, over gloo).
-`--strong` (C5's other half) splits one --packets batch into tile-aligned,
-byte-balanced contiguous shards, one per rank.
+A step = one bt_parse_filter_device() pass over one synthetic 16M-packet batch that is
+already resident in HBM (the reference's batch entry it replaces:
+PacketFilter::applyFilters(const std::vector<Packet>&), src/PacketFilter.cpp:121-130,
+plus ProtocolParser::parsePacket per walked layer, src/parser/ProtocolParser.cpp:69-95).
 
-Prints ONE JSON line on rank 0 with value = packets of all ranks / max step time,
-the roofline of the main kernel (HIP events around every main-kernel launch inside the
-timed region) and, at N=1, the same run's CPU baseline: the reference's own parser +
-PacketFilter (oracle/_ref, compiled from the reference sources) on the host cores.
+The headline (`value`) is the metric's 64-B case: "c2f" = 16,777,216 fixed 64-B
+Eth/IPv4/UDP frames (BASELINE configs[1]'s frames), parsed into packed records (48 B
+per packet on the device for untagged Eth/IPv4/UDP) AND filtered by C3's 5-tuple
+PacketFilter set (PROTOCOL udp, IP_RANGE 10.0.0.0/8, PORT_RANGE 1000-2000) with ordered
+pass-index compaction. The same run adds a `configs` object with one entry per other
+BASELINE config, each with its own ms_per_step, Mpps, roofline and CPU baseline:
+  c2  configs[1]: the same frames, parse-only
+  c3  configs[2]: IMIX 64/512/1500 Eth/VLAN/IPv4/{TCP,UDP}, parse + filter + compaction
+  c4  configs[3]: QinQ/IPv6/IHL+TCP options at 2-mod-4 offsets, parse + filter
+At N > 1 (C5, configs[4]) the entries are c3 (weak scaling: 16M IMIX packets per GPU)
+and c3_strong (one 16M IMIX batch split into tile-aligned, byte-balanced shards); the
+headline is weak scaling. Packet batches shard with no collective: the only cross-rank
+traffic is the timing barrier and the gathers of the per-rank times, over gloo.
+
+Captures are generated range by range on the host (bt_synth_fill_range) and streamed to
+the device, so no rank holds a whole capture in host memory.
+
+Timing: W untimed warm-up steps; then barrier + device sync, K steps, device sync +
+barrier; max over ranks. bt_time_device_ex launches the K steps with an event pair on
+every main kernel (from its own dispatch packet) and waits by polling, and its
+breakdown (enqueue / first event seen / last event seen / GPU span) goes into the line.
+The CPU baseline is the reference's own parser + PacketFilter (oracle/_ref, compiled
+from the reference sources) on rank 0, on every host CPU the process may use
+(affinity, bounded by the cgroup CPU quota when there is one), after all GPU timing.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -37,12 +52,16 @@ from beatrice_amd import abi, shard, synth  # noqa: E402
 
 METRIC = "Mpps + achieved HBM GB/s, device-resident parse+filter, 64B and IMIX"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LINE = 128              # bytes per HBM access line (the FETCH_SIZE granule)
 
 C3_FILTERS = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
 
 WORKLOADS = {
+    "c2f": dict(cfg=synth.C2, fixed=True, parse=True, filters=C3_FILTERS,
+                name="C2 frames + filter: 16M x 64B Eth/IPv4/UDP, fixed stride, parse + PacketFilter "
+                     "(udp, 10.0.0.0/8, 1000-2000) + ordered compaction (metric's 64B parse+filter)"),
     "c2": dict(cfg=synth.C2, fixed=True, parse=True, filters=None,
                name="C2: 16M x 64B Eth/IPv4/UDP, fixed stride, parse-only (BASELINE configs[1])"),
     "c3": dict(cfg=synth.C3, fixed=False, parse=True, filters=C3_FILTERS,
@@ -52,27 +71,147 @@ WORKLOADS = {
                name="C4: 16M QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets, parse + PacketFilter "
                     "(BASELINE configs[3])"),
 }
+KERNEL_SOURCES = ["beatrice_amd/csrc/bt_kernels.hip", "beatrice_amd/csrc/bt_device.h",
+                  "beatrice_amd/csrc/bt_runtime.cpp"]
 
 
-def payload_extra_bytes(data: np.ndarray, desc: np.ndarray) -> float:
+def kernel_source_sha() -> str:
+    """Key of the committed PMC traffic figures: the sources that decide what the
+    kernels load and store (tools/pmc_traffic.py writes the same key)."""
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def host_cpus() -> dict:
+    """CPUs this process may run on: the affinity set, bounded by the cgroup v2/v1 CPU
+    quota when one is set (threads past the quota only time-share it)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = int(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                p = int(fh.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"model": model, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "threads": threads}
+
+
+def header_need(buf: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
+    """Bytes from each frame's start that the layer walk + filters read: the kernel's
+    header_end() (bt_kernels.hip) with its 38-B floor, at most the frame."""
+    def b(k):
+        return buf[off + k].astype(np.int64)
+    et0, et1, et2 = b(12) << 8 | b(13), b(16) << 8 | b(17), b(20) << 8 | b(21)
+    vl = lambda e: (e == 0x8100) | (e == 0x88A8)  # noqa: E731
+    t0 = vl(et0)
+    t1 = t0 & vl(et1)
+    o3 = 14 + 4 * t0 + 4 * t1
+    et = np.where(t1, et2, np.where(t0, et1, et0))
+    ihl = np.where(t1, b(22), np.where(t0, b(18), b(14))) & 15
+    v4end = o3 + 40 + np.where(ihl > 5, 4 * ihl - 20, 0)
+    end = np.where(et == 0x0800, v4end, np.where(et == 0x86DD, o3 + 60, o3))
+    return np.minimum(np.maximum(end, 38), ln)
+
+
+def unique_lines(start: np.ndarray, nbytes: np.ndarray, prev_last: int = -1) -> tuple[int, int]:
+    """Distinct 128-B lines the byte ranges [start, start + nbytes) touch, for ranges in
+    ascending start order (a line shared by neighbouring frames counts once); prev_last
+    carries the last line counted across calls. Returns (lines, new prev_last)."""
+    live = nbytes > 0
+    first = (start // LINE)[live]
+    last = ((start + nbytes - 1) // LINE)[live]
+    if len(first) == 0:
+        return 0, prev_last
+    before = np.maximum.accumulate(np.concatenate([[prev_last], last[:-1]]))
+    new = last - np.maximum(first, before + 1) + 1
+    return int(np.maximum(new, 0).sum()), int(max(prev_last, last.max()))
+
+
+class Capture:
+    """Per-rank capture streamed to the device, plus the statistics the roofline needs
+    (computed per streamed range, so the capture is never whole on the host)."""
+
+    def __init__(self, ctx, wl, n_total, seed, lo, hi, chunk=1 << 20):
+        cfg = wl["cfg"]
+        self.desc_full, _ = synth.layout(cfg, n_total, seed)
+        off_full = synth.desc_off(self.desc_full)
+        ln_full = synth.desc_len(self.desc_full)
+        self.n = n = hi - lo
+        # rebase to a 128-B-aligned start so every window keeps its line alignment
+        base = (int(off_full[lo]) & ~(LINE - 1)) if n else 0
+        nbytes = int(off_full[hi - 1] + ln_full[hi - 1]) - base if n else 16
+        self.desc = synth.make_desc(off_full[lo:hi] - base, ln_full[lo:hi])
+        self.stride = 64 if wl["fixed"] else 0
+        filt = wl["filters"] is not None
+        self.run = abi.DeviceRun(ctx, None, None if wl["fixed"] else self.desc, n, stride=self.stride,
+                                 records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt,
+                                 data_bytes=nbytes)
+        self.win_bytes = 0        # sum of min(len, 128)
+        self.need_lines = 0       # distinct 128-B lines of [off, off + header_need)
+        need_last = -1
+        self.payload_extra = 0    # PAYLOAD window bytes past 128 (only with --payload)
+        i = lo - lo % synth.RNG_BLOCK
+        while i < hi:
+            j = min(hi, i + chunk)
+            buf, b0, _ = synth.fill_range(cfg, seed, self.desc_full, i, j)
+            s = max(i, lo)
+            rel = off_full[s:j] - b0
+            lens = ln_full[s:j]
+            self.run.upload_data(buf[int(rel[0]):int(rel[-1] + lens[-1])], int(off_full[s]) - base)
+            start = off_full[s:j] - base
+            w = np.minimum(lens, 128)
+            self.win_bytes += int(w.sum())
+            k, need_last = unique_lines(start, header_need(buf, rel, lens), need_last)
+            self.need_lines += k
+            if wl.get("payload"):
+                self.payload_extra += payload_extra_bytes(buf, rel, lens)
+            i = j
+
+    def cpu_sample(self, wl, seed, n_sample):
+        """The first n_sample packets of the same capture, for the CPU baseline."""
+        m = min(n_sample, len(self.desc_full))
+        buf, b0, nb = synth.fill_range(wl["cfg"], seed, self.desc_full, 0, m)
+        d = self.desc_full[:m]
+        return buf[:nb + 16].copy(), synth.make_desc(synth.desc_off(d) - b0, synth.desc_len(d))
+
+
+def payload_extra_bytes(buf, rel, lens) -> int:
     """Bytes a PAYLOAD slot reads beyond the 128-B header window: applyPayloadFilter's
     window is [14 + 4*IHL, +min(len - that, 100)) of IPv4 frames (src/PacketFilter.cpp:293-309)."""
-    off = synth.desc_off(desc).astype(np.int64)
-    ln = synth.desc_len(desc).astype(np.int64)
-    ok = ln >= 34
-    idx = np.minimum(off + 14, len(data) - 1)
-    ipv4 = ok & (data[np.minimum(off + 12, len(data) - 1)] == 8) & (data[np.minimum(off + 13, len(data) - 1)] == 0)
-    po = 14 + (data[idx].astype(np.int64) & 15) * 4
-    end = np.minimum(ln, po + 100)
-    extra = np.where(ipv4 & (ln > po), np.maximum(0, end - 128), 0)
-    return float(extra.sum())
+    ok = lens >= 34
+    ipv4 = ok & (buf[rel + 12] == 8) & (buf[rel + 13] == 0)
+    po = 14 + (buf[rel + 14].astype(np.int64) & 15) * 4
+    end = np.minimum(lens, po + 100)
+    return int(np.where(ipv4 & (lens > po), np.maximum(0, end - 128), 0).sum())
 
 
 def main_kernel_name(wl, flags: int = 0) -> str:
-    """The main-kernel variant launch_main picks (bt_kernels.hip launch_t): descriptor
-    mode with packed tiled records (or none) and non-temporal record stores runs the
-    counted-wait pipeline unless BT_NO_PIPE is set or prefetch is off; everything else
-    runs bt_parse_filter_main."""
+    """The main-kernel variant launch_main picks (bt_kernels.hip launch_t)."""
     no_pipe = os.environ.get("BT_NO_PIPE", "") not in ("", "0")
     layout = flags & (abi.OPT_RECORDS_AOS | abi.OPT_RECORDS_PLANES)
     nt_stores = not (flags & abi.OPT_CACHE_DEFAULT) or (flags & abi.OPT_NT_STORES)
@@ -80,54 +219,175 @@ def main_kernel_name(wl, flags: int = 0) -> str:
     return "bt_parse_filter_pipe" if pipe else "bt_parse_filter_main"
 
 
-def algorithmic_bytes(desc: np.ndarray, fixed: bool, rec_bytes: float, filt: bool) -> float:
-    """Bytes the main kernel must move per launch (SURVEY.md §8(d) formula, R = the
-    packed record's stored slabs, counted from this run's records):
-    min(len,128) header read + 8 B descriptor (0 for fixed stride) + R
-    + 1 B decision + 1/8 B verdict bit (the ordered pass-index list is written by the
-    compaction kernels and is not counted here)."""
-    n = len(desc)
-    lens = synth.desc_len(desc)
-    b = float(np.minimum(lens, 128).sum())
-    if not fixed:
-        b += 8.0 * n
-    b += rec_bytes
+def record_write_stats(run) -> tuple[int, int]:
+    """(record bytes stored, 128-B lines they fill) from this run's tiled records: slabs
+    0-1 at every slot (2 KiB per tile), slab k >= 2 packed to the front of its region."""
+    rec = run.d_rec.download(np.zeros(run.d_rec.nbytes, np.uint8))
+    nt = (run.n + 63) // 64
+    ok = rec[: nt * 6 * 1024].reshape(nt, 6, 64, 16)[:, 1, :, 1].astype(np.int64)
+    nd = 5 + ((ok & abi.L_VLAN0) != 0) + ((ok & abi.L_VLAN1) != 0) + \
+        np.where(ok & abi.L_IPV4, 5, np.where(ok & abi.L_IPV6, 10, 0)) + \
+        np.where(ok & abi.L_TCP, 5, np.where(ok & (abi.L_UDP | abi.L_ICMP), 2, 0))
+    ns = (nd + 3) // 4
+    live = (np.arange(nt * 64).reshape(nt, 64) < run.n)
+    ns = np.where(live, ns, 0)
+    stored = int(ns.sum()) * 16
+    lines = nt * 2 * (1024 // LINE)
+    for k in range(2, 6):
+        cnt = (ns > k).sum(axis=1)
+        lines += int(((cnt * 16 + LINE - 1) // LINE).sum())
+    return stored, lines
+
+
+def load_traffic(path, key, n):
+    """Per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py), if the
+    committed figure was measured on these kernel sources and this batch size."""
+    if not os.path.exists(path):
+        return None, "no profiles/traffic.json"
+    try:
+        with open(path) as fh:
+            rec = json.load(fh).get(key)
+    except (OSError, ValueError) as e:
+        return None, f"unreadable: {e}"
+    if not rec:
+        return None, f"no PMC measurement for {key}"
+    if rec.get("packets") != n:
+        return None, f"measured at {rec.get('packets')} packets, not {n}"
+    sha = kernel_source_sha()
+    if rec.get("kernel_src_sha") != sha:
+        return None, f"stale: measured on kernel sources {rec.get('kernel_src_sha')}, these are {sha}"
+    return rec, os.path.relpath(path, ROOT)
+
+
+def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
+    """GPU half of one workload: build, warm up, time K steps. Returns this rank's
+    results (the CPU baseline and the cross-rank max are filled in by the caller)."""
+    seed = synth.SEEDS[wl["cfg"]] + (0 if strong else rank)
+    n_job = args.packets if strong else args.packets * world
+    if strong:
+        d_all, _ = synth.layout(wl["cfg"], args.packets, seed)
+        lo, hi = shard.shard_bounds(synth.desc_len(d_all), world)[rank]
+        n_total = args.packets
+        del d_all
+    else:
+        lo, hi, n_total = 0, args.packets, args.packets
+    cap = Capture(ctx, wl, n_total, seed, lo, hi)
+    run, n = cap.run, cap.n
+    filt = wl["filters"] is not None
     if filt:
-        b += n * (1.0 + 1.0 / 8.0)
-    return b
+        prog = ctx.compile(wl["filters"])
+        if wl.get("payload") and abi.KINDS[prog[0].kind] != "PAYLOAD":
+            sys.exit(f"--payload {wl['payload']!r} is not GPU-compilable (kind {abi.KINDS[prog[0].kind]})")
+    for _ in range(args.warmup):
+        run.run()
+    ctx.time_device_ex(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
+    n_pass = run.n_pass() if filt else 0
+    rec_bytes, rec_lines = record_write_stats(run) if wl["parse"] and n else (0, 0)
+    # A few untimed steps right before the timed region, so the GPU does not sit idle
+    # through the host work above between warm-up and t0 (they are drained by the sync).
+    for _ in range(2):
+        run.run()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    tm = ctx.time_device_ex(run.batch, run.outs, args.steps)
+    ta = time.perf_counter()
+    ctx.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    step_s = (t1 - t0) / args.steps
+
+    # algorithmic bytes of one main-kernel launch (SURVEY §8(d), R = the stored slabs):
+    # min(len,128) header read + 8 B descriptor (0 for fixed stride) + R + 1 B decision
+    # + 1/8 B verdict bit; the compaction kernels' pass_idx is not the main kernel's
+    algo = cap.win_bytes + (0 if wl["fixed"] else 8 * n) + rec_bytes + (n * 1.125 if filt else 0)
+    algo += cap.payload_extra
+    # the 128-B-line floor of what the walk must touch: header lines + descriptors +
+    # record lines + decisions + verdict words
+    floor_read = cap.need_lines * LINE + (0 if wl["fixed"] else 8 * n)
+    floor_write = rec_lines * LINE + ((n + (n + 63) // 64 * 8) if filt else 0)
+    main_ms = tm.main_ms
+    mine = {"step_s": step_s, "main_ms": main_ms, "n": n, "algo": algo, "pass": n_pass,
+            "host_ms": 1e3 * (ta - t0), "tail_ms": 1e3 * (t1 - ta)}
+    ranks = [mine]
+    if dist is not None:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    step_max = max(r["step_s"] for r in ranks)
+    kms_max = max(r["main_ms"] for r in ranks)
+    value = n_job / step_max / 1e6
+    achieved = algo / (main_ms * 1e-3) / 1e9
+    key = name if not wl.get("payload") else None
+    traffic_rec, traffic_src = load_traffic(args.traffic_json, key, n) if key else (None, "PAYLOAD variant")
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic_rec["traffic"] if traffic_rec else None,
+            "traffic_source": traffic_src,
+            "traffic_bytes_per_packet": round(traffic_rec["traffic"] / n, 2) if traffic_rec else None,
+            "traffic_floor": floor_read + floor_write,
+            "traffic_floor_bytes_per_packet": round((floor_read + floor_write) / max(n, 1), 2),
+            "traffic_floor_read_per_packet": round(floor_read / max(n, 1), 2),
+            "traffic_floor_write_per_packet": round(floor_write / max(n, 1), 2),
+            "kernel": main_kernel_name(wl, flags), "kernel_ms": round(main_ms, 4),
+            "kernel_ms_min": round(tm.main_min_ms, 4), "kernel_ms_max": round(tm.main_max_ms, 4),
+            "algorithmic_bytes_per_packet": round(algo / max(n, 1), 2),
+            "record_bytes_per_packet": round(rec_bytes / max(n, 1), 2),
+            "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),
+            "gpu_span_ms_per_step": round(tm.span_ms / args.steps, 4)}
+    if traffic_rec:
+        roof["traffic_read_per_packet"] = traffic_rec.get("read_per_packet")
+        roof["traffic_write_per_packet"] = traffic_rec.get("write_per_packet")
+    timing = tm.as_dict()
+    timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4), "host_call_ms": round(mine["host_ms"], 4),
+                   "tail_sync_ms": round(mine["tail_ms"], 4),
+                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None})
+    out = {"workload": wl["name"], "value": round(value, 2), "unit": "Mpps", "ms_per_step": round(step_max * 1e3, 4),
+           "scaling": "strong" if strong else "weak", "packets_per_gpu": n, "packets_total": n_job,
+           "pass_fraction": round(n_pass / n, 4) if filt and n else None, "roofline": roof, "timing": timing}
+    if world > 1:
+        out["per_rank"] = [{"rank": i, "packets": r["n"], "ms_per_step": round(r["step_s"] * 1e3, 4),
+                            "kernel_ms": round(r["main_ms"], 4),
+                            "frac": round(r["algo"] / (r["main_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                           for i, r in enumerate(ranks)]
+        out["kernel_ms_max_over_ranks"] = round(kms_max, 4)
+    sample = cap.cpu_sample(wl, seed, args.cpu_sample) if rank == 0 and not args.no_cpu else None
+    run.free()
+    return out, sample
 
 
-def cpu_baseline(data, desc, wl, n_sample, seconds):
-    """The reference's own parser + PacketFilter (oracle/_ref) on the host cores, on a
-    bounded sample of the same capture; falls back to the C oracle port."""
+def cpu_baseline(sample, wl, seconds, cpus):
+    """The reference's own parser + PacketFilter (oracle/_ref) on the host CPUs, on a
+    bounded sample of the same capture; the C oracle port where _ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol  # checker/baseline only
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
-    sub = desc[:n_sample]
+    data, sub = sample
+    threads = cpus["threads"]
     filters = wl["filters"] or []
     if ol.ref_available():
-        done, el = ol.ref_bench(data, sub, len(sub), filters, parse=wl["parse"], threads=threads,
-                                seconds=seconds)
+        done, el = ol.ref_bench(data, sub, len(sub), filters, parse=wl["parse"], threads=threads, seconds=seconds)
         kind = "reference"
     else:
         t0 = time.perf_counter()
         done = 0
         while time.perf_counter() - t0 < seconds:
-            ol.oracle_run(data, sub, len(sub), filters if filters else None, parse=wl["parse"],
-                          threads=threads)
+            ol.oracle_run(data, sub, len(sub), filters if filters else None, parse=wl["parse"], threads=threads)
             done += len(sub)
         el = time.perf_counter() - t0
         kind = "port"
     what = ("ProtocolParser::parsePacket per walked layer" if wl["parse"] else "") + \
            (" + PacketFilter::applyFilters" if filters else "")
     return {"value": round(done / el / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": kind,
+            "cpu_model": cpus["model"], "affinity_cpus": cpus["affinity_cpus"],
+            "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
             "sample": f"first {len(sub)} packets of the same capture, repeated for {el:.1f}s; "
-                      f"{what.strip()}; {threads} std::threads, per-thread instances, disjoint shards"}
+                      f"{what.strip()}; {threads} std::threads (one per usable host CPU), per-thread "
+                      f"instances, disjoint shards"}
 
 
 def main():
@@ -135,20 +395,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default="c2f", choices=sorted(WORKLOADS), help="the headline workload")
+    ap.add_argument("--configs", default="auto",
+                    help="comma list of extra workloads for the `configs` object (suffix _strong: strong "
+                         "scaling), 'none', or 'auto' (N=1: c2,c3,c4; N>1: c3,c3_strong)")
     ap.add_argument("--packets", type=int, default=1 << 24)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 18)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--grid-waves", type=int, default=0, help="persistent grid size in wavefronts (0 = auto)")
     ap.add_argument("--no-prefetch", action="store_true", help="A/B: disable the next-tile load prefetch")
     ap.add_argument("--flags", type=int, default=None, help="raw bt_opts.flags (A/B experiments)")
     ap.add_argument("--payload", default=None,
-                    help="c3/c4: put a PAYLOAD regex FIRST in the filter program (every IPv4 packet runs the "
-                         "GPU DFA: worst case); reported in config, not the default workload")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling (C5): --packets is the whole job, split across the ranks in "
-                         "tile-aligned, byte-balanced contiguous shards (beatrice_amd/shard.py)")
+                    help="put a PAYLOAD regex FIRST in the headline's filter program (every IPv4 packet runs "
+                         "the GPU DFA: worst case); reported in config, not the default workload")
+    ap.add_argument("--strong", action="store_true", help="the headline as strong scaling (C5's other half)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -160,117 +421,68 @@ def main():
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
-    wl = WORKLOADS[args.config]
-    n_job = args.packets * (1 if args.strong else world)
-    if args.strong:
-        # every rank generates the same capture and keeps its own shard, rebased
-        data, desc = synth.capture(wl["cfg"], args.packets, seed=synth.SEEDS[wl["cfg"]])
-        lo, hi = shard.shard_bounds(synth.desc_len(desc), world)[rank]
-        if wl["fixed"]:
-            data, desc = np.ascontiguousarray(data[lo * 64:hi * 64]), desc[lo:hi]
-        else:
-            data, desc = shard.local_batch(data, desc, lo, hi)
-    else:
-        data, desc = synth.capture(wl["cfg"], args.packets, seed=synth.SEEDS[wl["cfg"]] + rank)
-    n = len(desc)
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
-    flags |= abi.OPT_SPIN_SYNC   # the timed region's end is not delayed by a sleeping host thread
+    flags |= abi.OPT_SPIN_SYNC   # host waits spin: no wake-up latency inside the timed region
     # BT_BENCH_DEVICE: put every rank on one device (multi-rank rehearsal on a 1-GPU box)
     device = int(os.environ.get("BT_BENCH_DEVICE", local))
     ctx = abi.Context(device, grid_waves=args.grid_waves, flags=flags)
+
+    head = dict(WORKLOADS[args.config])
     if args.payload is not None:
-        if not wl["filters"]:
-            sys.exit("--payload needs a filtering workload (c3 / c4)")
-        wl = dict(wl, filters=[{"type": abi.PAYLOAD, "expr": args.payload, "priority": 9}] + wl["filters"],
-                  name=wl["name"] + f" + PAYLOAD /{args.payload}/ first")
-    if wl["filters"]:
-        prog = ctx.compile(wl["filters"])
-        if args.payload is not None and abi.KINDS[prog[0].kind] != "PAYLOAD":
-            sys.exit(f"--payload {args.payload!r} is not GPU-compilable (kind {abi.KINDS[prog[0].kind]})")
-    filt = wl["filters"] is not None
-    run = abi.DeviceRun(ctx, data, None if wl["fixed"] else desc, n, stride=64 if wl["fixed"] else 0,
-                        records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt)
-    for _ in range(args.warmup):
-        run.run()
-    ctx.time_device(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
-    n_pass = run.n_pass() if filt else 0
-    rec_bytes = 16.0 * run.record_slabs() if wl["parse"] else 0.0   # packed records: slabs stored
-    # Two more untimed steps right before the timed region: an idle GPU (host-side work
-    # between warm-up and t0) was measured to start the first timed kernel up to ~27 ms
-    # late in 3 of 8 processes, with the device-side span unchanged.
-    for _ in range(2):
-        run.run()
+        if not head["filters"]:
+            sys.exit("--payload needs a filtering workload")
+        head.update(filters=[{"type": abi.PAYLOAD, "expr": args.payload, "priority": 9}] + head["filters"],
+                    name=head["name"] + f" + PAYLOAD /{args.payload}/ first", payload=args.payload)
+    if args.configs == "auto":
+        extra = ["c2", "c3", "c4"] if world == 1 else ["c3", "c3_strong"]
+    elif args.configs == "none":
+        extra = []
+    else:
+        extra = [c for c in args.configs.split(",") if c]
+    extra = [c for c in extra if c != args.config or (args.strong != c.endswith("_strong"))]
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    ms_iter, main_ms = ctx.time_device(run.batch, run.outs, args.steps)
-    ta = time.perf_counter()
-    ctx.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    if os.environ.get("BT_DEBUG_TIMING"):
-        print(f"[bench] time_device {1e3 * (ta - t0):.3f} ms, sync+barrier {1e3 * (t1 - ta):.3f} ms", file=sys.stderr)
-    step_s = (t1 - t0) / args.steps
-    if dist is not None:
-        import torch
-        t = torch.tensor([step_s, main_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        step_s, main_ms = float(t[0]), float(t[1])
-    value = n_job / step_s / 1e6
-
-    algo = algorithmic_bytes(desc, wl["fixed"], rec_bytes, filt)
-    if args.payload is not None:
-        algo += payload_extra_bytes(data, desc)
-    achieved = algo / (main_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    if os.path.exists(args.traffic_json):   # rocprofv3 PMC passes of this kernel (tools/pmc_traffic.py)
-        try:
-            with open(args.traffic_json) as fh:
-                rec = json.load(fh).get(args.config)
-            if rec and rec.get("packets") == n:
-                traffic = rec["traffic"]
-                traffic_src = os.path.relpath(args.traffic_json, ROOT)
-        except Exception:
-            traffic = None
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(data, desc, wl, args.cpu_sample, args.cpu_seconds)
+    results, samples = {}, {}
+    jobs = [("__head__", args.config, head, args.strong)] + \
+           [(c, c.replace("_strong", ""), dict(WORKLOADS[c.replace("_strong", "")]), c.endswith("_strong"))
+            for c in extra]
+    for key, name, wl, strong in jobs:
+        res, sample = measure(name, wl, args, ctx, flags, dist, rank, world, strong)
+        results[key] = res
+        samples[key] = (sample, wl)
+    cpus = host_cpus()
+    if rank == 0 and not args.no_cpu:
+        for key, (sample, wl) in samples.items():
+            if sample is not None and not (key != "__head__" and results[key]["scaling"] == "strong"):
+                results[key]["cpu_baseline"] = cpu_baseline(sample, wl, args.cpu_seconds, cpus)
+            else:
+                results[key]["cpu_baseline"] = None
 
     if rank == 0:
+        h = results.pop("__head__")
         line = {
             "metric": METRIC,
-            "value": round(value, 2),
+            "value": h["value"],
             "unit": "Mpps",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(step_s * 1e3, 4),
+            "ms_per_step": h["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": h["scaling"],
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64)",
-            "config": {"workload": wl["name"], "packets_per_gpu": n, "packets_total": n_job,
-                       "parallelism": f"batch split x{world}",
-                       "pass_fraction": round(n_pass / n, 4) if filt else None},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": main_kernel_name(wl, flags), "kernel_ms": round(main_ms, 4),
-                         "algorithmic_bytes_per_packet": round(algo / n, 2),
-                         "record_bytes_per_packet": round(rec_bytes / n, 2),
-                         "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),
-                         "gpu_span_ms_per_step": round(ms_iter, 4)},
-            "cpu_baseline": cpu,
+            "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64, streamed to HBM)",
+            "config": {"workload": h["workload"], "packets_per_gpu": h["packets_per_gpu"],
+                       "packets_total": h["packets_total"], "parallelism": f"batch split x{world}",
+                       "pass_fraction": h["pass_fraction"]},
+            "roofline": h["roofline"],
+            "cpu_baseline": h.get("cpu_baseline"),
+            "timing": h["timing"],
         }
+        if "per_rank" in h:
+            line["per_rank"] = h["per_rank"]
+        line["configs"] = results
         print(json.dumps(line), flush=True)
-    run.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -445,6 +445,28 @@ int  bt_synchronize(bt_ctx* ctx);
  * main_ms is -1 (HIP does not time events recorded inside a graph). */
 int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
                     uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
+/* The same with a breakdown of where the host's wall time goes (bench.py puts it in its
+ * JSON line). The host waits by polling hipEventQuery (no interrupt wake-up): the time
+ * until the first event is seen complete and from there until the last one are
+ * reported separately, so a late start on the GPU and a late completion notice can be
+ * told apart. */
+typedef struct bt_timing {
+    float span_ms;                 /* GPU: event before the first step -> after the last */
+    float main_ms;                 /* mean main-kernel time (its own dispatch events)     */
+    float main_min_ms, main_max_ms;
+    float lead_ms;                 /* GPU: first event -> first main kernel's start       */
+    float gap_ms;                  /* GPU: sum over steps of (next main start - main end) */
+    double enqueue_ms;             /* host: all launches enqueued                         */
+    double first_seen_ms;          /* host: enqueue done -> first event seen complete     */
+    double last_seen_ms;           /* host: first event seen -> last event seen           */
+    double query_ms;               /* host: elapsed-time queries                          */
+    double wall_ms;                /* host: the whole call                                */
+    int32_t spin_rc;               /* hipSetDeviceFlags(spin) result at bt_create, -1 unset */
+    uint32_t device_flags;         /* hipGetDeviceFlags after bt_create                   */
+    uint32_t reserved[6];
+} bt_timing;
+int  bt_time_device_ex(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t iters,
+                       bt_timing* timing);
 
 /* ---- text output --------------------------------------------------------------
  * The text the reference's ParseResult formatters print for every walked layer of

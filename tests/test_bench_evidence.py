@@ -1,14 +1,15 @@
 """CPU: the bench contract and the committed evidence agree with each other.
 
-* bench.py's helpers: the algorithmic-bytes formula and the name of the
-  main-kernel variant it reports;
+* bench.py's helpers: the 128-B-line traffic floor (distinct lines of the walked header
+  windows), the host-CPU count of the CPU baseline, range-by-range capture streaming, and
+  the name of the main-kernel variant it reports;
 * every committed bench line (profiles/r01/bench_*.json) carries the contract's keys, and
   its roofline numbers follow from its own fields (achieved = algorithmic bytes x packets
   / kernel time, frac = achieved / peak);
 * the rocprofv3 kernel stats committed beside it (profiles/r01/*_kernel_stats.csv) agree
   with the bench's own event timing of the same command within 5 %, and name the kernel
   the bench line names;
-* the PMC traffic the bench lines quote is the one in profiles/traffic.json.
+* the PMC traffic the bench lines quote is the round's committed figure.
 """
 import csv
 import json
@@ -32,14 +33,40 @@ def _line(path):
         return [json.loads(x) for x in fh if x.startswith("{")][-1]
 
 
-def test_algorithmic_bytes_formula():
-    data, desc = synth.capture(synth.C3, 1000, seed=3)
-    lens = synth.desc_len(desc).astype(np.int64)
-    got = bench.algorithmic_bytes(desc, fixed=False, rec_bytes=58.0 * 1000, filt=True)
-    want = np.minimum(lens, 128).sum() + 8 * 1000 + 58.0 * 1000 + 1000 * 1.125
-    assert got == pytest.approx(want)
-    got = bench.algorithmic_bytes(desc, fixed=True, rec_bytes=0.0, filt=False)
-    assert got == pytest.approx(np.minimum(lens, 128).sum())
+def test_unique_lines_and_header_need():
+    # lines shared by neighbouring frames count once; a range split across calls counts the same
+    start = np.array([0, 64, 100, 300, 1000], np.int64)
+    nb = np.array([64, 64, 0, 10, 129], np.int64)
+    assert bench.unique_lines(start, nb) == (1 + 0 + 1 + 2, 8)   # lines 0 | (0) | 2 | 7, 8
+    a, p = bench.unique_lines(start[:2], nb[:2])
+    b, _ = bench.unique_lines(start[2:], nb[2:], p)
+    assert a + b == 4
+    # header_need follows the kernel's walk: C2 Eth/IPv4/UDP = 14 + 20 + 20 (floor 38)
+    data, desc = synth.capture(synth.C2, 64)
+    buf = np.concatenate([data, np.zeros(128, np.uint8)])
+    need = bench.header_need(buf, synth.desc_off(desc), synth.desc_len(desc))
+    assert (need == 54).all()
+    data, desc = synth.capture(synth.C4, 4096)
+    buf = np.concatenate([data, np.zeros(128, np.uint8)])
+    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+    need = bench.header_need(buf, off, ln)
+    assert (need >= np.minimum(38, ln)).all() and (need <= np.minimum(ln, 122)).all()
+
+
+def test_host_cpus_reports_affinity_and_quota():
+    c = bench.host_cpus()
+    assert c["threads"] >= 1 and c["threads"] <= c["affinity_cpus"]
+    if c["cgroup_quota_cpus"] is not None:
+        assert c["threads"] <= max(1, int(c["cgroup_quota_cpus"]))
+
+
+def test_fill_range_streams_the_same_capture():
+    for cfg in (synth.C3, synth.C4):
+        data, desc = synth.capture(cfg, 70000)
+        off, ln = synth.desc_off(desc), synth.desc_len(desc)
+        buf, b0, nb = synth.fill_range(cfg, synth.SEEDS[cfg], desc, 65536, 70000)
+        assert b0 == off[65536] and nb == off[-1] + ln[-1] - b0
+        assert (buf[:nb] == data[b0:b0 + nb]).all()
 
 
 def test_main_kernel_name(monkeypatch):
@@ -74,8 +101,8 @@ def test_committed_bench_line_is_consistent(cfg):
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
     c = d["cpu_baseline"]
     assert c["kind"] in ("reference", "port") and c["cores"] >= 1 and c["value"] > 0
-    # the PMC traffic quoted is the committed per-launch figure
-    traffic = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[cfg]
+    # the PMC traffic quoted is the round's committed per-launch figure
+    traffic = json.load(open(os.path.join(PROFILES, "traffic.json")))[cfg]
     assert r["traffic"] == traffic["traffic"] and traffic["packets"] == n
 
 

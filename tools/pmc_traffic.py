@@ -10,12 +10,19 @@ FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half the 
 of a wide (16 B/lane) coalesced streaming read, so the corrected read traffic is 2x
 FETCH_SIZE; WRITE_SIZE is exact for 16-B-per-lane streaming stores. Both raw and
 corrected numbers are written; `traffic` (what bench.py reports) is the corrected sum.
+Each figure is keyed with bench.kernel_source_sha() of the sources it was measured on;
+bench.py reports `traffic: null` (with the reason) when the key does not match.
 """
 import argparse
 import csv
 import glob
 import json
 import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (kernel_source_sha: the key bench.py checks the figure against)
 
 KERNEL = "bt_parse_filter_"   # bt_parse_filter_main (fixed stride) or bt_parse_filter_pipe (descriptors)
 
@@ -62,6 +69,9 @@ def main():
         "write": write_b,
         "traffic": 2.0 * fetch_b + write_b,
         "traffic_per_packet": (2.0 * fetch_b + write_b) / a.packets,
+        "read_per_packet": 2.0 * fetch_b / a.packets,
+        "write_per_packet": write_b / a.packets,
+        "kernel_src_sha": bench.kernel_source_sha(),
         "dispatches": [nf, nw],
         "note": "read = 2 x FETCH_SIZE (gfx950 wide-read correction, MI355X_MICROARCH.md HBM section)",
     }
