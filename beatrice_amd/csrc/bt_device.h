@@ -7,10 +7,24 @@
 
 namespace bt {
 
-// Compiled filter slot as the device sees it (16 B; kernel-argument resident).
+// Compiled filter slot as the device sees it (32 B; kernel-argument resident).
+// kind / a / b: the bt_filter_slot fields (PAYLOAD: a = blob offset, b = blob size).
+// mask / lo / span / ctl: the same slot as one uniform predicate over the packet's
+// features (to_device_program), so a program without PAYLOAD slots is evaluated with
+// no per-kind branching:
+//   x1, x2 = the feature pair ctl&3 selects: 0 (src, dst IPv4), 1 (sport, dport),
+//            2 (proto, proto), 3 (pbit, pbit) with pbit = tcp | udp<<1 | icmp<<2
+//   pred   = ((x1 & mask) - lo) <= span  ||  ((x2 & mask) - lo) <= span   (unsigned)
+//   gate   = ctl>>2 & 3: 0 none, 1 IPv4 gate (len >= 34, EtherType 0x0800),
+//            2 IPv4 gate and the TCP/UDP length gate of the port filter
+//   result = !gate ? 0 : ctl>>4 & 3: 0 pred, 1 throw (2), 2 host (3)
 struct DevFilter {
-    uint32_t kind, a, b, pad;
+    uint32_t kind, a, b, ctl;
+    uint32_t mask, lo, span, pad;
 };
+constexpr uint32_t kSelIp = 0, kSelPort = 1, kSelProto = 2, kSelPbit = 3;
+constexpr uint32_t kGateNone = 0, kGateIpv4 = 1, kGateL4 = 2;
+constexpr uint32_t kResPred = 0, kResThrow = 1, kResHost = 2;
 
 struct DevProgram {
     uint32_t n;

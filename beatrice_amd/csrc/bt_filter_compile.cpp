@@ -160,6 +160,29 @@ int compile_filters(const bt_filter_desc* f, uint32_t n, bt_filter_slot* out, ui
     return BT_OK;
 }
 
+// The uniform-predicate form of one slot (bt_device.h DevFilter): every built-in kind
+// is a masked range test over a feature pair, behind one of three gates.
+void uniform_form(const bt_filter_slot& s, DevFilter* d) {
+    auto set = [&](uint32_t sel, uint32_t gate, uint32_t res, uint32_t mask, uint32_t lo, uint32_t span) {
+        d->ctl = sel | (gate << 2) | (res << 4);
+        d->mask = mask;
+        d->lo = lo;
+        d->span = span;
+    };
+    switch (s.kind) {
+    case BT_K_TRUE: set(kSelProto, kGateNone, kResPred, 0u, 0u, ~0u); break;            // 0 - 0 <= ~0
+    case BT_K_BPF: set(kSelPbit, kGateIpv4, kResPred, s.a, 1u, 6u); break;              // pbit & a in 1..7
+    case BT_K_PROTO_EQ: set(kSelProto, kGateIpv4, kResPred, 0xFFu, s.a, 0u); break;     // proto == a
+    case BT_K_PROTO_NZ: set(kSelProto, kGateIpv4, kResPred, 0xFFu, 1u, 254u); break;    // proto in 1..255
+    case BT_K_IP_MASK: set(kSelIp, kGateIpv4, kResPred, s.b, s.a, 0u); break;           // (ip & b) == a
+    case BT_K_PORT: set(kSelPort, kGateL4, kResPred, 0xFFFFu, s.a, s.b - s.a); break;   // a <= port <= b
+    case BT_K_IP_THROW: set(kSelProto, kGateIpv4, kResThrow, 0u, 0u, 0u); break;
+    case BT_K_PORT_THROW: set(kSelProto, kGateL4, kResThrow, 0u, 0u, 0u); break;
+    case BT_K_HOST: case BT_K_PAYLOAD: set(kSelProto, kGateNone, kResHost, 0u, 0u, 0u); break;
+    default: set(kSelProto, kGateNone, kResPred, 0u, 1u, 0u); break;                    // FALSE: 0 - 1 > 0
+    }
+}
+
 void to_device_program(const bt_filter_slot* s, uint32_t n, DevProgram* p) {
     std::memset(p, 0, sizeof(*p));
     p->n = n;
@@ -167,6 +190,8 @@ void to_device_program(const bt_filter_slot* s, uint32_t n, DevProgram* p) {
         p->f[i].kind = s[i].kind;
         p->f[i].a = s[i].a;
         p->f[i].b = s[i].b;
+        // compile_one turns an empty port range (a > b) into FALSE, so span never wraps
+        uniform_form(s[i], &p->f[i]);
     }
 }
 

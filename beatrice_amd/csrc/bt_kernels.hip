@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "bt_device.h"
 
@@ -389,6 +390,10 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
 // priority order with early exit (src/PacketFilter.cpp:57-119), wave-uniform slot by slot
 // until every lane has decided. Returns the decision code (BT_DECIDE_*) and the deciding
 // slot. `lrow` = the lane's LDS row, reused to stage a PAYLOAD window after the parse.
+// F = 1: no PAYLOAD slot in the program: every slot is evaluated in its uniform-predicate
+// form (bt_device.h DevFilter), one straight-line sequence with no per-kind branches.
+// F = 2: the per-kind evaluator and the GPU DFA for PAYLOAD slots.
+template <int F>
 __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const uint8_t* dfa_lds,
                                                   uint32_t* lrow, uint64_t my_off, uint32_t len,
                                                   const uint32_t* w0, bool live, uint32_t& slot) {
@@ -403,6 +408,26 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
     uint32_t code = BT_DECIDE_PASS;
     slot = prog.n ? prog.n - 1u : 0u;
     bool open = live;
+    if constexpr (F == 1) {
+        const uint32_t pbit = (x.proto == 6 ? 1u : 0u) | (x.proto == 17 ? 2u : 0u) | (x.proto == 1 ? 4u : 0u);
+        const bool g4 = x.gate & x.l4_ok;
+        for (uint32_t f = 0; f < prog.n; ++f) {
+            if (__ballot(open) == 0ull) break;
+            const DevFilter& d = prog.f[f];
+            const uint32_t sel = d.ctl & 3u, gm = (d.ctl >> 2) & 3u, rm = (d.ctl >> 4) & 3u;   // uniform
+            const uint32_t x1 = sel == kSelIp ? x.src : sel == kSelPort ? x.sport : sel == kSelProto ? x.proto : pbit;
+            const uint32_t x2 = sel == kSelIp ? x.dst : sel == kSelPort ? x.dport : sel == kSelProto ? x.proto : pbit;
+            const bool pred = (((x1 & d.mask) - d.lo) <= d.span) | (((x2 & d.mask) - d.lo) <= d.span);
+            const bool g = gm == kGateNone ? true : gm == kGateIpv4 ? x.gate : g4;
+            const uint32_t r = !g ? 0u : rm == kResPred ? (pred ? 1u : 0u) : rm == kResThrow ? 2u : 3u;
+            if (open && r != 1u) {
+                code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+                slot = f;
+                open = false;
+            }
+        }
+        return code;
+    }
     uint32_t staged_sh = ~0u;   // payload window not staged yet
     for (uint32_t f = 0; f < prog.n; ++f) {
         if (__ballot(open) == 0ull) break;
@@ -629,7 +654,7 @@ __device__ __forceinline__ bool round_b(const MainArgs& a, uint32_t t, uint32_t 
     return wide;
 }
 
-template <int FIXED_LOG2, int REC, bool FILTER, bool PREFETCH>
+template <int FIXED_LOG2, int REC, int FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
     constexpr uint32_t kRow = row_dw<FIXED_LOG2>();
@@ -639,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     const uint32_t wid = threadIdx.x >> 6;
     uint32_t* img = lds_all + wid * (kWave * kRow);
     const uint32_t* row = img + lane * kRow;
-    if (FILTER && a.dfa_bytes) {   // uniform: the whole block copies the pool once
+    if (FILTER == 2 && a.dfa_bytes) {   // uniform: the whole block copies the pool once
         const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
         for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
         __syncthreads();
@@ -745,7 +770,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
             if (lane == 0) {
@@ -869,7 +894,7 @@ __device__ __forceinline__ void st_b128(const __amdgpu_buffer_rsrc_t& r, uint32_
     __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, NT ? 2 : 0);
 }
 
-template <int REC, bool FILTER>
+template <int REC, int FILTER>
 __device__ __forceinline__ void pad_stores() {   // the prologue's stand-ins for a tile's stores
     const auto r = rsrc_of(g_zero16, 0u);
     const u32x4 z = {0u, 0u, 0u, 0u};
@@ -886,7 +911,7 @@ __device__ __forceinline__ void pad_stores() {   // the prologue's stand-ins for
 // measured slower on C2 (0.369 against 0.340 ms for bt_parse_filter_main without
 // prefetch, at 1-4 blocks/CU): there, a wave's loads in flight during its record stores
 // cost more HBM efficiency than the hidden latency gains.
-template <int REC, bool FILTER, int DW>
+template <int REC, int FILTER, int DW>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevProgram prog) {
     static_assert(REC == kRecTiled || REC == kRecNone, "pipe variant: tiled records or none");
     constexpr uint32_t kRow = kRowDwords;
@@ -896,7 +921,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
     uint32_t* img = lds_all + wid * (kWave * kRow);
     const uint32_t* row = img + lane * kRow;
-    if (FILTER && a.dfa_bytes) {
+    if (FILTER == 2 && a.dfa_bytes) {
         const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
         for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
         __syncthreads();
@@ -974,7 +999,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
@@ -1124,17 +1149,21 @@ bool use_pipe() {
     return on;
 }
 
-template <int FL, int REC, bool F>
+template <int FL, int REC, int F>
 void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipStream_t st, hipEvent_t e0,
               hipEvent_t e1) {
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t dyn = F ? (a.dfa_bytes + 15u) & ~15u : 0u;
+    const uint32_t dyn = F == 2 ? (a.dfa_bytes + 15u) & ~15u : 0u;
     auto go = [&](auto kernel, int resident) {
         int g = grid > 0 ? grid : resident;
-        // Fixed stride: two blocks (8 waves) per CU. C2 measured 0.416 ms at the
-        // residency (7 blocks/CU), 0.403 at 3, 0.387 at 2, 0.56 at 1 (4 processes each):
-        // fewer concurrent read and write streams suit HBM better here.
-        if (FL >= 0 && grid <= 0) g = std::min(g, 2 * cu_count());
+        // Fixed stride: two blocks (8 waves) per CU parse-only, four with a filter. C2
+        // measured 0.416 ms at the residency (7 blocks/CU), 0.403 at 3, 0.387 at 2, 0.56
+        // at 1 (4 processes each): fewer concurrent read and write streams suit HBM
+        // better. With the filter (its decision / verdict stores and the slot loop per
+        // tile) the 64-B parse+filter headline measured 0.462 ms at 2 blocks/CU, 0.391 at
+        // 3, 0.379 at 4, 0.44 at 5, 0.40 at 6, 0.375 at 7 (2 passes each): 4 keeps every
+        // wave on exactly 64 tiles of a 16M batch.
+        if (FL >= 0 && grid <= 0) g = std::min(g, (F ? 4 : 2) * cu_count());
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
         if (e0 || e1)
             hipExtLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, e0, e1, 0, a, prog);
@@ -1150,22 +1179,29 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
             return;
         }
     }
-    if (pf && FL < 0) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
+    static const bool fixed_pf = [] {   // A/B: next-tile prefetch in fixed-stride mode
+        const char* e = getenv("BT_FIXED_PREFETCH");
+        return e && *e && *e != '0';
+    }();
+    if (pf && (FL < 0 || fixed_pf)) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
     else go(bt_parse_filter_main<FL, REC, F, false>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn));
 }
 
 template <int FL>
-void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, bool f, int grid, bool pf, hipStream_t st,
+void launch_fl(const MainArgs& a, const DevProgram& prog, int rec, int f, int grid, bool pf, hipStream_t st,
                hipEvent_t e0, hipEvent_t e1) {
-    if (rec == kRecPlanes) {
-        if (f) launch_t<FL, kRecPlanes, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecPlanes, false>(a, prog, grid, pf, st, e0, e1);
-    } else if (rec == kRecTiled) {
-        if (f) launch_t<FL, kRecTiled, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecTiled, false>(a, prog, grid, pf, st, e0, e1);
-    } else if (rec == kRecAoS) {
-        if (f) launch_t<FL, kRecAoS, true>(a, prog, grid, pf, st, e0, e1); else launch_t<FL, kRecAoS, false>(a, prog, grid, pf, st, e0, e1);
-    } else {
-        launch_t<FL, kRecNone, true>(a, prog, grid, pf, st, e0, e1);
-    }
+    // f: 0 no filter, 1 built-in slots only (uniform predicates), 2 with PAYLOAD slots
+    auto by_f = [&](auto rec_c) {
+        constexpr int R = decltype(rec_c)::value;
+        if (f == 2) launch_t<FL, R, 2>(a, prog, grid, pf, st, e0, e1);
+        else if (f == 1) launch_t<FL, R, 1>(a, prog, grid, pf, st, e0, e1);
+        else launch_t<FL, R, 0>(a, prog, grid, pf, st, e0, e1);
+    };
+    if (rec == kRecPlanes) by_f(std::integral_constant<int, kRecPlanes>{});
+    else if (rec == kRecTiled) by_f(std::integral_constant<int, kRecTiled>{});
+    else if (rec == kRecAoS) by_f(std::integral_constant<int, kRecAoS>{});
+    else if (f == 2) launch_t<FL, kRecNone, 2>(a, prog, grid, pf, st, e0, e1);
+    else launch_t<FL, kRecNone, 1>(a, prog, grid, pf, st, e0, e1);
 }
 
 }  // namespace
@@ -1185,12 +1221,14 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
     // Next-tile prefetch: the pipe kernel always prefetches (BT_OPT_NO_PREFETCH selects
     // bt_parse_filter_main without it). In bt_parse_filter_main it pays for descriptor
     // mode (+3 % C3) but not for fixed stride (-16 % C2); launch_t drops it there.
+    // the filter variant: none, built-in slots only, or with PAYLOAD DFAs
+    const int f = !filter ? 0 : a.dfa_bytes ? 2 : 1;
     switch (fl) {
-    case 0: launch_fl<0>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
-    case 1: launch_fl<1>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
-    case 2: launch_fl<2>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
-    case 3: launch_fl<3>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
-    default: launch_fl<-1>(a, prog, rec_layout, filter, grid, prefetch, st, e0, e1); break;
+    case 0: launch_fl<0>(a, prog, rec_layout, f, grid, prefetch, st, e0, e1); break;
+    case 1: launch_fl<1>(a, prog, rec_layout, f, grid, prefetch, st, e0, e1); break;
+    case 2: launch_fl<2>(a, prog, rec_layout, f, grid, prefetch, st, e0, e1); break;
+    case 3: launch_fl<3>(a, prog, rec_layout, f, grid, prefetch, st, e0, e1); break;
+    default: launch_fl<-1>(a, prog, rec_layout, f, grid, prefetch, st, e0, e1); break;
     }
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }

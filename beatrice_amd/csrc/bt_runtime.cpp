@@ -769,16 +769,22 @@ int bt_dev_free(bt_ctx* c, void* p) {
     return BT_OK;
 }
 
+// Both copies are ordered on the context stream and complete before returning: a
+// pageable hipMemcpy on the null stream may return once the source is staged, and it is
+// not ordered with the context's non-blocking stream.
 int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
-    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return BT_OK;
 }
 
 int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return BT_OK;
 }
 

@@ -168,8 +168,10 @@ class Capture:
         self.desc = synth.make_desc(off_full[lo:hi] - base, ln_full[lo:hi])
         self.stride = 64 if wl["fixed"] else 0
         filt = wl["filters"] is not None
+        outs = wl.get("outputs") or ("records", "decide", "verdict", "pass_idx")   # A/B: --outputs
         self.run = abi.DeviceRun(ctx, None, None if wl["fixed"] else self.desc, n, stride=self.stride,
-                                 records=wl["parse"], decide=filt, verdict=filt, pass_idx=filt,
+                                 records=wl["parse"] and "records" in outs, decide=filt and "decide" in outs,
+                                 verdict=filt and "verdict" in outs, pass_idx=filt and "pass_idx" in outs,
                                  data_bytes=nbytes)
         self.win_bytes = 0        # sum of min(len, 128)
         self.need_lines = 0       # distinct 128-B lines of [off, off + header_need)
@@ -282,7 +284,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
         run.run()
     ctx.time_device_ex(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
     n_pass = run.n_pass() if filt else 0
-    rec_bytes, rec_lines = record_write_stats(run) if wl["parse"] and n else (0, 0)
+    rec_bytes, rec_lines = record_write_stats(run) if run.d_rec is not None and n else (0, 0)
     # A few untimed steps right before the timed region, so the GPU does not sit idle
     # through the host work above between warm-up and t0 (they are drained by the sync).
     for _ in range(2):
@@ -410,6 +412,8 @@ def main():
                     help="put a PAYLOAD regex FIRST in the headline's filter program (every IPv4 packet runs "
                          "the GPU DFA: worst case); reported in config, not the default workload")
     ap.add_argument("--strong", action="store_true", help="the headline as strong scaling (C5's other half)")
+    ap.add_argument("--outputs", default=None,
+                    help="A/B only: comma list of the headline's outputs (records,decide,verdict,pass_idx)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -428,6 +432,8 @@ def main():
     ctx = abi.Context(device, grid_waves=args.grid_waves, flags=flags)
 
     head = dict(WORKLOADS[args.config])
+    if args.outputs is not None:
+        head.update(outputs=tuple(args.outputs.split(",")), name=head["name"] + f" [outputs: {args.outputs}]")
     if args.payload is not None:
         if not head["filters"]:
             sys.exit("--payload needs a filtering workload")

@@ -2,7 +2,7 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for c in ${CFGS:-c2 c3}; do
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/sq_$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > /dev/null 2>&1 || exit 4
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/sq_$c -o run -- python3 bench.py --config $c --configs none --steps 3 --warmup 1 --no-cpu > /dev/null 2>&1 || exit 4
   python3 - $c <<'PY'
 import csv, glob, sys
 c = sys.argv[1]
