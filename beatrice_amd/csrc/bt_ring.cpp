@@ -93,9 +93,20 @@ inline uint32_t prefix_len(const uint8_t* f, uint32_t len) {
 inline void copy_prefix(Chain& ch) {
     const uint32_t m = prefix_len(ch.pend, ch.pend_len);
     if (((uintptr_t)ch.pend_slot & 15u) == 0) {
-        for (uint32_t k = 0; k < m; k += 16) {
+        // whole 16-B chunks of the frame with vector loads; the last partial chunk with
+        // memcpy into a zeroed chunk, so no load reads past the frame (whose end may be
+        // the end of the ring mapping)
+        const uint32_t full = std::min(m, ch.pend_len) & ~15u;
+        uint32_t k = 0;
+        for (; k < full; k += 16) {
             const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k));
             _mm_stream_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k), v);
+        }
+        if (k < m) {
+            alignas(16) uint8_t tail[16] = {};
+            std::memcpy(tail, ch.pend + k, std::min<uint32_t>(16u, ch.pend_len - std::min(ch.pend_len, k)));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k),
+                             _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
         }
     } else {
         std::memcpy(ch.pend_slot, ch.pend, m);

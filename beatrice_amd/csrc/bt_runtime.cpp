@@ -46,6 +46,9 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr uint32_t kHostSlot = 112;   // bytes of each frame staged for the device (>= kNeedParse + pad)
+// ... and with a GPU PAYLOAD slot in the program: applyPayloadFilter's window ends at most
+// at 14 + 60 + 100 = 174 bytes (src/PacketFilter.cpp:293-309), rounded up to 16
+constexpr uint32_t kHostSlotPayload = 176;
 
 struct HostSlot {                      // one half of the double-buffered host pipeline
     hipStream_t stream = nullptr;
@@ -133,8 +136,12 @@ struct bt_ctx {
     std::vector<bt_filter_slot> slots;
     DevProgram prog{};
     std::vector<uint8_t> dfa_pool;     // BT_K_PAYLOAD tables of the current program
-    uint8_t* dfa_dev = nullptr;
-    size_t dfa_cap = 0;
+    // PAYLOAD DFA pools, double-buffered: a recompile writes the buffer no queued launch
+    // uses (dfa_ev[k] is recorded after every launch that reads dfa_dev[k])
+    uint8_t* dfa_dev[2] = {nullptr, nullptr};
+    hipEvent_t dfa_ev[2] = {nullptr, nullptr};
+    bool dfa_used[2] = {false, false};
+    int dfa_cur = 0;
 
     // device workspace for bt_parse_filter_device
     uint32_t ws_cap = 0;
@@ -199,7 +206,12 @@ namespace {
 int ensure_ws(bt_ctx* c, uint32_t n) {
     if (n <= c->ws_cap) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
-    if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
+    // a cached BT_OPT_GRAPH timing graph holds the pointers replaced here
+    if (c->tgraph) { (void)hipGraphExecDestroy(c->tgraph); c->tgraph = nullptr; }
+    if (c->tile_pass) {   // launches queued on any stream may still use the old workspace
+        HIP_TRY(hipDeviceSynchronize());
+        (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict);
+    }
     c->tile_pass = nullptr; c->chunk_sums = nullptr; c->verdict = nullptr; c->ws_cap = 0;
     const uint32_t ntiles = (n + 63) / 64;
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
@@ -245,7 +257,7 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
     a.tile_pass = compact ? c->tile_pass : nullptr;
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
-    a.dfa = c->dfa_dev;
+    a.dfa = c->dfa_dev[c->dfa_cur];
     a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
     // Cache policy (measured, profiles/r01): non-temporal record stores everywhere
     // (C2 +3..9 %), non-temporal header loads in descriptor mode (C3 +15 %, C4 +8 %;
@@ -266,6 +278,10 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     // pair of hipEventRecord around the launch left the GPU idle ~6 us each, per step)
     int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, e1);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (a.dfa_bytes) {   // the pool this launch reads stays untouched until it has run
+        HIP_TRY(hipEventRecord(c->dfa_ev[c->dfa_cur], st));
+        c->dfa_used[c->dfa_cur] = true;
+    }
     if (compact) {
         rc = launch_compact(a.verdict, c->tile_pass, a.ntiles, b->n, c->chunk_sums, o->pass_idx, o->n_pass, st);
         if (rc) return fail(rc, "compaction launch failed");
@@ -287,7 +303,7 @@ void free_host(bt_ctx* c) {
     c->host_ready = false;
 }
 
-size_t in_bytes(uint32_t chunk) { return (size_t)chunk * kHostSlot + (size_t)chunk * 8; }
+size_t in_bytes(uint32_t chunk) { return (size_t)chunk * kHostSlotPayload + (size_t)chunk * 8; }
 size_t out_bytes(uint32_t chunk) { return (size_t)chunk * BT_REC_BYTES + chunk + ((size_t)chunk + 63) / 64 * 8; }
 
 int ensure_host(bt_ctx* c) {
@@ -385,7 +401,10 @@ void bt_destroy(bt_ctx* c) {
     c->pool.reset();
     if (c->tgraph) (void)hipGraphExecDestroy(c->tgraph);
     if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
-    if (c->dfa_dev) (void)hipFree(c->dfa_dev);
+    for (int k = 0; k < 2; ++k) {
+        if (c->dfa_dev[k]) (void)hipFree(c->dfa_dev[k]);
+        if (c->dfa_ev[k]) (void)hipEventDestroy(c->dfa_ev[k]);
+    }
     for (auto e : c->tev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -436,19 +455,22 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
     }
     std::lock_guard<std::mutex> lk(c->mu);
     if (!pool.empty()) {
+        // write the pool into the buffer no queued launch reads: launches on any stream
+        // that still read it (with the old program) are waited for first
         HIP_TRY(hipSetDevice(c->device));
-        if (pool.size() > c->dfa_cap) {
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            if (c->dfa_dev) HIP_TRY(hipFree(c->dfa_dev));
-            c->dfa_dev = nullptr;
-            c->dfa_cap = 0;
-            HIP_TRY(hipMalloc(&c->dfa_dev, kDfaPoolMax));
-            c->dfa_cap = kDfaPoolMax;
+        const int k = c->dfa_cur ^ 1;
+        if (!c->dfa_dev[k]) {
+            HIP_TRY(hipMalloc(&c->dfa_dev[k], kDfaPoolMax));
+            HIP_TRY(hipEventCreateWithFlags(&c->dfa_ev[k], hipEventDisableTiming));
         }
-        // ordered behind work already queued on the context stream
-        HIP_TRY(hipMemcpyAsync(c->dfa_dev, pool.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
+        if (c->dfa_used[k]) HIP_TRY(hipEventSynchronize(c->dfa_ev[k]));
+        HIP_TRY(hipMemcpyAsync(c->dfa_dev[k], pool.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        c->dfa_used[k] = false;
+        c->dfa_cur = k;
     }
+    // a cached BT_OPT_GRAPH timing graph holds the old program: drop it
+    if (c->tgraph) { (void)hipGraphExecDestroy(c->tgraph); c->tgraph = nullptr; }
     c->dfa_pool = std::move(pool);
     c->slots = slots;
     to_device_program(c->slots.data(), m, &c->prog);
@@ -595,7 +617,7 @@ namespace {
 // Host batch pipeline shared by bt_parse_filter (base + descriptors) and
 // bt_parse_filter_ptrs (one pointer per frame): frame(i, &len) returns frame i.
 template <class FrameFn>
-int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_t* verdict, uint8_t* decide,
+int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_t* verdict, uint8_t* decide,
                   uint32_t* pass_idx, uint32_t* n_pass) {
     int rc = ensure_host(c);
     if (rc) return rc;
@@ -607,6 +629,9 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
     if (!ver && (pass_idx || n_pass)) { vtmp.resize(((size_t)n + 63) / 64); ver = vtmp.data(); }
 
     const uint32_t chunk = c->chunk;
+    // bytes staged per frame: the header walk's, or with a GPU PAYLOAD slot in the program
+    // the payload window's too (bytes past the staged prefix would be the next frame's)
+    const uint32_t slot = c->dfa_pool.empty() ? kHostSlot : kHostSlotPayload;
     uint32_t next = 0, k = 0;
     while (next < n || c->hs[0].busy || c->hs[1].busy) {
         HostSlot& s = c->hs[k & 1];
@@ -616,10 +641,10 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
         }
         if (next < n) {
             const uint32_t cnt = std::min(chunk, n - next);
-            // gather the header prefixes (<= kHostSlot bytes) into pinned staging:
+            // gather the header prefixes (<= slot bytes) into pinned staging:
             // per-worker byte counts, exclusive scan, then parallel copies
             uint8_t* pre = s.h_in;
-            uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlot);
+            uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlotPayload);
             const unsigned T = c->pool->size();
             std::vector<uint64_t> part(T + 1, 0);
             const uint32_t base_i = next;
@@ -629,7 +654,7 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
                 for (uint32_t i = a; i < b; ++i) {
                     uint32_t len = 0;
                     (void)frame(base_i + i, &len);
-                    sum += (std::min(len, kHostSlot) + 15) & ~15u;
+                    sum += (std::min(len, slot) + 15) & ~15u;
                 }
                 part[w + 1] = sum;
             });
@@ -640,7 +665,7 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
                 for (uint32_t i = a; i < b; ++i) {
                     uint32_t len = 0;
                     const uint8_t* f = frame(base_i + i, &len);
-                    const uint32_t m = std::min(len, kHostSlot);
+                    const uint32_t m = std::min(len, slot);
                     if (m) std::memcpy(pre + p, f, m);
                     d[i] = BT_DESC(p, len);
                     p += (m + 15) & ~15u;
@@ -649,13 +674,13 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
             const uint64_t pos = part[T];
             const size_t pre_bytes = (pos + 15) & ~15ull;
             if (pre_bytes) HIP_TRY(hipMemcpyAsync(s.d_in, pre, pre_bytes, hipMemcpyHostToDevice, s.stream));
-            HIP_TRY(hipMemcpyAsync(s.d_in + (size_t)chunk * kHostSlot, d, (size_t)cnt * 8, hipMemcpyHostToDevice,
+            HIP_TRY(hipMemcpyAsync(s.d_in + (size_t)chunk * kHostSlotPayload, d, (size_t)cnt * 8, hipMemcpyHostToDevice,
                                    s.stream));
             bt_batch b{};
             b.base = s.d_in;
-            b.desc = reinterpret_cast<const uint64_t*>(s.d_in + (size_t)chunk * kHostSlot);
+            b.desc = reinterpret_cast<const uint64_t*>(s.d_in + (size_t)chunk * kHostSlotPayload);
             b.n = cnt;
-            b.bytes = (uint64_t)chunk * kHostSlot;
+            b.bytes = (uint64_t)chunk * kHostSlotPayload;
             bt_outputs o{};
             uint8_t* drec = s.d_out;
             uint8_t* ddec = s.d_out + (size_t)chunk * BT_REC_BYTES;
@@ -695,6 +720,19 @@ int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_
         if (n_pass) *n_pass = np;
     }
     return BT_OK;
+}
+
+template <class FrameFn>
+int host_pipeline(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uint64_t* verdict, uint8_t* decide,
+                  uint32_t* pass_idx, uint32_t* n_pass) {
+    const int rc = host_pipeline_run(c, n, frame, records, verdict, decide, pass_idx, n_pass);
+    if (rc) {   // retire chunks still in flight, so none is drained into a later call's buffers
+        for (auto& s : c->hs) {
+            if (s.busy) (void)hipEventSynchronize(s.done);
+            s.busy = false;
+        }
+    }
+    return rc;
 }
 
 }  // namespace

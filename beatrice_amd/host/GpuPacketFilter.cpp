@@ -276,6 +276,38 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
     return v;
 }
 
+GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<Packet>& packets) {
+    Verdicts v;
+    std::lock_guard<std::mutex> lock(filtersMutex_);
+    if (dirty_) compileLocked();
+    if (packets.empty()) return v;
+    const auto t0 = std::chrono::steady_clock::now();
+    runBatch(packets, v.decide);
+    const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
+                     (int64_t)packets.size();
+    const std::string none;
+    for (size_t i = 0; i < packets.size(); ++i) {
+        uint32_t d = v.decide[i];
+        if ((d >> 6) == BT_DECIDE_HOST) {
+            try {
+                d = resolveHost(packets[i], d & 63u);
+            } catch (...) {   // a CUSTOM callback threw for this packet
+                d = (BT_DECIDE_THROW << 6) | (d & 63u);
+            }
+            v.decide[i] = (uint8_t)d;
+        }
+        const uint32_t code = d >> 6, slot = d & 63u;
+        if (code == BT_DECIDE_THROW) {
+            v.error_idx.push_back((uint32_t)i);
+            continue;
+        }
+        const bool passed = code == BT_DECIDE_PASS;
+        if (passed) v.pass_idx.push_back((uint32_t)i);
+        updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
+    }
+    return v;
+}
+
 std::vector<uint32_t> GpuPacketFilter::classifyMapped(const bt_batch& batch, const bt_outputs& out,
                                                      uint8_t* decideHost, uint64_t* verdictHost,
                                                      const std::function<Packet(uint32_t)>& packetOf) {

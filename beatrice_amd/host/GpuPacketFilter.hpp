@@ -58,8 +58,18 @@ public:
     struct Verdicts {
         std::vector<uint8_t> decide;     // (code << 6) | slot
         std::vector<uint32_t> pass_idx;  // ascending
+        std::vector<uint32_t> error_idx; // classifyPerPacket only: packets whose evaluation threw
     };
     Verdicts classify(const std::vector<Packet>& packets);
+
+    // The same batch with the exceptions attributed per packet, as a per-packet caller
+    // sees them: PluginManager::processPacket catches a plugin's exception for each
+    // packet and goes on with the next one (src/PluginManager.cpp:158-171). A packet whose
+    // evaluation would throw (a std::stoi expression past its gates, or a throwing CUSTOM
+    // callback) is listed in error_idx with decide code BT_DECIDE_THROW and, as in the
+    // reference, does not update the stats; every other packet is classified and counted.
+    // Never throws for a filter; throws std::runtime_error if the device fails.
+    Verdicts classifyPerPacket(const std::vector<Packet>& packets);
 
     // Zero-copy form over frames the device already sees (a capture ring registered
     // with bt_host_register): runs parse+filter over `batch` into `out` (device-visible

@@ -6,40 +6,65 @@
 // Configuration (environment, read in onStart):
 //   BEATRICE_GPU_DEVICE    device index (default 0)
 //   BEATRICE_GPU_BATCH     packets per GPU batch (default 65536)
-//   BEATRICE_GPU_FLUSH_US  flush a partial batch after this many microseconds (default 2000)
+//   BEATRICE_GPU_FLUSH_US  a partial batch is classified at the latest this many
+//                          microseconds after its first packet arrived, by the plugin's
+//                          flush thread when no further packet comes (default 2000)
 //   BEATRICE_GPU_FILTERS   ';'-separated  name|TYPE|priority|expression  entries, TYPE one of
 //                          BPF PROTOCOL IP_RANGE PORT_RANGE PAYLOAD CUSTOM
+//
+// Results. Each packet is attributed on its own, as PluginManager::processPacket sees a
+// per-packet plugin (src/PluginManager.cpp:158-171: an exception is caught per packet and
+// the next packet goes on): a packet whose filter evaluation throws counts in
+// getErrorCount(), the others are classified (GpuPacketFilter::classifyPerPacket).
+// Downstream consumers get every batch's verdicts, in arrival order, through a verdict
+// sink: C++ setVerdictSink(), or the C hook gpu_plugin_set_sink() for code that only has
+// the IPacketPlugin* PluginManager created.
+//
 // Link with -Wl,-z,nodelete: ~PluginManager dlcloses handles before destroying plugins
 // (src/PluginManager.cpp:26-34).
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "GpuPacketFilter.hpp"
 #include "beatrice/IPacketPlugin.hpp"
+#include "beatrice_gpu_plugin.h"
 
 namespace beatrice {
 namespace gpu {
 
 class GpuParseFilterPlugin : public IPacketPlugin {
 public:
+    using Sink = std::function<void(uint64_t seq, const std::vector<Packet>&, const GpuPacketFilter::Verdicts&)>;
+
+    ~GpuParseFilterPlugin() override { stopFlusher(); }
+
     void onStart() override {
-        std::lock_guard<std::mutex> g(gpu_mu_);
-        std::lock_guard<std::mutex> lk(mu_);
-        const int device = env_int("BEATRICE_GPU_DEVICE", 0);
-        batch_ = (size_t)env_int("BEATRICE_GPU_BATCH", 65536);
-        flush_us_ = env_int("BEATRICE_GPU_FLUSH_US", 2000);
-        filter_ = std::make_unique<GpuPacketFilter>(device);
-        if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
-        pending_.reserve(batch_);
+        stopFlusher();
+        {
+            std::lock_guard<std::mutex> g(gpu_mu_);
+            std::lock_guard<std::mutex> lk(mu_);
+            const int device = env_int("BEATRICE_GPU_DEVICE", 0);
+            batch_ = (size_t)std::max(1, env_int("BEATRICE_GPU_BATCH", 65536));
+            flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
+            filter_ = std::make_unique<GpuPacketFilter>(device);
+            if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
+            pending_.reserve(batch_);
+            stop_ = false;
+        }
+        flusher_ = std::thread([this] { flushLoop(); });
     }
 
     void onStop() override {
+        stopFlusher();
         flush();
         std::lock_guard<std::mutex> g(gpu_mu_);
         filter_.reset();
@@ -47,27 +72,25 @@ public:
 
     // onPacket may run on several context threads at once (src/BeatriceContext.cpp:215-278).
     // A full batch is swapped out under mu_ and classified outside it, so the other
-    // threads keep appending to a fresh batch while the GPU works; gpu_mu_ sends the
-    // batches to the device one at a time.
+    // threads keep appending to a fresh batch while the GPU works.
     void onPacket(Packet& packet) override {
         if (!enabled_) return;
         std::vector<Packet> full;
+        uint64_t seq = 0;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            if (pending_.empty()) first_ = std::chrono::steady_clock::now();
-            pending_.push_back(packet);        // shares the immutable bytes, no copy
-            const auto age =
-                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - first_);
-            if (pending_.size() >= batch_ || age.count() >= flush_us_) {
-                full.swap(pending_);
-                pending_.reserve(batch_);
+            if (pending_.empty()) {
+                first_ = std::chrono::steady_clock::now();
+                cv_.notify_one();              // the flush thread arms this batch's deadline
             }
+            pending_.push_back(packet);        // shares the immutable bytes, no copy
+            if (pending_.size() >= batch_) seq = takeLocked(full);
         }
-        if (!full.empty()) classifyBatch(full);
+        if (!full.empty()) classifyBatch(full, seq);
     }
 
     std::string getName() const override { return "gpu_parse_filter"; }
-    std::string getVersion() const override { return "1.0.0"; }
+    std::string getVersion() const override { return "1.1.0"; }
     std::string getDescription() const override {
         return "MI355X parse + PacketFilter stage (gfx950 kernels behind the beatrice_gpu C-ABI)";
     }
@@ -81,13 +104,21 @@ public:
         if (filter_) filter_->resetStats();
     }
 
+    // Classifies the partial batch now (the flush thread does this on its own after
+    // BEATRICE_GPU_FLUSH_US).
     void flush() {
         std::vector<Packet> full;
+        uint64_t seq = 0;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            full.swap(pending_);
+            if (!pending_.empty()) seq = takeLocked(full);
         }
-        if (!full.empty()) classifyBatch(full);
+        if (!full.empty()) classifyBatch(full, seq);
+    }
+
+    void setVerdictSink(Sink s) {
+        std::lock_guard<std::mutex> g(gpu_mu_);
+        sink_ = std::move(s);
     }
     uint64_t passed() const { return passed_; }
     GpuPacketFilter* filter() { return filter_.get(); }
@@ -96,6 +127,48 @@ private:
     static int env_int(const char* k, int d) {
         const char* v = std::getenv(k);
         return v ? std::atoi(v) : d;
+    }
+
+    // Hands the pending batch out with the next sequence number (mu_ held).
+    uint64_t takeLocked(std::vector<Packet>& out) {
+        out.swap(pending_);
+        pending_.reserve(batch_);
+        return next_seq_++;
+    }
+
+    // The flush thread: sleeps until the pending batch's deadline (first packet + flush_us)
+    // or a stop, and classifies a batch that is still partial then.
+    void flushLoop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        while (!stop_) {
+            if (pending_.empty()) {
+                cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
+                continue;
+            }
+            const auto deadline = first_ + std::chrono::microseconds(flush_us_);
+            if (std::chrono::steady_clock::now() < deadline) {
+                cv_.wait_until(lk, deadline);
+                continue;
+            }
+            std::vector<Packet> full;
+            const uint64_t seq = takeLocked(full);
+            lk.unlock();
+            try {
+                classifyBatch(full, seq);
+            } catch (const std::exception&) {   // the device failed: nobody to throw to here
+                errors_ += full.size();
+            }
+            lk.lock();
+        }
+    }
+
+    void stopFlusher() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        if (flusher_.joinable()) flusher_.join();
     }
 
     void configure(const std::string& spec) {
@@ -122,26 +195,38 @@ private:
         }
     }
 
-    void classifyBatch(const std::vector<Packet>& batch) {
-        std::lock_guard<std::mutex> g(gpu_mu_);
+    // Batches reach the device and the sink in sequence order, whichever thread took them.
+    void classifyBatch(const std::vector<Packet>& batch, uint64_t seq) {
+        std::unique_lock<std::mutex> g(gpu_mu_);
+        order_cv_.wait(g, [&] { return done_seq_ == seq; });
+        struct Advance {   // the next batch may go even if this one throws
+            GpuParseFilterPlugin* p;
+            ~Advance() {
+                ++p->done_seq_;
+                p->order_cv_.notify_all();
+            }
+        } advance{this};
         if (!filter_) return;
-        try {
-            auto v = filter_->classify(batch);
-            processed_ += batch.size();
-            passed_ += v.pass_idx.size();
-        } catch (const std::exception&) {
-            // a filter expression the reference would throw on: count the batch as errors
-            errors_ += batch.size();
-        }
+        const auto v = filter_->classifyPerPacket(batch);
+        processed_ += batch.size();
+        passed_ += v.pass_idx.size();
+        errors_ += v.error_idx.size();
+        if (sink_) sink_(seq, batch, v);
     }
 
-    std::mutex mu_;        // pending_, first_
-    std::mutex gpu_mu_;    // filter_ (one batch on the device at a time)
+    std::mutex mu_;                    // pending_, first_, next_seq_, stop_
+    std::condition_variable cv_;       // wakes the flush thread
+    std::mutex gpu_mu_;                // filter_, sink_, done_seq_ (one batch on the device at a time)
+    std::condition_variable order_cv_;
     std::unique_ptr<GpuPacketFilter> filter_;
     std::vector<Packet> pending_;
     std::chrono::steady_clock::time_point first_;
     size_t batch_ = 65536;
     int flush_us_ = 2000;
+    uint64_t next_seq_ = 0, done_seq_ = 0;
+    bool stop_ = true;
+    std::thread flusher_;
+    Sink sink_;
     std::atomic<bool> enabled_{true};
     std::atomic<uint64_t> processed_{0}, passed_{0}, errors_{0};
 };
@@ -151,10 +236,31 @@ private:
 
 extern "C" beatrice::IPacketPlugin* createPlugin() { return new beatrice::gpu::GpuParseFilterPlugin(); }
 
-// Test/ops hooks (plain C): flush a partial batch, read the pass counter.
+// C hooks (include/beatrice_gpu_plugin.h): flush a partial batch, read the pass counter,
+// install a verdict sink.
 extern "C" void gpu_plugin_flush(beatrice::IPacketPlugin* p) {
     static_cast<beatrice::gpu::GpuParseFilterPlugin*>(p)->flush();
 }
 extern "C" uint64_t gpu_plugin_passed(const beatrice::IPacketPlugin* p) {
     return static_cast<const beatrice::gpu::GpuParseFilterPlugin*>(p)->passed();
+}
+extern "C" void gpu_plugin_set_sink(beatrice::IPacketPlugin* p, gpu_verdict_sink_fn fn, void* user) {
+    auto* g = static_cast<beatrice::gpu::GpuParseFilterPlugin*>(p);
+    if (!fn) {
+        g->setVerdictSink(nullptr);
+        return;
+    }
+    g->setVerdictSink([fn, user](uint64_t seq, const std::vector<beatrice::Packet>& b,
+                                 const beatrice::gpu::GpuPacketFilter::Verdicts& v) {
+        std::vector<const uint8_t*> frames(b.size());
+        std::vector<uint32_t> lens(b.size());
+        for (size_t i = 0; i < b.size(); ++i) {
+            frames[i] = b[i].data();
+            lens[i] = (uint32_t)b[i].length();
+        }
+        gpu_verdict_batch c{seq, (uint32_t)b.size(), frames.data(), lens.data(), v.decide.data(),
+                            v.pass_idx.data(), (uint32_t)v.pass_idx.size(), v.error_idx.data(),
+                            (uint32_t)v.error_idx.size()};
+        fn(user, &c);
+    });
 }

@@ -1,0 +1,333 @@
+// test_plugin.cpp — the GPU plugin inside the reference's plugin pipeline, against the
+// reference PacketFilter (compiled from its own sources, oracle/_ref/obj).
+//
+// PluginManager (src/PluginManager.cpp) logs through spdlog, which this image lacks, so
+// it is not compiled; Host below performs its exact call sequence on the plugin:
+//   loadPlugin    dlopen(path, RTLD_LAZY), dlsym("createPlugin"), create(), onStart()  (:57-95)
+//   processPacket for each plugin: try { onPacket(packet) } catch (...) {}               (:158-171)
+//   unload        onStop(), dlclose, then the plugin's destructor (~PluginManager)     (:14-36)
+// and FakeBackend is an in-memory ICaptureBackend whose getPackets hands out a synthetic
+// capture in batches, the way BeatriceContext::runSingleThreaded pulls them (:180-213).
+//
+// Checks:
+//   flush    a partial batch is classified by the plugin's own flush thread within
+//            2 x BEATRICE_GPU_FLUSH_US with no further onPacket;
+//   errors   with a filter the reference's std::stoi throws on past its gates, exactly the
+//            packets that reach it are errors (per packet, as the reference throws per
+//            applyFilters call) and every other packet is classified;
+//   sink     the verdict sink sees every batch once, in order, and each packet's verdict
+//            and deciding filter equal the reference's FilterResult;
+//   threads  onPacket from 4 threads at once: every packet is classified exactly once.
+// Prints one line per check; exit status 0 = all passed.
+#include <dlfcn.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "beatrice/ICaptureBackend.hpp"
+#include "beatrice/IPacketPlugin.hpp"
+#include "beatrice/PacketFilter.hpp"
+#include "beatrice_gpu.h"
+#include "beatrice_gpu_plugin.h"
+
+extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
+extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
+
+using beatrice::Packet;
+using beatrice::PacketFilter;
+using Clock = std::chrono::steady_clock;
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                                  \
+    do {                                                                  \
+        if (!(cond)) {                                                    \
+            ++g_fail;                                                     \
+            std::printf("FAIL %s:%d: ", __FILE__, __LINE__);              \
+            std::printf(__VA_ARGS__);                                     \
+            std::printf("\n");                                            \
+            return false;                                                 \
+        }                                                                 \
+    } while (0)
+
+// ---- in-memory capture backend ------------------------------------------------------
+class FakeBackend : public beatrice::ICaptureBackend {
+public:
+    FakeBackend(int cfg, uint32_t n, uint64_t seed) {
+        desc_.resize(n);
+        data_.resize(bt_synth_layout(cfg, n, seed, desc_.data()));
+        bt_synth_fill(cfg, n, seed, desc_.data(), data_.data(), 8);
+    }
+    beatrice::Result<void> initialize(const Config& c) override { cfg_ = c; return beatrice::Result<void>::success(); }
+    beatrice::Result<void> start() override { running_ = true; return beatrice::Result<void>::success(); }
+    beatrice::Result<void> stop() override { running_ = false; return beatrice::Result<void>::success(); }
+    bool isRunning() const noexcept override { return running_; }
+    std::optional<Packet> nextPacket(std::chrono::milliseconds) override {
+        auto v = getPackets(1, std::chrono::milliseconds(0));
+        if (v.empty()) return std::nullopt;
+        return v.front();
+    }
+    std::vector<Packet> getPackets(size_t maxPackets, std::chrono::milliseconds) override {
+        std::vector<Packet> out;
+        while (out.size() < maxPackets && next_ < desc_.size()) {
+            const uint8_t* f = data_.data() + (desc_[next_] & 0xFFFFFFFFFFFFull);
+            out.emplace_back(std::shared_ptr<const uint8_t[]>(f, [](const uint8_t*) {}),
+                             (size_t)(desc_[next_] >> 48));
+            ++next_;
+        }
+        return out;
+    }
+    void rewind() { next_ = 0; }
+    size_t size() const { return desc_.size(); }
+    void setPacketCallback(std::function<void(Packet)>) override {}
+    void removePacketCallback() override {}
+    Statistics getStatistics() const override { return {}; }
+    void resetStatistics() override {}
+    std::string getName() const override { return "fake (in-memory)"; }
+    std::string getVersion() const override { return "1"; }
+    std::vector<std::string> getSupportedFeatures() const override { return {}; }
+    bool isFeatureSupported(const std::string&) const override { return false; }
+    Config getConfig() const override { return cfg_; }
+    beatrice::Result<void> updateConfig(const Config& c) override { cfg_ = c; return beatrice::Result<void>::success(); }
+    std::string getLastError() const override { return ""; }
+    bool isHealthy() const override { return true; }
+    beatrice::Result<void> healthCheck() override { return beatrice::Result<void>::success(); }
+    bool isZeroCopyEnabled() const override { return false; }
+    bool isDMAAccessEnabled() const override { return false; }
+    beatrice::Result<void> enableZeroCopy(bool) override { return beatrice::Result<void>::success(); }
+    beatrice::Result<void> enableDMAAccess(bool, const std::string&) override { return beatrice::Result<void>::success(); }
+    beatrice::Result<void> setDMABufferSize(size_t) override { return beatrice::Result<void>::success(); }
+    size_t getDMABufferSize() const override { return 0; }
+    std::string getDMADevice() const override { return ""; }
+    beatrice::Result<void> allocateDMABuffers(size_t) override { return beatrice::Result<void>::success(); }
+    beatrice::Result<void> freeDMABuffers() override { return beatrice::Result<void>::success(); }
+
+private:
+    std::vector<uint8_t> data_;
+    std::vector<uint64_t> desc_;
+    size_t next_ = 0;
+    Config cfg_;
+    bool running_ = false;
+};
+
+// ---- PluginManager's call sequence ----------------------------------------------------
+struct Host {
+    void* handle = nullptr;
+    beatrice::IPacketPlugin* plugin = nullptr;
+    void (*set_sink)(gpu_plugin*, gpu_verdict_sink_fn, void*) = nullptr;
+    void (*flush)(gpu_plugin*) = nullptr;
+
+    bool load(const char* path) {
+        handle = dlopen(path, RTLD_LAZY);                                   // :57
+        if (!handle) return false;
+        using Create = beatrice::IPacketPlugin* (*)();
+        auto create = reinterpret_cast<Create>(dlsym(handle, "createPlugin"));   // :67-68
+        set_sink = reinterpret_cast<decltype(set_sink)>(dlsym(handle, "gpu_plugin_set_sink"));
+        flush = reinterpret_cast<decltype(flush)>(dlsym(handle, "gpu_plugin_flush"));
+        if (!create || !set_sink || !flush) return false;
+        plugin = create();                                                  // :79
+        plugin->onStart();                                                  // :95
+        return true;
+    }
+    void processPacket(Packet& p) {                                        // :158-171
+        try {
+            plugin->onPacket(p);
+        } catch (const std::exception&) {
+        }
+    }
+    void unload() {   // ~PluginManager (:14-36): onStop, dlclose, then the destructor
+        if (plugin) {
+            try {
+                plugin->onStop();
+            } catch (const std::exception&) {
+            }
+        }
+        if (handle) dlclose(handle);   // the plugin is linked -z nodelete: its code stays
+        handle = nullptr;
+        delete plugin;
+        plugin = nullptr;
+    }
+};
+
+// ---- verdict sink -----------------------------------------------------------------------
+struct Sink {
+    std::mutex mu;
+    std::vector<uint64_t> seqs;
+    std::vector<uint8_t> decide;           // in arrival order over all batches
+    std::set<uint64_t> errors, passes;     // global packet positions
+    std::atomic<uint64_t> packets{0};
+    Clock::time_point last_call;
+    static void call(void* user, const gpu_verdict_batch* b) {
+        auto* s = static_cast<Sink*>(user);
+        std::lock_guard<std::mutex> lk(s->mu);
+        const uint64_t base = s->decide.size();
+        s->seqs.push_back(b->seq);
+        s->decide.insert(s->decide.end(), b->decide, b->decide + b->n);
+        for (uint32_t k = 0; k < b->n_error; ++k) s->errors.insert(base + b->error_idx[k]);
+        for (uint32_t k = 0; k < b->n_pass; ++k) s->passes.insert(base + b->pass_idx[k]);
+        s->packets += b->n;
+        s->last_call = Clock::now();
+    }
+};
+
+static std::vector<PacketFilter::FilterResult> reference(const std::vector<Packet>& pk,
+                                                         const std::vector<std::tuple<std::string, int, int, std::string>>& fs,
+                                                         std::vector<bool>& threw) {
+    PacketFilter ref;
+    for (auto& [name, type, prio, expr] : fs) {
+        PacketFilter::FilterConfig c;
+        c.type = static_cast<PacketFilter::FilterType>(type);
+        c.priority = prio;
+        c.expression = expr;
+        ref.addFilter(name, c);
+    }
+    std::vector<PacketFilter::FilterResult> out(pk.size());
+    threw.assign(pk.size(), false);
+    for (size_t i = 0; i < pk.size(); ++i) {
+        try {
+            out[i] = ref.applyFilters(pk[i]);
+        } catch (const std::exception&) {
+            threw[i] = true;
+        }
+    }
+    return out;
+}
+
+static std::string spec_of(const std::vector<std::tuple<std::string, int, int, std::string>>& fs) {
+    static const char* names[] = {"BPF", "PROTOCOL", "IP_RANGE", "PORT_RANGE", "PAYLOAD", "CUSTOM"};
+    std::string s;
+    for (auto& [name, type, prio, expr] : fs)
+        s += name + "|" + names[type] + "|" + std::to_string(prio) + "|" + expr + ";";
+    return s;
+}
+
+// The filter set and the packets the plugin saw, in the order it saw them.
+static bool pipeline_case(const char* so, FakeBackend& be, int flush_us, int batch, const char* what,
+                          const std::vector<std::tuple<std::string, int, int, std::string>>& fs) {
+    setenv("BEATRICE_GPU_FILTERS", spec_of(fs).c_str(), 1);
+    setenv("BEATRICE_GPU_BATCH", std::to_string(batch).c_str(), 1);
+    setenv("BEATRICE_GPU_FLUSH_US", std::to_string(flush_us).c_str(), 1);
+    Host h;
+    CHECK(h.load(so), "load %s: %s", so, dlerror());
+    Sink sink;
+    h.set_sink(h.plugin, &Sink::call, &sink);
+
+    // warm-up (the first batch initialises the device): one partial batch, flushed by hand
+    be.rewind();
+    std::vector<Packet> seen;
+    auto pkts = be.getPackets(100, std::chrono::milliseconds(0));
+    for (auto& p : pkts) h.processPacket(p);
+    h.flush(h.plugin);
+    seen.insert(seen.end(), pkts.begin(), pkts.end());
+
+    // BeatriceContext-style loop: pull batches of 64 from the backend, one onPacket each
+    for (;;) {
+        auto b = be.getPackets(64, std::chrono::milliseconds(0));
+        if (b.empty()) break;
+        for (auto& p : b) h.processPacket(p);
+        seen.insert(seen.end(), b.begin(), b.end());
+    }
+    // no further onPacket: the partial tail must be classified by the flush thread
+    const auto t_last = Clock::now();
+    const auto limit = t_last + std::chrono::microseconds(2 * flush_us);
+    while (sink.packets < seen.size() && Clock::now() < limit + std::chrono::seconds(5))
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    const double after_us = std::chrono::duration<double, std::micro>(sink.last_call - t_last).count();
+    CHECK(sink.packets == seen.size(), "%s: sink saw %lu of %zu packets", what, (unsigned long)sink.packets.load(),
+          seen.size());
+    CHECK(after_us <= 2.0 * flush_us, "%s: tail classified %.0f us after the last packet (limit %d)", what, after_us,
+          2 * flush_us);
+    for (size_t k = 0; k < sink.seqs.size(); ++k) CHECK(sink.seqs[k] == k, "%s: batch %zu has seq %lu", what, k,
+                                                        (unsigned long)sink.seqs[k]);
+
+    std::vector<bool> threw;
+    const auto want = reference(seen, fs, threw);
+    uint64_t n_err = 0, n_pass = 0;
+    for (size_t i = 0; i < seen.size(); ++i) {
+        const bool err = sink.errors.count(i) != 0, pass = sink.passes.count(i) != 0;
+        CHECK(err == threw[i], "%s: packet %zu error %d, reference threw %d", what, i, (int)err, (int)threw[i]);
+        if (threw[i]) { ++n_err; continue; }
+        CHECK(pass == want[i].passed, "%s: packet %zu passed %d, reference %d", what, i, (int)pass,
+              (int)want[i].passed);
+        n_pass += pass;
+        const uint32_t code = sink.decide[i] >> 6;
+        CHECK(code == (want[i].passed ? BT_DECIDE_PASS : BT_DECIDE_REJECT), "%s: packet %zu decide code %u", what, i,
+              code);
+    }
+    CHECK(h.plugin->getErrorCount() == n_err, "%s: plugin errors %lu, reference threw on %lu", what,
+          (unsigned long)h.plugin->getErrorCount(), (unsigned long)n_err);
+    CHECK(h.plugin->getProcessedPacketCount() == seen.size(), "%s: processed %lu", what,
+          (unsigned long)h.plugin->getProcessedPacketCount());
+    h.unload();
+    std::printf("ok   %-8s %zu packets via FakeBackend -> processPacket; tail flushed %.0f us after the last "
+                "packet (flush %d us); %zu batches in order; %lu passed, %lu errors = reference\n",
+                what, seen.size(), after_us, flush_us, sink.seqs.size(), (unsigned long)n_pass, (unsigned long)n_err);
+    return true;
+}
+
+static bool threads_case(const char* so, FakeBackend& be) {
+    setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|2|udp;net|IP_RANGE|1|10.0.0.0/8;", 1);
+    setenv("BEATRICE_GPU_BATCH", "4096", 1);
+    setenv("BEATRICE_GPU_FLUSH_US", "3000", 1);
+    Host h;
+    CHECK(h.load(so), "load");
+    Sink sink;
+    h.set_sink(h.plugin, &Sink::call, &sink);
+    be.rewind();
+    const auto all = be.getPackets(be.size(), std::chrono::milliseconds(0));
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < all.size(); i += 4) {
+                Packet p = all[i];
+                h.processPacket(p);
+            }
+        });
+    for (auto& x : th) x.join();
+    const auto limit = Clock::now() + std::chrono::seconds(10);
+    while (sink.packets < all.size() && Clock::now() < limit) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    CHECK(sink.packets == all.size(), "threads: sink saw %lu of %zu", (unsigned long)sink.packets.load(), all.size());
+    for (size_t k = 0; k < sink.seqs.size(); ++k) CHECK(sink.seqs[k] == k, "threads: batch order");
+    std::vector<bool> threw;
+    const auto want = reference(all, {{"proto", 1, 2, "udp"}, {"net", 2, 1, "10.0.0.0/8"}}, threw);
+    uint64_t ref_pass = 0;
+    for (auto& r : want) ref_pass += r.passed;
+    CHECK(sink.passes.size() == ref_pass, "threads: %zu passed, reference %lu", sink.passes.size(),
+          (unsigned long)ref_pass);
+    CHECK(h.plugin->getProcessedPacketCount() == all.size() && h.plugin->getErrorCount() == 0, "threads: counts");
+    h.unload();
+    std::printf("ok   threads  %zu packets from 4 onPacket threads, %zu batches in order, %lu passed = reference\n",
+                all.size(), sink.seqs.size(), (unsigned long)ref_pass);
+    return true;
+}
+
+int main(int argc, char** argv) {
+    const char* so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
+    int ndev = 0;
+    if (bt_device_count(&ndev) != BT_OK || ndev == 0) {
+        std::printf("no GPU\n");
+        return 2;
+    }
+    FakeBackend c3(3, 50000, 0x5EED0003ull), fuzz(9, 20000, 0xF00Dull);
+    bool ok = true;
+    // the reference's 5-tuple set; batches of 4096, 20 ms flush
+    ok &= pipeline_case(so, c3, 20000, 4096, "c3", {{"proto", 1, 3, "udp"}, {"net", 2, 2, "10.0.0.0/8"},
+                                                       {"ports", 3, 1, "1000-2000"}});
+    // a stoi-throwing IP_RANGE past the UDP gate: per-packet errors; short flush
+    ok &= pipeline_case(so, fuzz, 5000, 1000, "errors", {{"proto", 1, 3, "udp"}, {"bad", 2, 2, "10.x.0.0/8"},
+                                                           {"ports", 3, 1, "1-65535"}});
+    ok &= threads_case(so, c3);
+    std::printf(ok && !g_fail ? "ALL OK\n" : "FAILURES\n");
+    return ok && !g_fail ? 0 : 1;
+}

@@ -18,3 +18,17 @@ def test_cpp_adapter_matches_reference():
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "ALL OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_plugin_in_the_reference_pipeline():
+    """tests/cpp/test_plugin.cpp: the plugin driven through PluginManager's call sequence
+    from an in-memory capture backend — flush thread, per-packet errors, ordered verdict
+    sink — against the reference PacketFilter."""
+    b = os.path.join(ROOT, "tests", "cpp", "test_plugin")
+    assert os.path.exists(b), "tests/cpp/test_plugin not built (make -C tests/cpp in the build container)"
+    r = subprocess.run([b, os.path.join(ROOT, "beatrice_amd", "libgpu_parse_filter_plugin.so")],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "ALL OK" in r.stdout

@@ -356,3 +356,27 @@ def test_repeated_runs_are_identical(gpu_ctx):
             assert out["n_pass"] == first["n_pass"]
     finally:
         r.free()
+
+
+@pytest.mark.parametrize("fset", ["c3", "mixed", "throw_after", "empty"])
+def test_fixed_stride_headline_kernel_on_reference_fixture(fset):
+    """The headline's kernel form — fixed 64-B stride, no descriptors
+    (bt_parse_filter_main<2, tiled, filter>) — on the c1 golden frames (10k x 64 B at
+    stride 64) against the compiled reference's own records and applyFilters outcomes,
+    not only against the C restatement."""
+    g, man = load_golden("c1")
+    n = len(g["desc"])
+    assert (synth.desc_off(g["desc"]) == np.arange(n) * 64).all() and (synth.desc_len(g["desc"]) == 64).all()
+    filters = man["filter_sets"][fset]
+    ctx = abi.Context(0)
+    try:
+        ctx.compile(filters)
+        out = run_dev(ctx, g["data"], None, n, stride=64)
+        assert np.array_equal(out["records"], g["rec"]), "records differ from the reference fixture"
+        host = compare_decisions(out["decide"], g[f"code__{fset}"], g[f"src__{fset}"], filters, where=f"c1/{fset}")
+        assert len(host) == 0
+        check_filter_outputs(out, n)
+        out = run_dev(ctx, g["data"], None, n, stride=64, filt=False)   # the C2 parse-only form
+        assert np.array_equal(out["records"], g["rec"])
+    finally:
+        ctx.close()

@@ -94,3 +94,41 @@ def test_payload_host_option_and_pool_limit():
         assert kinds.index("HOST") == kinds.count("PAYLOAD")
     finally:
         ctx.close()
+
+
+def test_host_batch_payload_past_staged_headers():
+    """bt_parse_filter (host buffers, prefix staging): a GPU PAYLOAD slot reads
+    applyPayloadFilter's window up to frame byte 174 (src/PacketFilter.cpp:293-309), past
+    the 112-B header prefix staged for the walk. Frames longer than that with the match
+    beyond byte 112 (IHL up to 15, so the window starts at byte 74) decide exactly as
+    the compiled reference PacketFilter."""
+    rng = np.random.default_rng(5)
+    frames = []
+    for i in range(3000):
+        ihl = 5 + (i % 11)
+        po = 14 + 4 * ihl
+        ln = int(rng.integers(34, 260))
+        f = bytearray(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00"
+        if ln > 14:
+            f[14] = 0x40 | ihl
+        at = po + int(rng.choice([0, 38, 60, 90, 95, 99]))   # the window holds bytes [po, po + 100)
+        if i % 3 and at + 5 <= ln:
+            f[at:at + 5] = b"MAGIC"
+        frames.append(bytes(f))
+    data, desc = synth.pack_frames(frames, align=1)
+    n = len(desc)
+    filters = [{"type": abi.PROTOCOL, "expr": "ip", "priority": 2},
+               {"type": abi.PAYLOAD, "expr": "MAG+IC", "priority": 1}]
+    ctx = abi.Context(0, host_chunk_packets=1000)
+    try:
+        prog = ctx.compile(filters)
+        assert abi.KINDS[prog[1].kind] == "PAYLOAD"
+        out = ctx.run_host(data, desc)
+    finally:
+        ctx.close()
+    code, src = ol.ref_filter(data, desc, n, filters)
+    assert not ((out["decide"] >> 6) == 3).any(), "the GPU DFA slot left packets to the host"
+    compare_decisions(out["decide"], code, src, filters, where="host-batch payload")
+    late = [i for i, f in enumerate(frames) if f.find(b"MAGIC") >= 112]
+    assert len(late) > 100 and (code[late] == 0).sum() > 50
