@@ -101,6 +101,37 @@ class Timing(ctypes.Structure):
                 for k, _ in self._fields_ if k != "reserved"}
 
 
+class FieldDef(ctypes.Structure):
+    """bt_field_def: one FieldDefinition of a user protocol table."""
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint64), ("type", ctypes.c_uint32),
+                ("endianness", ctypes.c_uint32)]
+
+
+class ExtractOut(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_void_p), ("values", ctypes.c_void_p), ("image", ctypes.c_void_p),
+                ("n_cap", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+# FieldType (reference include/parser/FieldDefinition.hpp:16-35)
+(FT_UINT8, FT_UINT16, FT_UINT32, FT_UINT64, FT_INT8, FT_INT16, FT_INT32, FT_INT64, FT_FLOAT32, FT_FLOAT64,
+ FT_BYTES, FT_STRING, FT_BOOLEAN, FT_MAC, FT_IPV4, FT_IPV6, FT_TIMESTAMP, FT_CUSTOM) = range(18)
+
+
+def field_table(fields):
+    """fields: (offset, length, type, endianness) tuples -> (bt_field_def array, n)."""
+    arr = (FieldDef * max(1, len(fields)))()
+    for i, (o, ln, t, e) in enumerate(fields):
+        arr[i] = FieldDef(int(o), int(ln), int(t), int(e))
+    return arr, len(fields)
+
+
+def proto_span(fields) -> int:
+    arr, n = field_table(fields)
+    span = ctypes.c_uint64(0)
+    _check(lib().bt_proto_span(arr, n, ctypes.byref(span)))
+    return span.value
+
+
 class Tpv3Ring(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("block_size", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32)]
@@ -110,7 +141,7 @@ EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_record_gather", "bt_record_gather_planes",
+    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
@@ -155,6 +186,9 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "bt_time_device_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
                                              ctypes.POINTER(Timing)]),
+        "bt_proto_span": (ctypes.c_int, [vp, u32, ctypes.POINTER(u64)]),
+        "bt_extract_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), vp]),
+        "bt_extract": (ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, vp]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
         "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
@@ -335,6 +369,22 @@ class Context:
         t = Timing()
         _check(lib().bt_time_device_ex(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(t)))
         return t
+
+    def extract_host(self, frames, fields):
+        """bt_extract over a list of frames (bytes): (status[n], values[nf, n], image[n, span])."""
+        n = len(frames)
+        bufs = [np.frombuffer(bytes(f), np.uint8) if len(f) else np.zeros(1, np.uint8) for f in frames]
+        ptrs = (ctypes.c_void_p * max(1, n))(*[b.ctypes.data for b in bufs])
+        lens = np.array([len(f) for f in frames], np.uint32)
+        arr, nf = field_table(fields)
+        span = proto_span(fields)
+        span = span if span <= 0xFFFF else 0
+        status = np.zeros(max(n, 1), np.uint8)
+        values = np.zeros(max(1, nf * n), np.uint64)          # field-major, column stride n
+        image = np.zeros(max(1, n * span), np.uint8)
+        _check(lib().bt_extract(self.h, ptrs, lens.ctypes.data, n, arr, nf, status.ctypes.data,
+                                values.ctypes.data if nf else None, image.ctypes.data if span else None))
+        return status[:n], values[:nf * n].reshape(nf, n), image[:n * span].reshape(n, span)
 
     def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
         """bt_parse_filter over host buffers. Returns dict of numpy outputs."""
@@ -590,5 +640,50 @@ class DeviceRun:
 
     def free(self):
         for b in (self.d_data, self.d_desc, self.d_rec, self.d_dec, self.d_ver, self.d_pidx, self.d_npass):
+            if b is not None:
+                b.free()
+
+
+class DeviceExtract:
+    """Device-resident batch for bt_extract_device (user protocol tables)."""
+
+    def __init__(self, ctx: Context, data: np.ndarray, desc: np.ndarray | None, n: int, fields, stride: int = 0,
+                 desc_format: int = DESC_PACKED, image=True):
+        self.ctx, self.n = ctx, n
+        self.fields = list(fields)
+        self.span = proto_span(self.fields)
+        self.d_data = ctx.alloc((data.nbytes + 255) // 256 * 256 + 256)
+        self.d_data.upload(data)
+        self.d_desc = None
+        if desc is not None:
+            self.d_desc = ctx.alloc(max(16, desc.nbytes))
+            self.d_desc.upload(np.ascontiguousarray(desc))
+        self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n, int(data.nbytes),
+                           desc_format, 0)
+        nf = len(self.fields)
+        img = image and 0 < self.span <= 0xFFFF
+        self.d_status = ctx.alloc(max(16, n))
+        self.d_values = ctx.alloc(max(16, nf * n * 8)) if nf else None
+        self.d_image = ctx.alloc(max(16, n * self.span)) if img else None
+        self.out = ExtractOut(self.d_status.ptr, self.d_values.ptr if self.d_values else None,
+                              self.d_image.ptr if self.d_image else None, n, 0)
+        self.table, self.nf = field_table(self.fields)
+
+    def run(self, stream=None):
+        _check(lib().bt_extract_device(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
+                                       ctypes.byref(self.out), stream))
+
+    def fetch(self):
+        self.ctx.synchronize()
+        n, nf = self.n, len(self.fields)
+        status = self.d_status.download(np.zeros(max(n, 1), np.uint8))[:n]
+        values = self.d_values.download(np.zeros(max(1, nf * n), np.uint64))[:nf * n].reshape(nf, n) \
+            if self.d_values else np.zeros((nf, n), np.uint64)
+        image = self.d_image.download(np.zeros(max(16, n * self.span), np.uint8))[:n * self.span].reshape(n, self.span) \
+            if self.d_image else None
+        return status, values, image
+
+    def free(self):
+        for b in (self.d_data, self.d_desc, self.d_status, self.d_values, self.d_image):
             if b is not None:
                 b.free()

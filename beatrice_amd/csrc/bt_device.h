@@ -75,6 +75,33 @@ int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t 
                    uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream);
 int device_grid_blocks(int device);
 
+// ---- user-defined protocol extraction (bt_extract.hip) ----
+constexpr uint32_t kExWindow = 256;   // bytes of each packet staged in LDS; fields past it read memory
+struct ExField {                      // one bt_field_def as the kernel sees it
+    uint32_t offset, length;          // both < 65536 once the table's span is
+    uint32_t ctl;                     // type | endianness << 8
+    uint32_t pad;
+};
+struct ExTable {                      // kernel argument
+    uint32_t n;                       // fields
+    uint32_t span;                    // getTotalLength()
+    uint32_t window;                  // min(span, kExWindow)
+    uint32_t pad;
+    ExField f[BT_FIELD_MAX];
+};
+struct ExArgs {
+    const uint8_t* base;
+    const uint64_t* desc;             // nullptr: fixed stride
+    uint32_t desc_words;
+    uint64_t bytes;                   // readable size of base (rounded up to 16)
+    uint32_t stride, n, ntiles;
+    uint8_t* status;
+    uint64_t* values;
+    uint8_t* image;
+    uint32_t n_cap;
+};
+int launch_extract(const ExArgs& a, const ExTable& tab, void* stream);
+
 // Host filter compiler (bt_filter_compile.cpp): pure C++, no device needed.
 int compile_filters(const bt_filter_desc* f, uint32_t n, bt_filter_slot* out, uint32_t cap,
                     uint32_t* n_slots, char* err, size_t errlen);

@@ -166,6 +166,11 @@ struct bt_ctx {
     uint32_t tg_iters = 0;
     int spin_rc = -1;                  // hipSetDeviceFlags(hipDeviceScheduleSpin) result
     unsigned device_flags = 0;
+
+    // bt_extract (host lists): pinned + device staging, grown on demand
+    uint8_t* ex_h = nullptr;
+    uint8_t* ex_d = nullptr;
+    size_t ex_cap = 0;
 };
 
 namespace bt {
@@ -408,6 +413,8 @@ void bt_destroy(bt_ctx* c) {
     for (auto e : c->tev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ex_h) (void)hipHostFree(c->ex_h);
+    if (c->ex_d) (void)hipFree(c->ex_d);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -837,6 +844,171 @@ int bt_synchronize(bt_ctx* c) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return BT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// A bt_field_def table as the kernel takes it (ExTable), with the span and the checks the
+// C-ABI promises. span > 65535 can never parse a frame (lengths are 16-bit): *never = true.
+int build_table(const bt_field_def* f, uint32_t n, ExTable* t, uint64_t* span_out, bool* never) {
+    if (n && !f) return fail(BT_E_INVALID_ARGUMENT, "null field table");
+    if (n > BT_FIELD_MAX) return fail(BT_E_INVALID_ARGUMENT, "%u fields (max %u)", n, BT_FIELD_MAX);
+    // getTotalLength (src/parser/FieldDefinition.cpp:31-46): the end of the field that ends
+    // last (offset + length in size_t arithmetic)
+    uint64_t mo = 0, ml = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (f[k].type > BT_FT_CUSTOM) return fail(BT_E_INVALID_ARGUMENT, "field %u: unknown type %u", k, f[k].type);
+        if (f[k].type == BT_FT_BOOLEAN && f[k].length == 0)
+            return fail(BT_E_INVALID_ARGUMENT, "field %u: BOOLEAN of length 0 (the reference reads fieldData[0] "
+                        "of an empty vector)", k);
+        if (f[k].offset + f[k].length < f[k].offset)
+            return fail(BT_E_INVALID_ARGUMENT, "field %u: offset + length overflows", k);
+        if (f[k].offset + f[k].length > mo + ml) { mo = f[k].offset; ml = f[k].length; }
+    }
+    const uint64_t span = n ? mo + ml : 0;
+    if (span_out) *span_out = span;
+    *never = span > 0xFFFFu;
+    std::memset(t, 0, sizeof(*t));
+    t->n = n;
+    t->span = *never ? 0u : (uint32_t)span;
+    t->window = std::min<uint32_t>(t->span, kExWindow);
+    for (uint32_t k = 0; k < n && !*never; ++k) {
+        t->f[k].offset = (uint32_t)f[k].offset;
+        t->f[k].length = (uint32_t)f[k].length;
+        t->f[k].ctl = f[k].type | ((f[k].endianness & 0xFFu) << 8);
+    }
+    return BT_OK;
+}
+
+int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, const bt_extract_out* o, hipStream_t st) {
+    if (!b || !o) return fail(BT_E_INVALID_ARGUMENT, "null batch/outputs");
+    if (b->n && !b->base) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer");
+    if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
+    if (o->values && o->n_cap < b->n) return fail(BT_E_INVALID_ARGUMENT, "values n_cap %u < n %u", o->n_cap, b->n);
+    if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
+    if (!b->n) return BT_OK;
+    if (never) {   // no frame reaches the span: every packet PACKET_TOO_SHORT, no field
+        if (o->status) HIP_TRY(hipMemsetAsync(o->status, 9, b->n, st));
+        if (o->values) for (uint32_t k = 0; k < t.n; ++k)
+            HIP_TRY(hipMemsetAsync(o->values + (size_t)k * o->n_cap, 0, (size_t)b->n * 8, st));
+        return BT_OK;
+    }
+    ExArgs a{};
+    a.base = b->base;
+    a.desc = static_cast<const uint64_t*>(b->desc);
+    a.desc_words = b->desc_format == BT_DESC_XDP ? 2u : 1u;
+    uint64_t bytes = b->bytes;
+    if (!bytes) bytes = b->desc ? ~0ull : (uint64_t)b->n * b->stride;
+    a.bytes = bytes == ~0ull ? bytes : (bytes + 15) & ~15ull;
+    a.stride = b->stride;
+    a.n = b->n;
+    a.ntiles = (b->n + 63) / 64;
+    a.status = o->status;
+    a.values = o->values;
+    a.image = o->image;
+    a.n_cap = o->n_cap;
+    const int rc = launch_extract(a, t, st);
+    if (rc) return fail(rc, "extract kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return BT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bt_proto_span(const bt_field_def* fields, uint32_t n_fields, uint64_t* span) {
+    if (!span) return fail(BT_E_INVALID_ARGUMENT, "null span");
+    ExTable t;
+    bool never = false;
+    return build_table(fields, n_fields, &t, span, &never);
+}
+
+int bt_extract_device(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
+                      const bt_extract_out* out, void* stream) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    ExTable t;
+    bool never = false;
+    int rc = build_table(fields, n_fields, &t, nullptr, &never);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    return run_extract(c, b, t, never, out, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
+}
+
+int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,
+               uint32_t n_fields, uint8_t* status, uint64_t* values, uint8_t* image) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (n && (!frames || !lens)) return fail(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
+    ExTable t;
+    bool never = false;
+    uint64_t span64 = 0;
+    int rc = build_table(fields, n_fields, &t, &span64, &never);
+    if (rc) return rc;
+    if (!n) return BT_OK;
+    if (never) {
+        if (status) std::memset(status, 9, n);
+        if (values) std::memset(values, 0, (size_t)n_fields * n * 8);
+        return BT_OK;   // image: n x span bytes the caller could not have allocated anyway
+    }
+    const uint32_t span = t.span;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    // chunks of at most 1M packets: [prefixes | descriptors] in, [status | values | image] out
+    const uint32_t chunk = 1u << 20;
+    for (uint32_t lo = 0; lo < n; lo += chunk) {
+        const uint32_t m = std::min(chunk, n - lo);
+        std::vector<uint64_t> pos(m + 1, 0);
+        for (uint32_t i = 0; i < m; ++i) {
+            if (lens[lo + i] > 0xFFFFu) return fail(BT_E_INVALID_ARGUMENT, "frame %u longer than 65535 bytes", lo + i);
+            pos[i + 1] = pos[i] + ((std::min(lens[lo + i], span) + 15u) & ~15u);
+        }
+        const size_t pre = pos[m] + 16, dsc = (size_t)m * 8;
+        const size_t st_b = ((size_t)m + 15) & ~(size_t)15, val_b = (size_t)n_fields * m * 8, img_b = (size_t)m * span;
+        const size_t in_b = pre + dsc, out_b = st_b + val_b + img_b;
+        const size_t need = in_b + out_b + 64;
+        if (need > c->ex_cap) {
+            if (c->ex_h) (void)hipHostFree(c->ex_h);
+            if (c->ex_d) (void)hipFree(c->ex_d);
+            c->ex_h = nullptr;
+            c->ex_d = nullptr;
+            c->ex_cap = 0;
+            const size_t cap = std::max(need, (size_t)1 << 20);
+            HIP_TRY(hipHostMalloc(&c->ex_h, cap, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&c->ex_d, cap));
+            c->ex_cap = cap;
+        }
+        uint8_t* h = c->ex_h;
+        uint64_t* d = reinterpret_cast<uint64_t*>(h + pre);
+        for (uint32_t i = 0; i < m; ++i) {   // only [0, span) of a frame is ever read
+            const uint32_t k = std::min(lens[lo + i], span);
+            if (k) std::memcpy(h + pos[i], frames[lo + i], k);
+            d[i] = BT_DESC(pos[i], lens[lo + i]);
+        }
+        HIP_TRY(hipMemcpyAsync(c->ex_d, h, in_b, hipMemcpyHostToDevice, c->stream));
+        bt_batch b{};
+        b.base = c->ex_d;
+        b.desc = c->ex_d + pre;
+        b.n = m;
+        b.bytes = pre;
+        uint8_t* dout = c->ex_d + ((in_b + 15) & ~(size_t)15);
+        uint8_t* hout = h + ((in_b + 15) & ~(size_t)15);
+        bt_extract_out o{};
+        o.status = dout;
+        o.values = n_fields ? reinterpret_cast<uint64_t*>(dout + st_b) : nullptr;
+        o.image = span ? dout + st_b + val_b : nullptr;
+        o.n_cap = m;
+        rc = run_extract(c, &b, t, false, &o, c->stream);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(hout, dout, out_b, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (status) std::memcpy(status + lo, hout, m);
+        for (uint32_t k = 0; values && k < n_fields; ++k)
+            std::memcpy(values + (size_t)k * n + lo, hout + st_b + (size_t)k * m * 8, (size_t)m * 8);
+        if (image && span) std::memcpy(image + (size_t)lo * span, hout + st_b + val_b, img_b);
+    }
     return BT_OK;
 }
 

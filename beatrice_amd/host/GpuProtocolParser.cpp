@@ -5,8 +5,11 @@
 // ParseResult header fields :238-284.
 #include "GpuProtocolParser.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <ctime>
+#include <iomanip>
 #include <sstream>
 #include <stdexcept>
 
@@ -253,7 +256,12 @@ std::string GpuParsedBatch::format(uint32_t fmt) const {
     return format_recs(ctx_, recs_.data(), (uint32_t)recs_.size(), fmt);
 }
 
-GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts) {
+GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts)
+    : GpuProtocolParser(parser::ProtocolParser::ParserConfig{}, device, opts) {}
+
+GpuProtocolParser::GpuProtocolParser(const parser::ProtocolParser::ParserConfig& config, int device,
+                                     const bt_opts* opts)
+    : config_(config) {
     if (bt_create(device, opts, &ctx_) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
 }
@@ -329,6 +337,343 @@ GpuParsedBatch GpuProtocolParser::parseBatch(const uint8_t* base, const bt_pkt_d
     }
     run(b);
     return b;
+}
+
+// ---- user-defined protocols ------------------------------------------------------------
+
+namespace {
+
+// ProtocolParser::formatMacAddress / formatIPv4Address / formatIPv6Address / formatTimestamp
+// (src/parser/ProtocolParser.cpp:599-640), the same standard-library calls.
+std::string fmt_mac(const std::vector<uint8_t>& b) {
+    if (b.size() != 6) return "invalid";
+    static const char* d = "0123456789abcdef";
+    std::string s;
+    for (size_t i = 0; i < 6; ++i) {
+        if (i) s += ':';
+        s += d[b[i] >> 4];
+        s += d[b[i] & 15];
+    }
+    return s;
+}
+
+std::string fmt_ts(uint64_t ts) {
+    const auto tp = std::chrono::system_clock::from_time_t(ts);
+    const auto t = std::chrono::system_clock::to_time_t(tp);
+    const std::tm* tm = std::localtime(&t);
+    if (!tm) return "";   // the reference passes NULL to put_time here (and crashes)
+    std::stringstream ss;
+    ss << std::put_time(tm, "%Y-%m-%d %H:%M:%S");
+    return ss.str();
+}
+
+// ProtocolParser::validateField (:435-475): value constraints apply to the unsigned types,
+// pattern constraints to FieldValue::toString() (src/parser/ParserResult.cpp:9-48).
+std::string to_string_of(const FieldValue& v) {
+    if (!v.valid) return "INVALID";
+    switch (v.type) {
+    case FieldValueType::UINT8: return std::to_string(std::get<uint8_t>(v.value));
+    case FieldValueType::UINT16: return std::to_string(std::get<uint16_t>(v.value));
+    case FieldValueType::UINT32: return std::to_string(std::get<uint32_t>(v.value));
+    case FieldValueType::UINT64: return std::to_string(std::get<uint64_t>(v.value));
+    case FieldValueType::INT8: return std::to_string(std::get<int8_t>(v.value));
+    case FieldValueType::INT16: return std::to_string(std::get<int16_t>(v.value));
+    case FieldValueType::INT32: return std::to_string(std::get<int32_t>(v.value));
+    case FieldValueType::INT64: return std::to_string(std::get<int64_t>(v.value));
+    case FieldValueType::FLOAT32: return std::to_string(std::get<float>(v.value));
+    case FieldValueType::FLOAT64: return std::to_string(std::get<double>(v.value));
+    case FieldValueType::BYTES: return "[" + std::to_string(std::get<std::vector<uint8_t>>(v.value).size()) + " bytes]";
+    case FieldValueType::STRING: return std::get<std::string>(v.value);
+    case FieldValueType::BOOLEAN: return std::get<bool>(v.value) ? "true" : "false";
+    case FieldValueType::MAC_ADDRESS: case FieldValueType::IPV4_ADDRESS: case FieldValueType::IPV6_ADDRESS:
+    case FieldValueType::TIMESTAMP: case FieldValueType::CUSTOM:
+        return v.formatted.empty() ? "formatted" : v.formatted;
+    default: return "unknown";
+    }
+}
+
+bool validate_field(const FieldValue& v, const parser::FieldDefinition& f) {
+    if (!v.valid) return false;
+    if (!f.constraint) return true;
+    const auto& c = f.constraint.value();
+    if (c.minValue.index() != std::variant_npos && c.maxValue.index() != std::variant_npos) {
+        if (v.type == FieldValueType::UINT8 || v.type == FieldValueType::UINT16 || v.type == FieldValueType::UINT32 ||
+            v.type == FieldValueType::UINT64) {
+            const uint64_t x = std::visit([](const auto& y) -> uint64_t {
+                if constexpr (std::is_arithmetic_v<std::decay_t<decltype(y)>>) return static_cast<uint64_t>(y);
+                return 0;
+            }, v.value);
+            if (c.minValue.index() == 1 && x < std::get<uint64_t>(c.minValue)) return false;
+            if (c.maxValue.index() == 1 && x > std::get<uint64_t>(c.maxValue)) return false;
+        }
+    }
+    if (!c.pattern.empty() && to_string_of(v).find(c.pattern) == std::string::npos) return false;
+    return true;
+}
+
+// extractField (:286-383) from the GPU's value bits and the field's bytes.
+FieldValue field_value(const parser::FieldDefinition& f, uint64_t bits, const uint8_t* b) {
+    FieldValue v;
+    v.valid = true;
+    v.rawHex = hex(b, f.length);
+    std::vector<uint8_t> data(b, b + f.length);
+    auto as = [&](auto t) {
+        decltype(t) x;
+        std::memcpy(&x, &bits, sizeof(x));
+        return x;
+    };
+    using parser::FieldType;
+    switch (f.type) {
+    case FieldType::UINT8: v.type = FieldValueType::UINT8; v.value = as(uint8_t{}); break;
+    case FieldType::UINT16: v.type = FieldValueType::UINT16; v.value = as(uint16_t{}); break;
+    case FieldType::UINT32: v.type = FieldValueType::UINT32; v.value = as(uint32_t{}); break;
+    case FieldType::UINT64: v.type = FieldValueType::UINT64; v.value = as(uint64_t{}); break;
+    case FieldType::INT8: v.type = FieldValueType::INT8; v.value = as(int8_t{}); break;
+    case FieldType::INT16: v.type = FieldValueType::INT16; v.value = as(int16_t{}); break;
+    case FieldType::INT32: v.type = FieldValueType::INT32; v.value = as(int32_t{}); break;
+    case FieldType::INT64: v.type = FieldValueType::INT64; v.value = as(int64_t{}); break;
+    case FieldType::FLOAT32: v.type = FieldValueType::FLOAT32; v.value = as(float{}); break;
+    case FieldType::FLOAT64: v.type = FieldValueType::FLOAT64; v.value = as(double{}); break;
+    case FieldType::BYTES: v.type = FieldValueType::BYTES; v.value = data; break;
+    case FieldType::STRING: v.type = FieldValueType::STRING; v.value = std::string(data.begin(), data.end()); break;
+    case FieldType::BOOLEAN: v.type = FieldValueType::BOOLEAN; v.value = bits != 0; break;
+    case FieldType::MAC_ADDRESS:
+        v.type = FieldValueType::MAC_ADDRESS;
+        v.formatted = fmt_mac(data);
+        v.value = data;
+        break;
+    case FieldType::IPV4_ADDRESS:
+        v.type = FieldValueType::IPV4_ADDRESS;
+        v.formatted = data.size() == 4 ? fmt_ipv4(b) : "invalid";
+        v.value = data;
+        break;
+    case FieldType::IPV6_ADDRESS:
+        v.type = FieldValueType::IPV6_ADDRESS;
+        v.formatted = data.size() == 16 ? fmt_ipv6(b) : "invalid";
+        v.value = data;
+        break;
+    case FieldType::TIMESTAMP:
+        v.type = FieldValueType::TIMESTAMP;
+        v.value = bits;
+        v.formatted = fmt_ts(bits);
+        break;
+    case FieldType::CUSTOM:
+        v.type = FieldValueType::CUSTOM;
+        v.value = data;
+        if (f.formatter) v.formatted = f.formatter(data);
+        break;
+    }
+    return v;
+}
+
+std::vector<bt_field_def> table_of_def(const parser::ProtocolDefinition& d) {
+    std::vector<bt_field_def> t;
+    for (const auto& f : d.fields)
+        t.push_back(bt_field_def{(uint64_t)f.offset, (uint64_t)f.length, (uint32_t)f.type, (uint32_t)f.endianness});
+    return t;
+}
+
+}  // namespace
+
+std::vector<uint8_t> GpuFieldBatch::bytes(size_t i, size_t k) const {
+    const auto& f = def_.fields.at(k);
+    if (!isSuccess(i)) return {};
+    const uint8_t* b = image_.data() + i * span_ + f.offset;
+    return std::vector<uint8_t>(b, b + f.length);
+}
+
+ParseResult GpuFieldBatch::result(size_t i) const {   // parsePacketInternal (:238-284)
+    ParseResult r;
+    const uint32_t len = lens_.at(i);
+    r.protocolName = def_.name;
+    r.protocolVersion = def_.version;
+    r.rawData.assign(frames_[i], frames_[i] + len);
+    r.packetLength = len;
+    r.parsedBytes = 0;
+    if (!isSuccess(i)) {
+        r.status = ParseStatus::PACKET_TOO_SHORT;
+        r.errorMessage = "Packet too short for protocol";
+        return r;
+    }
+    size_t parsed = 0;
+    const uint8_t* img = image_.data() + i * span_;
+    for (size_t k = 0; k < def_.fields.size(); ++k) {
+        const auto& f = def_.fields[k];
+        if (f.offset + f.length > len) continue;   // :252-254 (never once len >= span)
+        FieldValue v = field_value(f, raw(i, k), img + f.offset);
+        r.fields[f.name] = v;   // ParseResult::addField (ParserResult.cpp:351-353)
+        if (validate_ && !validate_field(v, f)) {
+            parser::ValidationResult vr;
+            vr.fieldName = f.name;
+            vr.valid = false;
+            vr.errorMessage = "Field validation failed";
+            r.validationResults.push_back(vr);
+        }
+        parsed = std::max(parsed, f.offset + f.length);
+    }
+    r.parsedBytes = parsed;   // validateChecksum is always true (:477-480)
+    return r;
+}
+
+void GpuProtocolParser::countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us) {
+    if (!config_.enablePerformanceMetrics) return;   // parsePacket updates stats only then (:89-92)
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    const uint64_t n = ok + bad;
+    if (!n) return;
+    auto& st = stats_;
+    st.totalPacketsParsed += n;
+    st.successfulParses += ok;
+    st.failedParses += bad;
+    time_carry_us_ += us;
+    const auto total = std::chrono::microseconds((int64_t)time_carry_us_);
+    st.totalParseTime += total;
+    time_carry_us_ -= (double)total.count();
+    const auto each = std::chrono::microseconds((int64_t)(us / (double)n));
+    if (each < st.minParseTime) st.minParseTime = each;
+    if (each > st.maxParseTime) st.maxParseTime = each;
+    if (st.successfulParses) {
+        st.averageParseTime = std::chrono::microseconds(st.totalParseTime.count() / st.successfulParses);
+        st.averageValidationTime = std::chrono::microseconds(st.totalValidationTime.count() / st.successfulParses);
+    }
+    st.protocolUsageCount[protocol] += n;
+}
+
+void GpuProtocolParser::extract(GpuFieldBatch& b) {
+    const auto table = table_of_def(b.def_);
+    for (const auto& f : table)
+        if (f.type == BT_FT_BOOLEAN && f.length == 0)
+            throw std::invalid_argument("GpuProtocolParser: BOOLEAN field of length 0 (undefined in the reference)");
+    uint64_t span = 0;
+    if (bt_proto_span(table.data(), (uint32_t)table.size(), &span) != BT_OK)
+        throw std::invalid_argument(std::string("GpuProtocolParser: ") + bt_last_error());
+    const uint32_t n = (uint32_t)b.frames_.size();
+    b.span_ = span > 0xFFFFu ? 0 : span;
+    b.validate_ = config_.enableValidation;
+    b.status_.assign(n, 0);
+    b.values_.assign((size_t)table.size() * n, 0);
+    b.image_.assign((size_t)n * b.span_, 0);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (n && bt_extract(ctx_, b.frames_.data(), b.lens_.data(), n, table.data(), (uint32_t)table.size(),
+                        b.status_.data(), table.empty() ? nullptr : b.values_.data(),
+                        b.span_ ? b.image_.data() : nullptr) != BT_OK)
+        throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    const uint64_t ok = (uint64_t)std::count(b.status_.begin(), b.status_.end(), (uint8_t)0);
+    countParses(b.def_.name, ok, n - ok, us);
+}
+
+bool GpuProtocolParser::registerProtocol(const parser::ProtocolDefinition& protocol) {   // :41-50
+    std::unique_lock<std::shared_mutex> lk(protocols_mu_);
+    if (protocols_.find(protocol.name) != protocols_.end()) return false;
+    protocols_[protocol.name] = protocol;
+    return true;
+}
+
+bool GpuProtocolParser::unregisterProtocol(const std::string& name) {   // :52-62
+    std::unique_lock<std::shared_mutex> lk(protocols_mu_);
+    auto it = protocols_.find(name);
+    if (it == protocols_.end()) return false;
+    protocols_.erase(it);
+    return true;
+}
+
+bool GpuProtocolParser::hasProtocol(const std::string& name) const {
+    std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+    return protocols_.find(name) != protocols_.end();
+}
+
+std::vector<std::string> GpuProtocolParser::getSupportedProtocols() const {   // :193-204
+    std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+    std::vector<std::string> names;
+    names.reserve(protocols_.size());
+    for (const auto& kv : protocols_) names.push_back(kv.first);
+    return names;
+}
+
+void GpuProtocolParser::setConfig(const parser::ProtocolParser::ParserConfig& config) { config_ = config; }
+
+GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets,
+                                           const parser::ProtocolDefinition& protocol) {
+    GpuFieldBatch b;
+    b.def_ = protocol;
+    b.keep_ = packets;
+    for (const auto& p : b.keep_) {
+        b.frames_.push_back(p.data());
+        b.lens_.push_back((uint32_t)p.length());
+    }
+    extract(b);
+    return b;
+}
+
+GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets, const std::string& protocolName) {
+    parser::ProtocolDefinition def;
+    {
+        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+        auto it = protocols_.find(protocolName);
+        if (it == protocols_.end()) throw std::out_of_range("GpuProtocolParser: protocol not found: " + protocolName);
+        def = it->second;
+    }
+    return parseBatch(packets, def);
+}
+
+std::vector<GpuFieldBatch> GpuProtocolParser::parseBatchMultipleProtocols(const std::vector<Packet>& packets) {
+    std::vector<parser::ProtocolDefinition> defs;
+    {
+        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+        for (const auto& kv : protocols_) defs.push_back(kv.second);   // the reference's iteration order (:117)
+    }
+    std::vector<GpuFieldBatch> out;
+    for (const auto& d : defs) out.push_back(parseBatch(packets, d));
+    return out;
+}
+
+ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol) {
+    GpuFieldBatch b;   // :97-110; a batch of one, borrowing the caller's vector for the call
+    b.def_ = protocol;
+    b.frames_.push_back(packet.data());
+    b.lens_.push_back((uint32_t)packet.size());
+    extract(b);
+    return b.result(0);
+}
+
+ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, const std::string& protocolName) {
+    if (protocolName.empty()) {   // :70-72
+        auto all = parsePacketMultipleProtocols(packet);
+        if (all.empty()) throw std::out_of_range("GpuProtocolParser::parsePacket: no protocol registered");
+        return all[0];
+    }
+    parser::ProtocolDefinition def;
+    {
+        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+        auto it = protocols_.find(protocolName);
+        if (it == protocols_.end()) {   // :76-81: no stats update
+            ParseResult r;
+            r.status = ParseStatus::PROTOCOL_NOT_FOUND;
+            r.errorMessage = "Protocol not found: " + protocolName;
+            return r;
+        }
+        def = it->second;
+    }
+    return parsePacket(packet, def);
+}
+
+std::vector<ParseResult> GpuProtocolParser::parsePacketMultipleProtocols(const std::vector<uint8_t>& packet) {
+    std::vector<parser::ProtocolDefinition> defs;
+    {
+        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+        for (const auto& kv : protocols_) defs.push_back(kv.second);   // the reference's iteration order (:117)
+    }
+    std::vector<ParseResult> out;
+    for (const auto& d : defs) out.push_back(parsePacket(packet, d));
+    return out;
+}
+
+bool GpuProtocolParser::validatePacket(const std::vector<uint8_t>& packet, const std::string& protocolName) {
+    return parsePacket(packet, protocolName).isSuccess();
+}
+
+bool GpuProtocolParser::validatePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol) {
+    return parsePacket(packet, protocol).isSuccess();
 }
 
 }  // namespace gpu

@@ -15,11 +15,28 @@
 // ProtocolDetector::detectProtocol(frame) etc. except `confidence` of a non-Ethernet
 // frame, which the reference leaves uninitialised (ProtocolRegistry.cpp:355) and this
 // layer reports as 0.0.
+//
+// User-defined protocols (the rest of include/parser/ProtocolParser.hpp:56-93):
+// registerProtocol / unregisterProtocol / hasProtocol / getSupportedProtocols,
+// parsePacket(packet, name), parsePacket(packet, ProtocolDefinition),
+// parsePacketMultipleProtocols and validatePacket, with the reference's results, stats
+// and protocol iteration order; and the batch forms parseBatch(packets, name | definition)
+// / parseBatchMultipleProtocols, whose GpuFieldBatch holds the GPU's extracted columns
+// (bt_extract, beatrice_amd/csrc/bt_extract.hip) and materialises each packet's
+// ParseResult on demand. Differences, all where the reference is undefined: a TIMESTAMP
+// that localtime() cannot convert formats as "" (the reference crashes in put_time); a
+// BOOLEAN field of length 0 throws std::invalid_argument (the reference reads past an
+// empty vector); parsePacket(packet, "") with no protocol registered throws
+// std::out_of_range (the reference indexes an empty vector); a failed first parse does not
+// raise SIGFPE in the stats (the reference divides by successfulParses).
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "beatrice/Packet.hpp"
@@ -69,16 +86,74 @@ private:
     bt_ctx* ctx_ = nullptr;      // host pool for format(); owned by the GpuProtocolParser
 };
 
+// One user protocol over a batch: the GPU's columns (status, extractValue<T> bits per
+// numeric field, the [0, span) bytes of each packet) and ParseResult on demand.
+class GpuFieldBatch {
+public:
+    size_t size() const { return lens_.size(); }
+    const parser::ProtocolDefinition& protocol() const { return def_; }
+    parser::ParseStatus status(size_t i) const { return static_cast<parser::ParseStatus>(status_.at(i)); }
+    bool isSuccess(size_t i) const { return status_.at(i) == 0; }
+    // extractValue<T> bits of field k (0 for byte-typed fields and packets that did not parse)
+    uint64_t raw(size_t i, size_t k) const { return values_.at(k * size() + i); }
+    template <class T>
+    T value(size_t i, size_t k) const {
+        const uint64_t b = raw(i, k);
+        T v;
+        std::memcpy(&v, &b, sizeof(T));
+        return v;
+    }
+    // the field's bytes (empty when the packet did not parse)
+    std::vector<uint8_t> bytes(size_t i, size_t k) const;
+    // == ProtocolParser(config).parsePacket(packet_i, protocol()) but for wall-clock times (0)
+    parser::ParseResult result(size_t i) const;
+
+private:
+    friend class GpuProtocolParser;
+    parser::ProtocolDefinition def_;
+    bool validate_ = true;
+    uint64_t span_ = 0;
+    std::vector<uint8_t> status_;
+    std::vector<uint64_t> values_;     // field-major, column stride size()
+    std::vector<uint8_t> image_;       // size() x span_
+    std::vector<const uint8_t*> frames_;
+    std::vector<uint32_t> lens_;
+    std::vector<Packet> keep_;
+};
+
 class GpuProtocolParser {
 public:
     explicit GpuProtocolParser(int device = 0, const bt_opts* opts = nullptr);
+    explicit GpuProtocolParser(const parser::ProtocolParser::ParserConfig& config, int device = 0,
+                               const bt_opts* opts = nullptr);
     ~GpuProtocolParser();
     GpuProtocolParser(const GpuProtocolParser&) = delete;
     GpuProtocolParser& operator=(const GpuProtocolParser&) = delete;
 
+    // ---- builtin layer walk (Ethernet / VLAN / IPv4 / IPv6 / TCP / UDP / ICMP) ----
     GpuParsedBatch parseBatch(const std::vector<Packet>& packets);
     // borrows `base` for the lifetime of the returned batch
     GpuParsedBatch parseBatch(const uint8_t* base, const bt_pkt_desc* desc, uint32_t n);
+
+    // ---- user-defined protocols (ProtocolParser.hpp:63-72; ProtocolParser.cpp:41-143) ----
+    bool registerProtocol(const parser::ProtocolDefinition& protocol);
+    bool unregisterProtocol(const std::string& name);
+    bool hasProtocol(const std::string& name) const;
+    std::vector<std::string> getSupportedProtocols() const;
+    parser::ParseResult parsePacket(const std::vector<uint8_t>& packet, const std::string& protocolName = "");
+    parser::ParseResult parsePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol);
+    std::vector<parser::ParseResult> parsePacketMultipleProtocols(const std::vector<uint8_t>& packet);
+    bool validatePacket(const std::vector<uint8_t>& packet, const std::string& protocolName);
+    bool validatePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol);
+    void setConfig(const parser::ProtocolParser::ParserConfig& config);
+    const parser::ProtocolParser::ParserConfig& getConfig() const { return config_; }
+
+    // batch forms: one GPU pass per protocol over the whole batch
+    GpuFieldBatch parseBatch(const std::vector<Packet>& packets, const parser::ProtocolDefinition& protocol);
+    // PROTOCOL_NOT_FOUND has no batch form: throws std::out_of_range for an unknown name
+    GpuFieldBatch parseBatch(const std::vector<Packet>& packets, const std::string& protocolName);
+    // one batch per registered protocol, in the order parsePacketMultipleProtocols uses
+    std::vector<GpuFieldBatch> parseBatchMultipleProtocols(const std::vector<Packet>& packets);
 
     // ProtocolParser::getStats / resetStats (include/parser/ProtocolParser.hpp:40-54,
     // src/parser/ProtocolParser.cpp:174-182, updateStats :482-506): every walked layer of
@@ -92,7 +167,12 @@ public:
 
 private:
     void run(GpuParsedBatch& b);
+    void extract(GpuFieldBatch& b);
+    void countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us);
     bt_ctx* ctx_ = nullptr;
+    parser::ProtocolParser::ParserConfig config_;
+    std::unordered_map<std::string, parser::ProtocolDefinition> protocols_;   // as the reference's protocols_
+    mutable std::shared_mutex protocols_mu_;
     mutable std::mutex stats_mu_;
     parser::ProtocolParser::ParserStats stats_;
     double time_carry_us_ = 0.0;   // sub-microsecond remainder of the amortised time

@@ -468,6 +468,60 @@ typedef struct bt_timing {
 int  bt_time_device_ex(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t iters,
                        bt_timing* timing);
 
+/* ---- user-defined protocols: ProtocolParser with any ProtocolDefinition -------------
+ * Replaces ProtocolParser::parsePacketInternal / extractField / extractValue<T>
+ * (src/parser/ProtocolParser.cpp:238-433) for a table registered with registerProtocol
+ * (include/parser/ProtocolParser.hpp:63-69) or passed as a ProtocolDefinition: one
+ * kernel pass extracts every field of every packet of a batch.
+ *   span   = ProtocolDefinition::getTotalLength() (src/parser/FieldDefinition.cpp:31-46),
+ *            the largest field end; a packet shorter than span is PACKET_TOO_SHORT with no
+ *            field (:244-247), a longer one has every field (each ends within span).
+ *   values = the result of extractValue<T> for the field's type (:385-433), as the bits
+ *            of T zero-extended to 64: integer types and TIMESTAMP assemble the field's
+ *            bytes little-endian (LITTLE) or big-endian (BIG / NETWORK / HOST), byte i
+ *            shifted by (8 i) mod the width the shift is done in (32 for types narrower
+ *            than 64 bits, 64 otherwise) as x86-64 does, then cut to T; FLOAT32 / FLOAT64
+ *            are the raw bits when the length is 4 / 8, else 0; BOOLEAN is byte 0 != 0;
+ *            byte-typed fields (BYTES, STRING, MAC/IPV4/IPV6_ADDRESS, CUSTOM) are 0.
+ *   image  = the packet's bytes [0, span), from which the host materialises rawHex and
+ *            the byte-typed fields of the ParseResult.
+ * A BOOLEAN field of length 0 is rejected (BT_E_INVALID_ARGUMENT): the reference reads
+ * fieldData[0] of an empty vector there. */
+#define BT_FIELD_MAX 64u           /* fields per protocol table                          */
+enum bt_field_type {               /* FieldType (include/parser/FieldDefinition.hpp:16-35) */
+    BT_FT_UINT8 = 0, BT_FT_UINT16, BT_FT_UINT32, BT_FT_UINT64, BT_FT_INT8, BT_FT_INT16, BT_FT_INT32,
+    BT_FT_INT64, BT_FT_FLOAT32, BT_FT_FLOAT64, BT_FT_BYTES, BT_FT_STRING, BT_FT_BOOLEAN, BT_FT_MAC,
+    BT_FT_IPV4, BT_FT_IPV6, BT_FT_TIMESTAMP, BT_FT_CUSTOM
+};
+#define BT_ENDIAN_LITTLE 0u        /* Endianness::LITTLE (:37-42); 1..3 all decode big-endian */
+
+typedef struct bt_field_def {      /* FieldDefinition (:61-82): the parts extraction uses */
+    uint64_t offset;
+    uint64_t length;
+    uint32_t type;                 /* bt_field_type                                       */
+    uint32_t endianness;           /* Endianness value                                    */
+} bt_field_def;
+
+typedef struct bt_extract_out {    /* device-visible; any pointer may be NULL             */
+    uint8_t*  status;              /* n bytes: 0 SUCCESS, 9 PACKET_TOO_SHORT (ParseStatus) */
+    uint64_t* values;              /* n_fields x n_cap, field-major: values[f * n_cap + i] */
+    uint8_t*  image;               /* n x span bytes: packet i at image + i * span, its
+                                      bytes [0, span) when SUCCESS, zeros otherwise        */
+    uint32_t  n_cap;               /* values column stride (>= n)                         */
+    uint32_t  reserved;
+} bt_extract_out;
+
+/* getTotalLength() of a field table (0 for no fields). */
+int  bt_proto_span(const bt_field_def* fields, uint32_t n_fields, uint64_t* span);
+/* Device-resident extraction, asynchronous on `stream` (NULL = the context's stream);
+ * the table is copied into the launch, so it need not outlive the call. */
+int  bt_extract_device(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
+                       const bt_extract_out* out, void* stream);
+/* Host gather list in (the buffers of a std::vector<Packet>), host outputs back; waits. */
+int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                const bt_field_def* fields, uint32_t n_fields, uint8_t* status, uint64_t* values,
+                uint8_t* image);
+
 /* ---- text output --------------------------------------------------------------
  * The text the reference's ParseResult formatters print for every walked layer of
  * records [0, n) (reference src/parser/ParserResult.cpp:214-349; each layer is the

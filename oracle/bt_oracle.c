@@ -486,3 +486,74 @@ uint64_t bto_run(const uint8_t* base, const uint64_t* desc, uint32_t stride, uin
     }
     return passed;
 }
+
+/* ------------------------------------------------- user-defined protocol tables */
+/* FieldType values (reference include/parser/FieldDefinition.hpp:16-35) */
+enum { UT_U8, UT_U16, UT_U32, UT_U64, UT_I8, UT_I16, UT_I32, UT_I64, UT_F32, UT_F64, UT_BYTES, UT_STRING,
+       UT_BOOL, UT_MAC, UT_IPV4, UT_IPV6, UT_TIMESTAMP, UT_CUSTOM };
+
+/* ProtocolDefinition::getTotalLength (src/parser/FieldDefinition.cpp:31-46): the end of
+ * the first field whose end beats every earlier one. */
+static uint64_t user_total_length(const uint64_t* fields, uint32_t nf) {
+    uint64_t mo = 0, ml = 0;
+    if (!nf) return 0;
+    for (uint32_t k = 0; k < nf; ++k) {
+        const uint64_t end = fields[4 * k] + fields[4 * k + 1];
+        if (end > mo + ml) { mo = fields[4 * k]; ml = fields[4 * k + 1]; }
+    }
+    return mo + ml;
+}
+
+/* extractValue<T> (src/parser/ProtocolParser.cpp:385-433). The integer loop
+ * `value |= static_cast<T>(p[...]) << (i * 8)` shifts in int (types narrower than 32 bits
+ * are promoted), unsigned or 64-bit arithmetic; a count at or past that width is
+ * undefined in C++, and x86-64 takes it modulo the width, which is what the compiled
+ * reference does (pinned by the extract golden, lengths up to 20 on every type). */
+static uint64_t user_value(const uint8_t* p, uint64_t o, uint64_t L, uint32_t type, uint32_t endian) {
+    const int le = endian == 0;
+    uint64_t v = 0;
+    switch (type) {
+    case UT_F32:
+    case UT_F64: {
+        const uint64_t want = type == UT_F32 ? 4 : 8;
+        if (L != want) return 0;
+        for (uint64_t i = 0; i < want; ++i) v |= (uint64_t)p[o + (le ? i : want - 1 - i)] << (8 * i);
+        return v;
+    }
+    case UT_BOOL: return p[o] != 0;
+    case UT_BYTES: case UT_STRING: case UT_MAC: case UT_IPV4: case UT_IPV6: case UT_CUSTOM: return 0;
+    default: {
+        const int wide = type == UT_U64 || type == UT_I64 || type == UT_TIMESTAMP;
+        const uint32_t width = (type == UT_U8 || type == UT_I8) ? 8 : (type == UT_U16 || type == UT_I16) ? 16
+                             : (type == UT_U32 || type == UT_I32) ? 32 : 64;
+        for (uint64_t i = 0; i < L; ++i) {
+            const uint64_t b = p[o + (le ? i : L - 1 - i)];
+            v |= b << ((8 * i) & (wide ? 63 : 31));
+        }
+        return width == 64 ? v : (v & ((1ull << width) - 1));
+    }
+    }
+}
+
+uint64_t bto_extract(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n,
+                     const uint64_t* fields, uint32_t nf, uint8_t* status, uint64_t* values, uint8_t* image) {
+    const uint64_t span = user_total_length(fields, nf);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* f = desc ? base + (desc[i] & 0xFFFFFFFFFFFFull) : base + (uint64_t)i * stride;
+        const uint64_t len = desc ? desc[i] >> 48 : stride;
+        const int ok = len >= span;   /* parsePacketInternal :244-247 */
+        if (status) status[i] = ok ? 0 : 9;
+        for (uint32_t k = 0; values && k < nf; ++k) {
+            const uint64_t o = fields[4 * k], L = fields[4 * k + 1];
+            /* :251-254: a field past the packet is skipped (never, once len >= span) */
+            values[(uint64_t)k * n + i] = ok && o + L <= len
+                ? user_value(f, o, L, (uint32_t)fields[4 * k + 2], (uint32_t)fields[4 * k + 3]) : 0;
+        }
+        if (image && span) {
+            uint8_t* out = image + (uint64_t)i * span;
+            if (ok) memcpy(out, f, span);
+            else memset(out, 0, span);
+        }
+    }
+    return span;
+}

@@ -39,6 +39,15 @@ uint64_t bto_run(const uint8_t* base, const uint64_t* desc, uint32_t stride, uin
                  const bto_filter* f, uint32_t nf, uint8_t* records, uint8_t* decide,
                  int nthreads);
 
+/* User-defined protocol tables: ProtocolParser::parsePacket(frame, ProtocolDefinition)
+ * (reference src/parser/ProtocolParser.cpp:238-433). fields[4k..4k+3] = {offset, length,
+ * FieldType, Endianness}. status[i] = ParseStatus (0 SUCCESS / 9 PACKET_TOO_SHORT);
+ * values[k * n + i] = the bits of extractValue<T> zero-extended (bool 0/1, byte types 0);
+ * image + i * span = the frame's bytes [0, span) when SUCCESS, zeros otherwise (any
+ * output may be NULL). Returns the table's span (getTotalLength). */
+uint64_t bto_extract(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n,
+                     const uint64_t* fields, uint32_t nf, uint8_t* status, uint64_t* values, uint8_t* image);
+
 #ifdef __cplusplus
 }
 #endif

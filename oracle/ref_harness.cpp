@@ -22,6 +22,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <variant>
+#include <type_traits>
 
 using beatrice::Packet;
 using beatrice::PacketFilter;
@@ -350,6 +352,55 @@ int ref_filter_batch(const uint8_t* base, const uint64_t* desc, uint32_t stride,
         *what = 3;
     }
     return 1;
+}
+
+// ProtocolParser::parsePacket(frame, ProtocolDefinition) (reference
+// src/parser/ProtocolParser.cpp:97-110 -> parsePacketInternal :238-284) with a user field
+// table, over every frame: fields[4k..4k+3] = {offset, length, FieldType, Endianness}.
+// Outputs per packet: status (ParseStatus), per field the bits of the alternative the
+// FieldValue variant holds (arithmetic types memcpy'd into a zeroed u64, bool 0/1,
+// vectors / strings 0) at values[k * n + i], and the field's bytes decoded from its
+// rawHex, concatenated in table order at fb + i * fb_stride (zeros for a packet that did
+// not parse). Metrics are off (updateStats divides by successfulParses). Returns the
+// number of packets whose result has a field count other than 0 or nf.
+int ref_extract(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n, const uint64_t* fields,
+                uint32_t nf, uint8_t* status, uint64_t* values, uint8_t* fb, uint64_t fb_stride) {
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    ProtocolParser parser(cfg);
+    ProtocolDefinition def("USER", "1.0");
+    for (uint32_t k = 0; k < nf; ++k)
+        def.addField(FieldDefinition("f" + std::to_string(k), (size_t)fields[4 * k], (size_t)fields[4 * k + 1],
+                                     static_cast<FieldType>(fields[4 * k + 2]),
+                                     static_cast<Endianness>(fields[4 * k + 3])));
+    int odd = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t len;
+        const uint8_t* f = frame_at(base, desc, stride, i, &len);
+        const ParseResult r = parser.parsePacket(std::vector<uint8_t>(f, f + len), def);
+        status[i] = static_cast<uint8_t>(r.status);
+        if (r.fields.size() != 0 && r.fields.size() != nf) ++odd;
+        uint8_t* out = fb + (uint64_t)i * fb_stride;
+        std::memset(out, 0, fb_stride);
+        uint64_t at = 0;
+        for (uint32_t k = 0; k < nf; ++k) {
+            uint64_t bits = 0;
+            auto it = r.fields.find("f" + std::to_string(k));
+            if (it != r.fields.end()) {
+                std::visit([&](const auto& v) {
+                    using V = std::decay_t<decltype(v)>;
+                    if constexpr (std::is_same_v<V, bool>) bits = v ? 1u : 0u;
+                    else if constexpr (std::is_arithmetic_v<V>) std::memcpy(&bits, &v, sizeof(V));
+                }, it->second.value);
+                const std::string& hx = it->second.rawHex;
+                for (size_t b = 0; 2 * b + 1 < hx.size(); ++b)
+                    out[at + b] = (uint8_t)std::stoi(hx.substr(2 * b, 2), nullptr, 16);
+            }
+            values[(uint64_t)k * n + i] = bits;
+            at += fields[4 * k + 1];
+        }
+    }
+    return odd;
 }
 
 // CPU baseline: the reference parser (one parsePacket per walked layer) and the

@@ -17,6 +17,9 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <random>
+#include <variant>
+#include <type_traits>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -266,6 +269,157 @@ static bool parser_case(const char* label, const Capture& cap) {
     return true;
 }
 
+// ---- user-defined protocols: GpuProtocolParser vs ProtocolParser with the same tables ----
+static bool same_value(const beatrice::parser::FieldValue& x, const beatrice::parser::FieldValue& y) {
+    if (x.value.index() != y.value.index()) return false;
+    return std::visit([&](const auto& a) {
+        using V = std::decay_t<decltype(a)>;
+        const V& b = std::get<V>(y.value);
+        if constexpr (std::is_arithmetic_v<V>) return std::memcmp(&a, &b, sizeof(V)) == 0;   // NaN payloads too
+        else return a == b;
+    }, x.value);
+}
+
+static bool same_fv(const beatrice::parser::FieldValue& x, const beatrice::parser::FieldValue& y) {
+    return same_value(x, y) && x.type == y.type && x.rawHex == y.rawHex && x.formatted == y.formatted &&
+           x.valid == y.valid && x.errorMessage == y.errorMessage;
+}
+
+static bool same_result(const char* label, size_t i, const beatrice::parser::ParseResult& want,
+                        const beatrice::parser::ParseResult& got) {
+    CHECK(want.status == got.status && want.protocolName == got.protocolName &&
+              want.protocolVersion == got.protocolVersion && want.errorMessage == got.errorMessage &&
+              want.packetLength == got.packetLength && want.parsedBytes == got.parsedBytes && want.rawData == got.rawData,
+          "%s: packet %zu result header differs (status %d/%d)", label, i, (int)want.status, (int)got.status);
+    std::vector<std::string> ka, kb;
+    for (const auto& kv : want.fields) ka.push_back(kv.first);
+    for (const auto& kv : got.fields) kb.push_back(kv.first);
+    CHECK(ka == kb, "%s: packet %zu field order differs", label, i);
+    for (const auto& kv : want.fields)
+        CHECK(same_fv(kv.second, got.fields.at(kv.first)), "%s: packet %zu field %s differs (raw %s/%s fmt %s/%s)", label,
+              i, kv.first.c_str(), kv.second.rawHex.c_str(), got.fields.at(kv.first).rawHex.c_str(),
+              kv.second.formatted.c_str(), got.fields.at(kv.first).formatted.c_str());
+    CHECK(want.validationResults.size() == got.validationResults.size(), "%s: packet %zu validation count %zu/%zu", label,
+          i, want.validationResults.size(), got.validationResults.size());
+    for (size_t k = 0; k < want.validationResults.size(); ++k)
+        CHECK(want.validationResults[k].fieldName == got.validationResults[k].fieldName &&
+                  want.validationResults[k].valid == got.validationResults[k].valid &&
+                  want.validationResults[k].errorMessage == got.validationResults[k].errorMessage,
+              "%s: packet %zu validation result %zu differs", label, i, k);
+    return true;
+}
+
+static beatrice::parser::ProtocolDefinition parser_example_protocol() {   // examples/parser_example.cpp:18-22
+    using namespace beatrice::parser;
+    ProtocolDefinition p("CUSTOM_PROTO", "1.0");
+    p.addField(FieldFactory::createUInt32Field("header", 0, Endianness::NETWORK, true, "Protocol header"));
+    p.addField(FieldFactory::createUInt8Field("version", 4, true, "Protocol version"));
+    p.addField(FieldFactory::createUInt16Field("length", 5, Endianness::NETWORK, true, "Data length"));
+    p.addField(FieldFactory::createBytesField("data", 7, 10, "Payload data"));
+    return p;
+}
+
+static beatrice::parser::ProtocolDefinition random_protocol(std::mt19937& rng, int k) {
+    using namespace beatrice::parser;
+    ProtocolDefinition p("USER_" + std::to_string(k), std::to_string(k % 3) + ".0");
+    const int nf = 1 + (int)(rng() % 10);
+    static const size_t natural[18] = {1, 2, 4, 8, 1, 2, 4, 8, 4, 8, 0, 0, 1, 6, 4, 16, 8, 0};
+    for (int f = 0; f < nf; ++f) {
+        const auto t = static_cast<FieldType>(rng() % 18);
+        size_t len = (natural[(int)t] && rng() % 10 < 6) ? natural[(int)t] : rng() % 21;
+        if (t == FieldType::TIMESTAMP) len = rng() % 6;   // localtime() range (the reference crashes past it)
+        if (t == FieldType::BOOLEAN && len == 0) len = 1;
+        const size_t off = (k % 4 == 3 && rng() % 2) ? 200 + rng() % 100 : rng() % 80;
+        FieldDefinition fd("f" + std::to_string(f) + (rng() % 7 == 0 ? "" : "_" + std::to_string(rng() % 100)), off, len, t,
+                           static_cast<Endianness>(rng() % 4));
+        if (rng() % 5 == 0) {   // value / pattern constraints (validateField, ProtocolParser.cpp:435-475)
+            FieldConstraint c;
+            if (rng() % 2) { c.minValue = (uint64_t)(rng() % 64); c.maxValue = (uint64_t)(64 + rng() % 200); }
+            static const char* pats[] = {"", "1", "invalid", "bytes]", "true", ":", "0"};
+            c.pattern = pats[rng() % 7];
+            fd.constraint = c;
+        }
+        if (t == FieldType::CUSTOM && rng() % 2)
+            fd.formatter = [](const std::vector<uint8_t>& b) {
+                return "n=" + std::to_string(b.size()) + (b.empty() ? "" : "/" + std::to_string(b[0]));
+            };
+        p.addField(fd);
+    }
+    return p;
+}
+
+static bool user_proto_case(const char* label, const Capture& cap) {
+    using namespace beatrice::parser;
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    ProtocolParser ref(cfg);
+    beatrice::gpu::GpuProtocolParser gpu(cfg, 0);
+    std::mt19937 rng(0xB1A5);
+    std::vector<ProtocolDefinition> defs{parser_example_protocol(), ProtocolDefinition("EMPTY", "0")};
+    for (int k = 0; k < 24; ++k) defs.push_back(random_protocol(rng, k));
+    size_t nres = 0;
+    for (const auto& d : defs) {
+        CHECK(ref.registerProtocol(d) == gpu.registerProtocol(d), "%s: registerProtocol(%s)", label, d.name.c_str());
+        auto b = gpu.parseBatch(cap.packets, d);
+        for (size_t i = 0; i < cap.packets.size(); ++i) {
+            const uint8_t* f = cap.packets[i].data();
+            const std::vector<uint8_t> v(f, f + cap.packets[i].length());
+            ParseResult want = ref.parsePacket(v, d);
+            if (!same_result(label, i, want, b.result(i))) return false;
+            ++nres;
+        }
+    }
+    CHECK(ref.registerProtocol(defs[0]) == gpu.registerProtocol(defs[0]), "%s: duplicate registerProtocol", label);
+    CHECK(ref.getSupportedProtocols() == gpu.getSupportedProtocols(), "%s: getSupportedProtocols order", label);
+    // parser_example's own calls (examples/parser_example.cpp:31-83): by name, and its JSON
+    const std::vector<uint8_t> kat = {0x12, 0x34, 0x56, 0x78, 0x01, 0x00, 0x0A, 0xAA, 0xBB,
+                                      0xCC, 0xDD, 0xEE, 0xFF, 0x11, 0x22, 0x33, 0x44};
+    ParseResult want = ref.parsePacket(kat, "CUSTOM_PROTO"), got = gpu.parsePacket(kat, "CUSTOM_PROTO");
+    if (!same_result("parser_example", 0, want, got)) return false;
+    for (auto& kv : want.fields) kv.second.parseTime = std::chrono::microseconds(0);
+    CHECK(want.toJsonString() == got.toJsonString(), "parser_example: JSON differs");
+    CHECK(got.getFieldUInt("header") == 0x12345678u && got.getFieldUInt("version") == 1 &&
+              got.getFieldUInt("length") == 10 && got.getFieldBytes("data").size() == 10,
+          "parser_example: known answer (header 0x12345678, version 1, length 10, 10 data bytes)");
+    // by name, unknown name, all protocols, validatePacket
+    for (size_t i = 0; i < cap.packets.size() && i < 200; ++i) {
+        const std::vector<uint8_t> v(cap.packets[i].data(), cap.packets[i].data() + cap.packets[i].length());
+        auto w = ref.parsePacketMultipleProtocols(v), g = gpu.parsePacketMultipleProtocols(v);
+        CHECK(w.size() == g.size(), "%s: parsePacketMultipleProtocols size", label);
+        for (size_t k = 0; k < w.size(); ++k)
+            if (!same_result(label, i, w[k], g[k])) return false;
+        if (!same_result(label, i, ref.parsePacket(v, "USER_3"), gpu.parsePacket(v, "USER_3"))) return false;
+        if (!same_result(label, i, ref.parsePacket(v, "NO_SUCH"), gpu.parsePacket(v, "NO_SUCH"))) return false;
+        if (!same_result(label, i, ref.parsePacket(v, ""), gpu.parsePacket(v, ""))) return false;
+        CHECK(ref.validatePacket(v, "USER_5") == gpu.validatePacket(v, "USER_5"), "%s: validatePacket", label);
+    }
+    CHECK(ref.unregisterProtocol("USER_2") == gpu.unregisterProtocol("USER_2") &&
+              ref.unregisterProtocol("USER_2") == gpu.unregisterProtocol("USER_2") &&
+              ref.hasProtocol("USER_2") == gpu.hasProtocol("USER_2"),
+          "%s: unregisterProtocol / hasProtocol", label);
+    // stats with metrics on (the reference's default): the first parse must succeed there
+    {
+        ProtocolParser counted;
+        beatrice::gpu::GpuProtocolParser gcount(ProtocolParser::ParserConfig{}, 0);
+        (void)counted.parsePacket(kat, defs[0]);
+        (void)gcount.parsePacket(kat, defs[0]);
+        for (size_t k = 1; k < 6; ++k) {
+            (void)gcount.parseBatch(cap.packets, defs[k]);
+            for (const auto& p : cap.packets)
+                (void)counted.parsePacket(std::vector<uint8_t>(p.data(), p.data() + p.length()), defs[k]);
+        }
+        const auto w = counted.getStats(), g = gcount.getStats();
+        CHECK(w.totalPacketsParsed == g.totalPacketsParsed && w.successfulParses == g.successfulParses &&
+                  w.failedParses == g.failedParses && w.protocolUsageCount == g.protocolUsageCount,
+              "%s: user-protocol stats differ: total %lu/%lu ok %lu/%lu", label, (unsigned long)w.totalPacketsParsed,
+              (unsigned long)g.totalPacketsParsed, (unsigned long)w.successfulParses, (unsigned long)g.successfulParses);
+    }
+    std::printf("ok   proto   %-22s %zu packets x %zu tables (parser_example + random, constraints, CUSTOM "
+                "formatters): %zu ParseResults, by-name / multiple / unknown / stats\n",
+                label, cap.packets.size(), defs.size(), nres);
+    return true;
+}
+
 static bool plugin_case(const Capture& cap, const char* so) {
     setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|3|udp;net|IP_RANGE|2|10.0.0.0/8;ports|PORT_RANGE|1|1000-2000", 1);
     setenv("BEATRICE_GPU_BATCH", "4096", 1);
@@ -349,6 +503,8 @@ int main(int argc, char** argv) {
     ok &= parser_case("c3", c3);
     ok &= parser_case("c4", c4);
     ok &= parser_case("fuzz", fz);
+    ok &= user_proto_case("fuzz", fz);
+    ok &= user_proto_case("c3", c3);
     ok &= plugin_case(c3, plugin_so);
     std::printf("%s (%d failures)\n", ok && !g_fail ? "ALL OK" : "FAILED", g_fail);
     return ok && !g_fail ? 0 : 1;

@@ -50,6 +50,10 @@ def oracle():
         if not os.path.exists(ORACLE_SO):
             raise RuntimeError("oracle/libbt_oracle.so missing: make -C oracle")
         L = ctypes.CDLL(ORACLE_SO)
+        L.bto_extract.restype = ctypes.c_uint64
+        L.bto_extract.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p]
         L.bto_run.restype = ctypes.c_uint64
         L.bto_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
@@ -76,6 +80,10 @@ def ref():
         L.ref_filter_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.ref_extract.restype = ctypes.c_int
+        L.ref_extract.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_uint64]
         L.ref_bench.restype = ctypes.c_uint64
         L.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
@@ -132,3 +140,42 @@ def ref_bench(data, desc, n, filters, parse=True, threads=8, seconds=10.0, strid
     done = ref().ref_bench(_ptr(data), _ptr(desc), stride, n, f, len(filters), int(parse), threads,
                            seconds, ctypes.byref(el))
     return int(done), el.value
+
+
+def table_array(fields):
+    """fields: list of (offset, length, type, endianness) -> contiguous u64[nf, 4]."""
+    return np.ascontiguousarray(np.asarray(fields, dtype=np.uint64).reshape(-1, 4))
+
+
+def oracle_extract(data, desc, n, fields, stride=0):
+    """C restatement (bto_extract): (status[n], values[nf, n], image[n, span], span)."""
+    t = table_array(fields)
+    nf = len(t)
+    span = oracle().bto_extract(None, None, 0, 0, t.ctypes.data, nf, None, None, None)
+    status = np.zeros(n, np.uint8)
+    values = np.zeros((nf, n), np.uint64)
+    image = np.zeros((n, max(span, 1)), np.uint8)
+    oracle().bto_extract(_ptr(data), _ptr(desc), stride, n, t.ctypes.data, nf, status.ctypes.data,
+                         values.ctypes.data, image.ctypes.data)
+    return status, values, image[:, :span], int(span)
+
+
+def ref_extract(data, desc, n, fields, stride=0):
+    """The compiled reference's ProtocolParser::parsePacket(frame, ProtocolDefinition):
+    (status[n], values[nf, n], field_bytes[n, sum(length)])."""
+    t = table_array(fields)
+    nf = len(t)
+    fbw = int(t[:, 1].sum()) if nf else 0
+    status = np.zeros(n, np.uint8)
+    values = np.zeros((nf, n), np.uint64)
+    fb = np.zeros((n, max(fbw, 1)), np.uint8)
+    odd = ref().ref_extract(_ptr(data), _ptr(desc), stride, n, t.ctypes.data, nf, status.ctypes.data,
+                            values.ctypes.data, fb.ctypes.data, max(fbw, 1))
+    assert odd == 0, f"{odd} reference results with a partial field set"
+    return status, values, fb[:, :fbw]
+
+
+def field_bytes_of_image(image, fields):
+    """The concatenated field bytes (ref_extract's layout) cut out of [0, span) images."""
+    parts = [image[:, int(o):int(o) + int(ln)] for o, ln, _, _ in fields]
+    return np.concatenate(parts, axis=1) if parts else np.zeros((len(image), 0), np.uint8)
