@@ -22,6 +22,10 @@
  *                       host batch (pinned staging, H2D -> kernels -> D2H).
  *   bt_parse_filter_device  the same over device-resident buffers, async on a
  *                       caller stream (the hot path that bench.py measures).
+ *   bt_extract_device / bt_extract
+ *                       ProtocolParser::parsePacket(packet, ProtocolDefinition) and the
+ *                       by-name form for registered user protocols
+ *                       (src/parser/ProtocolParser.cpp:69-110, :238-433) over a batch.
  *
  * Record layout (bt_rec, 96 B per packet). Each layer L found by the layer walk
  * (DESIGN.md "R-WALK") has the field values that
@@ -517,7 +521,9 @@ int  bt_proto_span(const bt_field_def* fields, uint32_t n_fields, uint64_t* span
  * the table is copied into the launch, so it need not outlive the call. */
 int  bt_extract_device(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
                        const bt_extract_out* out, void* stream);
-/* Host gather list in (the buffers of a std::vector<Packet>), host outputs back; waits. */
+/* Host gather list in (the buffers of a std::vector<Packet>), host outputs back; waits.
+ * status: n bytes; values: n_fields x n, values[f * n + i]; image: n x span bytes. Only the
+ * [0, span) prefix of each frame is staged for the device. */
 int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                 const bt_field_def* fields, uint32_t n_fields, uint8_t* status, uint64_t* values,
                 uint8_t* image);
