@@ -115,3 +115,62 @@ def test_rocprof_stats_agree_with_bench_events(cfg):
     assert under["roofline"]["kernel"] in rows[0]["Name"]
     avg_ms = float(rows[0]["AverageNs"]) / 1e6
     assert avg_ms == pytest.approx(under["roofline"]["kernel_ms"], rel=0.05)
+
+
+R02 = os.path.join(ROOT, "profiles", "r02")
+
+
+def _check_entry(e, n_gpus=1):
+    n = e["packets_per_gpu"] if "packets_per_gpu" in e else e["config"]["packets_per_gpu"]
+    r = e["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_floor", "kernel_ms"):
+        assert k in r, k
+    achieved = r["algorithmic_bytes_per_packet"] * n / (r["kernel_ms"] * 1e-3) / 1e9
+    assert r["achieved"] == pytest.approx(achieved, rel=2e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
+    # wall time of the timed region agrees with the GPU span (round-1 verdict: within 5 %)
+    t = e["timing"]
+    assert t["spin_rc"] == 0 and 0.99 <= t["wall_over_span"] <= 1.05, t
+    if r["traffic"] is not None:
+        assert r["traffic_source"] == "profiles/traffic.json"
+        # measured traffic is never below the 128-B-line floor by more than L2 reuse explains
+        assert r["traffic_bytes_per_packet"] >= 0.97 * r["traffic_floor_bytes_per_packet"]
+
+
+def test_r02_default_line_covers_every_config():
+    d = _line(os.path.join(R02, "bench_default.json"))
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["n_gpus"] == 1 and "parse + PacketFilter" in d["config"]["workload"] and "64B" in d["config"]["workload"]
+    _check_entry(d)
+    assert d["cpu_baseline"]["kind"] == "reference" and d["cpu_baseline"]["cores"] >= 1
+    assert set(d["configs"]) == {"c2", "c3", "c4"}
+    for k, e in d["configs"].items():
+        _check_entry(e)
+        assert e["cpu_baseline"] and e["cpu_baseline"]["value"] > 0, k
+    assert d["value"] == pytest.approx(d["config"]["packets_total"] / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
+
+
+def test_r02_two_rank_line_has_per_rank_entries():
+    d = _line(os.path.join(R02, "bench_2rank_one_gpu.json"))
+    assert d["n_gpus"] == 2 and len(d["per_rank"]) == 2
+    assert set(d["configs"]) == {"c3", "c3_strong"}
+    assert d["configs"]["c3"]["scaling"] == "weak" and d["configs"]["c3_strong"]["scaling"] == "strong"
+    s = d["configs"]["c3_strong"]
+    assert sum(r["packets"] for r in s["per_rank"]) == s["packets_total"] == 1 << 24
+
+
+@pytest.mark.parametrize("cfg", ["c2f", "c2", "c3", "c4"])
+def test_r02_rocprof_stats_agree_with_bench_events(cfg):
+    under = _line(os.path.join(R02, "prof", f"{cfg}_bench_under_rocprof.json"))
+    with open(os.path.join(R02, "prof", f"{cfg}_kernel_stats.csv")) as fh:
+        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"]]
+    assert len(rows) == 1
+    assert under["roofline"]["kernel"] in rows[0]["Name"]
+    assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(under["roofline"]["kernel_ms"], rel=0.05)
+
+
+def test_committed_traffic_is_keyed_to_these_kernels():
+    d = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    assert set(d) >= {"c2f", "c2", "c3", "c4"}
+    for k, v in d.items():
+        assert v["kernel_src_sha"] == bench.kernel_source_sha(), f"{k}: PMC traffic measured on other kernel sources"
