@@ -241,6 +241,25 @@ def record_write_stats(run) -> tuple[int, int]:
     return stored, lines
 
 
+def record_write_stats_planes(run) -> tuple[int, int]:
+    """(record bytes stored, 128-B lines) for the plane-major layout: slab k of packet i at
+    plane k, row i; a wave stores slab k for its live lanes when any of them needs it."""
+    n = run.n
+    rec = run.d_rec.download(np.zeros(run.d_rec.nbytes, np.uint8))
+    ok = rec[n * 16: 2 * n * 16].reshape(n, 16)[:, 1].astype(np.int64)
+    nd = 5 + ((ok & abi.L_VLAN0) != 0) + ((ok & abi.L_VLAN1) != 0) + \
+        np.where(ok & abi.L_IPV4, 5, np.where(ok & abi.L_IPV6, 10, 0)) + \
+        np.where(ok & abi.L_TCP, 5, np.where(ok & (abi.L_UDP | abi.L_ICMP), 2, 0))
+    nt = (n + 63) // 64
+    ns = np.zeros(nt * 64, np.int64)
+    ns[:n] = (nd + 3) // 4
+    ns = ns.reshape(nt, 64)
+    live = np.minimum(64, n - np.arange(nt) * 64)
+    planes = 2 + sum((ns > k).any(axis=1).astype(np.int64) for k in range(2, 6))
+    stored = int((planes * live).sum()) * 16
+    return stored, -(-stored // LINE)
+
+
 def load_traffic(path, key, n):
     """Per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py), if the
     committed figure was measured on these kernel sources and this batch size."""
@@ -284,7 +303,15 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
         run.run()
     ctx.time_device_ex(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
     n_pass = run.n_pass() if filt else 0
-    rec_bytes, rec_lines = record_write_stats(run) if run.d_rec is not None and n else (0, 0)
+    if run.d_rec is None or not n:
+        rec_bytes, rec_lines = 0, 0
+    elif flags & abi.OPT_RECORDS_AOS:   # 96-B bt_rec per packet, contiguous
+        rec_bytes = n * abi.BT_REC_BYTES
+        rec_lines = -(-rec_bytes // LINE)
+    elif flags & abi.OPT_RECORDS_PLANES:   # six 16-B planes, slab k stored when any lane of the tile needs it
+        rec_bytes, rec_lines = record_write_stats_planes(run)
+    else:
+        rec_bytes, rec_lines = record_write_stats(run)
     # A few untimed steps right before the timed region, so the GPU does not sit idle
     # through the host work above between warm-up and t0 (they are drained by the sync).
     for _ in range(2):
