@@ -8,7 +8,7 @@ for cfg in $CFGS; do
   for i in $(seq $REPS); do
     for v in A B; do
       E=$EA; [ $v = B ] && E=$EB
-      env $E timeout -k 10 200 python bench.py --config $cfg --steps 30 --warmup 3 --no-cpu $EXTRA > gpurun_out/abe_${cfg}_${v}_$i.json 2>&1 || { tail -5 gpurun_out/abe_${cfg}_${v}_$i.json; exit 3; }
+      env $E timeout -k 10 200 python bench.py --configs none --config $cfg --steps 20 --warmup 3 --no-cpu $EXTRA > gpurun_out/abe_${cfg}_${v}_$i.json 2>&1 || { tail -5 gpurun_out/abe_${cfg}_${v}_$i.json; exit 3; }
       summ gpurun_out/abe_${cfg}_${v}_$i.json $cfg $v
     done
   done

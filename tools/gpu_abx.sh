@@ -2,12 +2,12 @@
 #   bash tools/gpu_abx.sh <libA.so> <libB.so> "<configs>" [reps] [extra bench args]
 mkdir -p gpurun_out
 A=$1; B=$2; CFGS=$3; REPS=${4:-3}; shift 4; EXTRA="$@"
-summ() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], sys.argv[3], d['value'], 'Mpps step', d['ms_per_step'], 'kern', r['kernel_ms'])" $1 $2 $3; }
+summ() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline']; print(sys.argv[2], sys.argv[3], d['value'], 'Mpps step', d['ms_per_step'], 'kern', r['kernel_ms'])" $1 $2 $3; }
 for cfg in $CFGS; do
   for i in $(seq $REPS); do
     for v in A B; do
       L=$A; [ $v = B ] && L=$B
-      BT_LIB_PATH=$PWD/$L timeout -k 10 200 python bench.py --config $cfg --steps 30 --warmup 3 --no-cpu $EXTRA > gpurun_out/ab_${cfg}_${v}_$i.json 2>&1 || { tail -5 gpurun_out/ab_${cfg}_${v}_$i.json; exit 3; }
+      BT_LIB_PATH=$PWD/$L timeout -k 10 200 python bench.py --configs none --config $cfg --steps 20 --warmup 3 --no-cpu $EXTRA > gpurun_out/ab_${cfg}_${v}_$i.json 2>&1 || { tail -5 gpurun_out/ab_${cfg}_${v}_$i.json; exit 3; }
       summ gpurun_out/ab_${cfg}_${v}_$i.json $cfg $v
     done
   done
