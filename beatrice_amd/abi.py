@@ -141,7 +141,7 @@ EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_record_gather", "bt_record_gather_planes",
+    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
@@ -189,6 +189,8 @@ def lib() -> ctypes.CDLL:
         "bt_proto_span": (ctypes.c_int, [vp, u32, ctypes.POINTER(u64)]),
         "bt_extract_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), vp]),
         "bt_extract": (ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, vp]),
+        "bt_time_extract_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), u32,
+                                              ctypes.POINTER(Timing)]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
         "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
@@ -647,19 +649,24 @@ class DeviceRun:
 class DeviceExtract:
     """Device-resident batch for bt_extract_device (user protocol tables)."""
 
-    def __init__(self, ctx: Context, data: np.ndarray, desc: np.ndarray | None, n: int, fields, stride: int = 0,
-                 desc_format: int = DESC_PACKED, image=True):
+    def __init__(self, ctx: Context, data: np.ndarray | None, desc: np.ndarray | None, n: int, fields, stride: int = 0,
+                 desc_format: int = DESC_PACKED, image=True, batch: Batch | None = None):
+        """data / desc are uploaded; or `batch` names packets already on the device
+        (e.g. a DeviceRun's), which this object then neither owns nor frees."""
         self.ctx, self.n = ctx, n
         self.fields = list(fields)
         self.span = proto_span(self.fields)
-        self.d_data = ctx.alloc((data.nbytes + 255) // 256 * 256 + 256)
-        self.d_data.upload(data)
-        self.d_desc = None
-        if desc is not None:
-            self.d_desc = ctx.alloc(max(16, desc.nbytes))
-            self.d_desc.upload(np.ascontiguousarray(desc))
-        self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n, int(data.nbytes),
-                           desc_format, 0)
+        self.d_data = self.d_desc = None
+        if batch is not None:
+            self.batch = batch
+        else:
+            self.d_data = ctx.alloc((data.nbytes + 255) // 256 * 256 + 256)
+            self.d_data.upload(data)
+            if desc is not None:
+                self.d_desc = ctx.alloc(max(16, desc.nbytes))
+                self.d_desc.upload(np.ascontiguousarray(desc))
+            self.batch = Batch(self.d_data.ptr, self.d_desc.ptr if self.d_desc else None, stride, n,
+                               int(data.nbytes), desc_format, 0)
         nf = len(self.fields)
         img = image and 0 < self.span <= 0xFFFF
         self.d_status = ctx.alloc(max(16, n))
@@ -672,6 +679,13 @@ class DeviceExtract:
     def run(self, stream=None):
         _check(lib().bt_extract_device(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
                                        ctypes.byref(self.out), stream))
+
+    def time(self, iters: int) -> Timing:
+        """bt_time_extract_ex: `iters` launches, each timed from its own dispatch."""
+        t = Timing()
+        _check(lib().bt_time_extract_ex(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
+                                        ctypes.byref(self.out), iters, ctypes.byref(t)))
+        return t
 
     def fetch(self):
         self.ctx.synchronize()

@@ -86,7 +86,7 @@ struct ExTable {                      // kernel argument
     uint32_t n;                       // fields
     uint32_t span;                    // getTotalLength()
     uint32_t window;                  // min(span, kExWindow)
-    uint32_t pad;
+    uint32_t row_dw;                  // LDS dwords per staged packet (set by launch_extract)
     ExField f[BT_FIELD_MAX];
 };
 struct ExArgs {
@@ -100,7 +100,8 @@ struct ExArgs {
     uint8_t* image;
     uint32_t n_cap;
 };
-int launch_extract(const ExArgs& a, const ExTable& tab, void* stream);
+int launch_extract(const ExArgs& a, const ExTable& tab, void* stream, void* timing_start = nullptr,
+                   void* timing_stop = nullptr);
 
 // Host filter compiler (bt_filter_compile.cpp): pure C++, no device needed.
 int compile_filters(const bt_filter_desc* f, uint32_t n, bt_filter_slot* out, uint32_t cap,

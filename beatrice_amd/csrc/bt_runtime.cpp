@@ -504,15 +504,79 @@ int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, vo
     return run_device(c, b, o, st, false, nullptr, nullptr);
 }
 
-int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
-    if (!c || !b || !o || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
-    std::lock_guard<std::mutex> lk(c->mu);
-    HIP_TRY(hipSetDevice(c->device));
+// The host side of a timed loop whose launches (K of them, each between the event pair
+// c->tev[2i], c->tev[2i+1]) were enqueued on c->stream after c->ev0 at h0, followed by
+// c->ev1: wait by polling, then fill the breakdown.
+static int finish_timing(bt_ctx* c, uint32_t iters, bool no_kernel_events, std::chrono::steady_clock::time_point h0,
+                         bt_timing* t, const char* who) {
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    const auto h1 = clk::now();
+    // Poll instead of hipEventSynchronize: a blocking wait is woken by an interrupt, whose
+    // latency would sit inside the caller's timed region.
+    auto poll = [](hipEvent_t e) -> hipError_t {
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q != hipErrorNotReady) return q;
+        }
+    };
+    HIP_TRY(poll(c->ev0));
+    const auto h2 = clk::now();
+    HIP_TRY(poll(c->ev1));
+    const auto h3 = clk::now();
+    float tot = 0, k = 0, kmin = 1e30f, kmax = 0, lead = 0, gap = 0;
+    HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
+    for (uint32_t i = 0; !no_kernel_events && i < iters; ++i) {
+        float x = 0;
+        HIP_TRY(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
+        k += x;
+        kmin = std::min(kmin, x);
+        kmax = std::max(kmax, x);
+        if (i + 1 < iters) {
+            float g = 0;
+            HIP_TRY(hipEventElapsedTime(&g, c->tev[2 * i + 1], c->tev[2 * i + 2]));
+            gap += g;
+        }
+    }
+    if (!no_kernel_events) HIP_TRY(hipEventElapsedTime(&lead, c->ev0, c->tev[0]));
+    const auto h4 = clk::now();
+    if (t) {
+        *t = bt_timing{};
+        t->span_ms = tot;
+        t->main_ms = no_kernel_events ? -1.0f : k / iters;
+        t->main_min_ms = no_kernel_events ? -1.0f : kmin;
+        t->main_max_ms = no_kernel_events ? -1.0f : kmax;
+        t->lead_ms = lead;
+        t->gap_ms = gap;
+        t->enqueue_ms = ms(h0, h1);
+        t->first_seen_ms = ms(h1, h2);
+        t->last_seen_ms = ms(h2, h3);
+        t->query_ms = ms(h3, h4);
+        t->wall_ms = ms(h0, h4);
+        t->spin_rc = c->spin_rc;
+        t->device_flags = c->device_flags;
+    }
+    static const bool dbg = getenv("BT_DEBUG_TIMING") != nullptr;
+    if (dbg)
+        fprintf(stderr, "[%s] enqueue %.3f ms, first-seen %.3f ms, last-seen %.3f ms, queries %.3f ms, "
+                "gpu span %.3f ms\n", who, ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, h4), tot);
+    return BT_OK;
+}
+
+static int ensure_timing_events(bt_ctx* c, uint32_t iters) {
     while (c->tev.size() < 2 * (size_t)iters) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
         c->tev.push_back(e);
     }
+    return BT_OK;
+}
+
+int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
+    if (!c || !b || !o || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = ensure_timing_events(c, iters)) return rc;
     // Default: plain launches with an event pair around every main kernel. BT_OPT_GRAPH:
     // the K steps replay as one hipGraph (no per-kernel events: HIP cannot time events
     // recorded inside a captured graph), main_ms is then reported as -1.
@@ -540,9 +604,7 @@ int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_
         c->tg_out = *o;
         c->tg_iters = iters;
     }
-    using clk = std::chrono::steady_clock;
-    auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-    const auto h0 = clk::now();
+    const auto h0 = std::chrono::steady_clock::now();
     if (use_graph) {
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(hipGraphLaunch(c->tgraph, c->stream));
@@ -555,56 +617,7 @@ int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_
         }
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
     }
-    const auto h1 = clk::now();
-    // Poll instead of hipEventSynchronize: a blocking wait is woken by an interrupt, whose
-    // latency would sit inside the caller's timed region.
-    auto poll = [](hipEvent_t e) -> hipError_t {
-        for (;;) {
-            const hipError_t q = hipEventQuery(e);
-            if (q != hipErrorNotReady) return q;
-        }
-    };
-    HIP_TRY(poll(c->ev0));
-    const auto h2 = clk::now();
-    HIP_TRY(poll(c->ev1));
-    const auto h3 = clk::now();
-    float tot = 0, k = 0, kmin = 1e30f, kmax = 0, lead = 0, gap = 0;
-    HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
-    for (uint32_t i = 0; !use_graph && i < iters; ++i) {
-        float x = 0;
-        HIP_TRY(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
-        k += x;
-        kmin = std::min(kmin, x);
-        kmax = std::max(kmax, x);
-        if (i + 1 < iters) {
-            float g = 0;
-            HIP_TRY(hipEventElapsedTime(&g, c->tev[2 * i + 1], c->tev[2 * i + 2]));
-            gap += g;
-        }
-    }
-    if (!use_graph) HIP_TRY(hipEventElapsedTime(&lead, c->ev0, c->tev[0]));
-    const auto h4 = clk::now();
-    if (t) {
-        *t = bt_timing{};
-        t->span_ms = tot;
-        t->main_ms = use_graph ? -1.0f : k / iters;
-        t->main_min_ms = use_graph ? -1.0f : kmin;
-        t->main_max_ms = use_graph ? -1.0f : kmax;
-        t->lead_ms = lead;
-        t->gap_ms = gap;
-        t->enqueue_ms = ms(h0, h1);
-        t->first_seen_ms = ms(h1, h2);
-        t->last_seen_ms = ms(h2, h3);
-        t->query_ms = ms(h3, h4);
-        t->wall_ms = ms(h0, h4);
-        t->spin_rc = c->spin_rc;
-        t->device_flags = c->device_flags;
-    }
-    static const bool dbg = getenv("BT_DEBUG_TIMING") != nullptr;
-    if (dbg)
-        fprintf(stderr, "[bt_time_device] enqueue %.3f ms, first-seen %.3f ms, last-seen %.3f ms, queries %.3f ms, "
-                "gpu span %.3f ms\n", ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, h4), tot);
-    return BT_OK;
+    return finish_timing(c, iters, use_graph, h0, t, "bt_time_device");
 }
 
 int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
@@ -883,7 +896,8 @@ int build_table(const bt_field_def* f, uint32_t n, ExTable* t, uint64_t* span_ou
     return BT_OK;
 }
 
-int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, const bt_extract_out* o, hipStream_t st) {
+int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, const bt_extract_out* o, hipStream_t st,
+                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     if (!b || !o) return fail(BT_E_INVALID_ARGUMENT, "null batch/outputs");
     if (b->n && !b->base) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer");
     if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
@@ -910,7 +924,7 @@ int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, cons
     a.values = o->values;
     a.image = o->image;
     a.n_cap = o->n_cap;
-    const int rc = launch_extract(a, t, st);
+    const int rc = launch_extract(a, t, st, e0, e1);
     if (rc) return fail(rc, "extract kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return BT_OK;
 }
@@ -936,6 +950,25 @@ int bt_extract_device(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, 
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     return run_extract(c, b, t, never, out, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
+}
+
+int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
+                       const bt_extract_out* out, uint32_t iters, bt_timing* t) {
+    if (!c || !b || !out || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
+    ExTable tab;
+    bool never = false;
+    int rc = build_table(fields, n_fields, &tab, nullptr, &never);
+    if (rc) return rc;
+    if (never || !b->n) return fail(BT_E_INVALID_ARGUMENT, "nothing to time: empty batch or a span no frame reaches");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = ensure_timing_events(c, iters))) return rc;
+    const auto h0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    for (uint32_t i = 0; i < iters; ++i)
+        if ((rc = run_extract(c, b, tab, never, out, c->stream, c->tev[2 * i], c->tev[2 * i + 1]))) return rc;
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    return finish_timing(c, iters, false, h0, t, "bt_time_extract");
 }
 
 int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,

@@ -18,6 +18,9 @@ BASELINE config, each with its own ms_per_step, Mpps, roofline and CPU baseline:
   c2  configs[1]: the same frames, parse-only
   c3  configs[2]: IMIX 64/512/1500 Eth/VLAN/IPv4/{TCP,UDP}, parse + filter + compaction
   c4  configs[3]: QinQ/IPv6/IHL+TCP options at 2-mod-4 offsets, parse + filter
+  c1  configs[0]'s protocol: parser_example's user table (ProtocolParser::parsePacket(frame,
+      ProtocolDefinition)) extracted on the GPU from the C2 frames, next to the
+      reference's own parsePacket on the host CPUs
 At N > 1 (C5, configs[4]) the entries are c3 (weak scaling: 16M IMIX packets per GPU)
 and c3_strong (one 16M IMIX batch split into tile-aligned, byte-balanced shards); the
 headline is weak scaling. Packet batches shard with no collective: the only cross-rank
@@ -71,8 +74,17 @@ WORKLOADS = {
                name="C4: 16M QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets, parse + PacketFilter "
                     "(BASELINE configs[3])"),
 }
+# configs[0]'s protocol: examples/parser_example.cpp:18-43's CUSTOM_PROTO (header u32 @0,
+# version u8 @4, length u16 @5, data BYTES[10] @7; all NETWORK byte order = 2), a user
+# table for ProtocolParser::parsePacket(frame, ProtocolDefinition)
+PARSER_EXAMPLE = [(0, 4, abi.FT_UINT32, 2), (4, 1, abi.FT_UINT8, 2), (5, 2, abi.FT_UINT16, 2), (7, 10, abi.FT_BYTES, 2)]
+WORKLOADS["c1"] = dict(cfg=synth.C2, fixed=True, parse=False, filters=None, extract=PARSER_EXAMPLE,
+                       name="C1's user protocol on the GPU: parser_example's CUSTOM_PROTO table (4 fields, span 17) "
+                            "extracted from 16M x 64B frames, fixed stride: status, extractValue<T> values, field "
+                            "bytes (ProtocolParser::parsePacket(frame, ProtocolDefinition), BASELINE configs[0])")
 # the kernels and their launch shapes (bt_runtime.cpp's cache-policy bits are A/B flags)
-KERNEL_SOURCES = ["beatrice_amd/csrc/bt_kernels.hip", "beatrice_amd/csrc/bt_device.h"]
+KERNEL_SOURCES = ["beatrice_amd/csrc/bt_kernels.hip", "beatrice_amd/csrc/bt_device.h",
+                  "beatrice_amd/csrc/bt_extract.hip"]
 
 
 def kernel_source_sha() -> str:
@@ -389,6 +401,86 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     return out, sample
 
 
+def measure_extract(name, wl, args, ctx, rank):
+    """The user-protocol extractor (bt_extract_tile) over a device-resident capture: one
+    step = one bt_extract_device pass over the batch (N=1 entry)."""
+    seed = synth.SEEDS[wl["cfg"]] + rank
+    cap = Capture(ctx, wl, args.packets, seed, 0, args.packets)
+    n, fields = cap.n, wl["extract"]
+    ex = abi.DeviceExtract(ctx, None, None, n, fields, batch=cap.run.batch)
+    for _ in range(args.warmup):
+        ex.run()
+    ex.time(args.steps)   # untimed: creates the per-launch event pairs
+    ok = int((ex.fetch()[0] == 0).sum())
+    for _ in range(2):
+        ex.run()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    tm = ex.time(args.steps)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    step_s = (t1 - t0) / args.steps
+    span, nf = ex.span, len(fields)
+    # algorithmic bytes: the [0, span) prefix read + status byte + one u64 per field + the
+    # span-byte image; the floor reads the 128-B lines of those prefixes
+    lens = synth.desc_len(cap.desc)
+    starts = synth.desc_off(cap.desc) if not wl["fixed"] else np.arange(n, dtype=np.int64) * cap.stride
+    rd = int(np.minimum(lens, span).sum())
+    lines, _ = unique_lines(starts, np.minimum(lens, span))
+    wr = n * (1 + 8 * nf + span)
+    algo = rd + wr
+    floor = lines * LINE + sum(-(-b // LINE) * LINE for b in (n, 8 * nf * n, span * n))
+    achieved = algo / (tm.main_ms * 1e-3) / 1e9
+    traffic_rec, traffic_src = load_traffic(args.traffic_json, name, n)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic_rec["traffic"] if traffic_rec else None, "traffic_source": traffic_src,
+            "traffic_bytes_per_packet": round(traffic_rec["traffic"] / n, 2) if traffic_rec else None,
+            "traffic_floor": floor, "traffic_floor_bytes_per_packet": round(floor / n, 2),
+            "kernel": "bt_extract_tile", "kernel_ms": round(tm.main_ms, 4),
+            "kernel_ms_min": round(tm.main_min_ms, 4), "kernel_ms_max": round(tm.main_max_ms, 4),
+            "algorithmic_bytes_per_packet": round(algo / n, 2), "kernel_mpps": round(n / (tm.main_ms * 1e-3) / 1e6, 1),
+            "gpu_span_ms_per_step": round(tm.span_ms / args.steps, 4)}
+    timing = tm.as_dict()
+    timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4),
+                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None})
+    out = {"workload": wl["name"], "value": round(n / step_s / 1e6, 2), "unit": "Mpps",
+           "ms_per_step": round(step_s * 1e3, 4), "scaling": "weak", "packets_per_gpu": n, "packets_total": n,
+           "parsed_fraction": round(ok / n, 4), "table": [list(f) for f in fields], "span": span,
+           "roofline": roof, "timing": timing,
+           "published": "parser_example: 25 us to parse its one 17-byte packet (README.md:1110; BASELINE.md §1)"}
+    sample = cap.cpu_sample(wl, seed, args.cpu_sample) if rank == 0 and not args.no_cpu else None
+    ex.free()
+    cap.run.free()
+    return out, sample
+
+
+def cpu_baseline_extract(sample, wl, seconds, cpus):
+    """The reference's ProtocolParser::parsePacket(frame, ProtocolDefinition) (oracle/_ref)
+    on the host CPUs over a bounded sample; the C restatement where _ref is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol  # checker/baseline only
+
+    data, sub = sample
+    threads = cpus["threads"]
+    if ol.ref_available():
+        done, el = ol.ref_bench_extract(data, sub, len(sub), wl["extract"], threads=threads, seconds=seconds)
+        kind = "reference"
+    else:
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < seconds:
+            ol.oracle_extract(data, sub, len(sub), wl["extract"])
+            done += len(sub)
+        el, kind, threads = time.perf_counter() - t0, "port", 1
+    return {"value": round(done / el / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": kind,
+            "cpu_model": cpus["model"], "affinity_cpus": cpus["affinity_cpus"],
+            "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
+            "sample": f"first {len(sub)} packets of the same capture, repeated for {el:.1f}s; "
+                      f"ProtocolParser::parsePacket(frame, CUSTOM_PROTO) with metrics off; {threads} "
+                      f"std::threads, per-thread parser instances, disjoint shards"}
+
+
 def cpu_baseline(sample, wl, seconds, cpus):
     """The reference's own parser + PacketFilter (oracle/_ref) on the host CPUs, on a
     bounded sample of the same capture; the C oracle port where _ref is absent."""
@@ -427,7 +519,7 @@ def main():
     ap.add_argument("--config", default="c2f", choices=sorted(WORKLOADS), help="the headline workload")
     ap.add_argument("--configs", default="auto",
                     help="comma list of extra workloads for the `configs` object (suffix _strong: strong "
-                         "scaling), 'none', or 'auto' (N=1: c2,c3,c4; N>1: c3,c3_strong)")
+                         "scaling), 'none', or 'auto' (N=1: c2,c3,c4,c1; N>1: c3,c3_strong)")
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 18)
@@ -467,7 +559,7 @@ def main():
         head.update(filters=[{"type": abi.PAYLOAD, "expr": args.payload, "priority": 9}] + head["filters"],
                     name=head["name"] + f" + PAYLOAD /{args.payload}/ first", payload=args.payload)
     if args.configs == "auto":
-        extra = ["c2", "c3", "c4"] if world == 1 else ["c3", "c3_strong"]
+        extra = ["c2", "c3", "c4", "c1"] if world == 1 else ["c3", "c3_strong"]
     elif args.configs == "none":
         extra = []
     else:
@@ -479,13 +571,18 @@ def main():
            [(c, c.replace("_strong", ""), dict(WORKLOADS[c.replace("_strong", "")]), c.endswith("_strong"))
             for c in extra]
     for key, name, wl, strong in jobs:
-        res, sample = measure(name, wl, args, ctx, flags, dist, rank, world, strong)
+        if wl.get("extract"):
+            res, sample = measure_extract(name, wl, args, ctx, rank)
+        else:
+            res, sample = measure(name, wl, args, ctx, flags, dist, rank, world, strong)
         results[key] = res
         samples[key] = (sample, wl)
     cpus = host_cpus()
     if rank == 0 and not args.no_cpu:
         for key, (sample, wl) in samples.items():
-            if sample is not None and not (key != "__head__" and results[key]["scaling"] == "strong"):
+            if sample is not None and wl.get("extract"):
+                results[key]["cpu_baseline"] = cpu_baseline_extract(sample, wl, args.cpu_seconds, cpus)
+            elif sample is not None and not (key != "__head__" and results[key]["scaling"] == "strong"):
                 results[key]["cpu_baseline"] = cpu_baseline(sample, wl, args.cpu_seconds, cpus)
             else:
                 results[key]["cpu_baseline"] = None
@@ -507,7 +604,7 @@ def main():
             "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64, streamed to HBM)",
             "config": {"workload": h["workload"], "packets_per_gpu": h["packets_per_gpu"],
                        "packets_total": h["packets_total"], "parallelism": f"batch split x{world}",
-                       "pass_fraction": h["pass_fraction"]},
+                       "pass_fraction": h.get("pass_fraction")},
             "roofline": h["roofline"],
             "cpu_baseline": h.get("cpu_baseline"),
             "timing": h["timing"],

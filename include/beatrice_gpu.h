@@ -25,7 +25,8 @@
  *   bt_extract_device / bt_extract
  *                       ProtocolParser::parsePacket(packet, ProtocolDefinition) and the
  *                       by-name form for registered user protocols
- *                       (src/parser/ProtocolParser.cpp:69-110, :238-433) over a batch.
+ *                       (src/parser/ProtocolParser.cpp:69-110, :238-433) over a batch;
+ *                       bt_time_extract_ex times it (bench.py's c1 entry).
  *
  * Record layout (bt_rec, 96 B per packet). Each layer L found by the layer walk
  * (DESIGN.md "R-WALK") has the field values that
@@ -527,6 +528,12 @@ int  bt_extract_device(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* f
 int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                 const bt_field_def* fields, uint32_t n_fields, uint8_t* status, uint64_t* values,
                 uint8_t* image);
+/* bt_extract_device `iters` times on the context's stream, each launch timed by an event
+ * pair from its own dispatch packet (bt_timing.main_* = the extraction kernel). For
+ * benchmarks; the outputs are those of the last launch. BT_E_INVALID_ARGUMENT for an empty
+ * batch or a table whose span no frame can reach (nothing would launch). */
+int  bt_time_extract_ex(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
+                        const bt_extract_out* out, uint32_t iters, bt_timing* timing);
 
 /* ---- text output --------------------------------------------------------------
  * The text the reference's ParseResult formatters print for every walked layer of

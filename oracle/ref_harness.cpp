@@ -446,4 +446,48 @@ uint64_t ref_bench(const uint8_t* base, const uint64_t* desc, uint32_t stride, u
     return total.load();
 }
 
+// CPU baseline of the user-protocol path: ProtocolParser::parsePacket(frame,
+// ProtocolDefinition) (src/parser/ProtocolParser.cpp:97-110) with metrics off, nthreads
+// std::threads with per-thread parser + definition on disjoint shards, repeated until
+// `seconds` of wall time pass. Returns packets parsed; *elapsed gets the wall seconds.
+uint64_t ref_bench_extract(const uint8_t* base, const uint64_t* desc, uint32_t stride, uint32_t n,
+                           const uint64_t* fields, uint32_t nf, int nthreads, double seconds, double* elapsed) {
+    std::atomic<uint64_t> total{0};
+    std::atomic<bool> stop{false};
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([&, t] {
+            ProtocolParser::ParserConfig cfg;
+            cfg.enablePerformanceMetrics = false;
+            ProtocolParser parser(cfg);
+            ProtocolDefinition def("USER", "1.0");
+            for (uint32_t k = 0; k < nf; ++k)
+                def.addField(FieldDefinition("f" + std::to_string(k), (size_t)fields[4 * k], (size_t)fields[4 * k + 1],
+                                             static_cast<FieldType>(fields[4 * k + 2]),
+                                             static_cast<Endianness>(fields[4 * k + 3])));
+            uint32_t lo = (uint32_t)((uint64_t)n * t / nthreads), hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+            uint64_t done = 0, sink = 0;
+            while (!stop.load(std::memory_order_relaxed)) {
+                for (uint32_t i = lo; i < hi; ++i) {
+                    uint32_t len;
+                    const uint8_t* f = frame_at(base, desc, stride, i, &len);
+                    const ParseResult r = parser.parsePacket(std::vector<uint8_t>(f, f + len), def);
+                    sink += r.fields.size();
+                    ++done;
+                    if ((done & 255) == 0) {
+                        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                        if (s >= seconds) stop = true;
+                        if (stop.load(std::memory_order_relaxed)) break;
+                    }
+                }
+            }
+            total += done + (sink == ~0ull);   // keep the results live
+        });
+    }
+    for (auto& x : th) x.join();
+    *elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return total.load();
+}
+
 }  // extern "C"

@@ -88,6 +88,10 @@ def ref():
         L.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+        L.ref_bench_extract.restype = ctypes.c_uint64
+        L.ref_bench_extract.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
+                                        ctypes.POINTER(ctypes.c_double)]
         L.ref_format.restype = ctypes.c_uint64
         L.ref_format.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
@@ -139,6 +143,16 @@ def ref_bench(data, desc, n, filters, parse=True, threads=8, seconds=10.0, strid
     el = ctypes.c_double(0)
     done = ref().ref_bench(_ptr(data), _ptr(desc), stride, n, f, len(filters), int(parse), threads,
                            seconds, ctypes.byref(el))
+    return int(done), el.value
+
+
+def ref_bench_extract(data, desc, n, fields, threads=8, seconds=5.0, stride=0):
+    """CPU baseline: the compiled reference's parsePacket(frame, ProtocolDefinition) on
+    `threads` threads for `seconds`. Returns (packets, elapsed seconds)."""
+    t = table_array(fields)
+    el = ctypes.c_double(0)
+    done = ref().ref_bench_extract(_ptr(data), _ptr(desc), stride, n, t.ctypes.data, len(t), threads, seconds,
+                                   ctypes.byref(el))
     return int(done), el.value
 
 

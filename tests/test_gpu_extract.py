@@ -115,3 +115,41 @@ def test_edges(gpu_ctx):
         run(gpu_ctx, data, desc, 1000, [(0, 0, abi.FT_BOOLEAN, 0)])
     with pytest.raises(abi.BtError):
         run(gpu_ctx, data, desc, 1000, [(0, 1, abi.FT_UINT8, 0)] * 65)
+
+
+def test_timed_extraction_matches_reference(gpu_ctx):
+    """bt_time_extract_ex (bench.py's c1 entry): K timed launches leave the reference's
+    outputs, and every launch has a positive, consistent event-pair duration."""
+    name = "parser_example"
+    r = abi.DeviceExtract(gpu_ctx, G["data"], G["desc"], MAN["n"], MAN["tables"][name])
+    try:
+        t = r.time(5)
+        assert t.main_ms > 0 and 0 < t.main_min_ms <= t.main_ms <= t.main_max_ms <= t.span_ms
+        check_against_golden(name, *r.fetch())
+    finally:
+        r.free()
+    empty = abi.DeviceExtract(gpu_ctx, G["data"], G["desc"], 0, MAN["tables"][name])
+    try:
+        with pytest.raises(abi.BtError):
+            empty.time(2)
+    finally:
+        empty.free()
+
+
+def test_extract_over_a_parse_batch(gpu_ctx):
+    """DeviceExtract over packets already on the device (a DeviceRun's batch, as the bench
+    uses it): same results as the oracle, and the DeviceRun keeps its buffer."""
+    n = 5000
+    data, desc = synth.capture(synth.C2, n)
+    fields = MAN["tables"]["parser_example"]
+    run_ = abi.DeviceRun(gpu_ctx, data, None, n, stride=64, records=False, decide=False, verdict=False,
+                         pass_idx=False)
+    try:
+        ex = abi.DeviceExtract(gpu_ctx, None, None, n, fields, batch=run_.batch)
+        ex.run()
+        st, val, img = ex.fetch()
+        ex.free()
+        est, evl, eimg, _ = ol.oracle_extract(data, None, n, fields, stride=64)
+        assert np.array_equal(st, est) and np.array_equal(val, evl) and np.array_equal(img, eimg)
+    finally:
+        run_.free()
