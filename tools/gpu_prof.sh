@@ -1,7 +1,7 @@
 # Profiles of the current kernels: rocprofv3 kernel stats + separate FETCH/WRITE PMC passes,
 # one bench workload at a time (--configs none). Usage: bash tools/gpu_prof.sh [OUTDIR] [configs...]
 OUT=${1:-gpurun_out/prof}; shift
-CFGS=${*:-c2f c2 c3 c4}
+CFGS=${*:-c2f c2 c3 c4 c1}
 mkdir -p $OUT
 export TMPDIR=/tmp
 for cfg in $CFGS; do
@@ -10,5 +10,5 @@ for cfg in $CFGS; do
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_${cfg}_write -o run -- python3 bench.py --config $cfg --configs none --steps 3 --warmup 1 --no-cpu > /dev/null 2>&1 || exit 4
   python3 tools/pmc_traffic.py --fetch $OUT/pmc_${cfg}_fetch --write $OUT/pmc_${cfg}_write --config $cfg --out $OUT/traffic.json | cut -c1-200
   cp $OUT/stats_$cfg/run_kernel_stats.csv $OUT/${cfg}_kernel_stats.csv
-  grep -E "parse_filter_(main|pipe)" $OUT/${cfg}_kernel_stats.csv | cut -d, -f2-5
+  grep -E "parse_filter_(main|pipe)|extract_tile" $OUT/${cfg}_kernel_stats.csv | cut -d, -f2-5
 done

@@ -9,7 +9,7 @@ c = sys.argv[1]
 per = {}
 for f in glob.glob(f"gpurun_out/sq_{c}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "parse_filter_" in r.get("Kernel_Name", ""):
+        if "parse_filter_" in r.get("Kernel_Name", "") or "extract_tile" in r.get("Kernel_Name", ""):
             per.setdefault(r["Dispatch_Id"], {}).setdefault(r["Counter_Name"], 0.0)
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
 d = per[sorted(per, key=int)[-1]]

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of the main kernel (bt_parse_filter_main / _pipe) from rocprofv3 PMC passes.
+"""Per-launch HBM traffic of the main kernel (bt_parse_filter_main / _pipe; bt_extract_tile for c1) from
+rocprofv3 PMC passes.
 
     python tools/pmc_traffic.py --fetch DIR_FETCH --write DIR_WRITE --config c2 \
         [--out profiles/traffic.json]
@@ -25,6 +26,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402  (kernel_source_sha: the key bench.py checks the figure against)
 
 KERNEL = "bt_parse_filter_"   # bt_parse_filter_main (fixed stride) or bt_parse_filter_pipe (descriptors)
+KERNEL_OF = {"c1": "bt_extract_tile"}   # bench.py's user-protocol entry
 
 
 def per_dispatch(d, counter):
@@ -56,6 +58,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                    "profiles", "traffic.json"))
     a = ap.parse_args()
+    global KERNEL
+    KERNEL = KERNEL_OF.get(a.config, KERNEL)
     fetch_kib, nf = per_dispatch(a.fetch, "FETCH_SIZE")
     write_kib, nw = per_dispatch(a.write, "WRITE_SIZE")
     fetch_b = fetch_kib * 1024.0
