@@ -441,6 +441,9 @@ def measure_extract(name, wl, args, ctx, rank):
             "kernel_ms_min": round(tm.main_min_ms, 4), "kernel_ms_max": round(tm.main_max_ms, 4),
             "algorithmic_bytes_per_packet": round(algo / n, 2), "kernel_mpps": round(n / (tm.main_ms * 1e-3) / 1e6, 1),
             "gpu_span_ms_per_step": round(tm.span_ms / args.steps, 4)}
+    if traffic_rec:
+        roof["traffic_read_per_packet"] = traffic_rec.get("read_per_packet")
+        roof["traffic_write_per_packet"] = traffic_rec.get("write_per_packet")
     timing = tm.as_dict()
     timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4),
                    "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None})

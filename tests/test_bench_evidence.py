@@ -110,7 +110,7 @@ def test_committed_bench_line_is_consistent(cfg):
 def test_rocprof_stats_agree_with_bench_events(cfg):
     under = _line(os.path.join(PROFILES, f"{cfg}_bench_under_rocprof.json"))
     with open(os.path.join(PROFILES, f"{cfg}_kernel_stats.csv")) as fh:
-        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"]]
+        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"] or "extract_tile" in x["Name"]]
     assert len(rows) == 1, [x["Name"] for x in rows]
     assert under["roofline"]["kernel"] in rows[0]["Name"]
     avg_ms = float(rows[0]["AverageNs"]) / 1e6
@@ -143,10 +143,13 @@ def test_r02_default_line_covers_every_config():
     assert d["n_gpus"] == 1 and "parse + PacketFilter" in d["config"]["workload"] and "64B" in d["config"]["workload"]
     _check_entry(d)
     assert d["cpu_baseline"]["kind"] == "reference" and d["cpu_baseline"]["cores"] >= 1
-    assert set(d["configs"]) == {"c2", "c3", "c4"}
+    assert set(d["configs"]) == {"c2", "c3", "c4", "c1"}
     for k, e in d["configs"].items():
         _check_entry(e)
         assert e["cpu_baseline"] and e["cpu_baseline"]["value"] > 0, k
+    c1 = d["configs"]["c1"]   # the user-protocol extractor on parser_example's table
+    assert c1["roofline"]["kernel"] == "bt_extract_tile" and c1["parsed_fraction"] == 1.0
+    assert c1["span"] == 17 and c1["cpu_baseline"]["kind"] == "reference"
     assert d["value"] == pytest.approx(d["config"]["packets_total"] / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
 
 
@@ -159,11 +162,11 @@ def test_r02_two_rank_line_has_per_rank_entries():
     assert sum(r["packets"] for r in s["per_rank"]) == s["packets_total"] == 1 << 24
 
 
-@pytest.mark.parametrize("cfg", ["c2f", "c2", "c3", "c4"])
+@pytest.mark.parametrize("cfg", ["c2f", "c2", "c3", "c4", "c1"])
 def test_r02_rocprof_stats_agree_with_bench_events(cfg):
     under = _line(os.path.join(R02, "prof", f"{cfg}_bench_under_rocprof.json"))
     with open(os.path.join(R02, "prof", f"{cfg}_kernel_stats.csv")) as fh:
-        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"]]
+        rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"] or "extract_tile" in x["Name"]]
     assert len(rows) == 1
     assert under["roofline"]["kernel"] in rows[0]["Name"]
     assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(under["roofline"]["kernel_ms"], rel=0.05)
