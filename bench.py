@@ -587,6 +587,13 @@ def main():
                 results[key]["cpu_baseline"] = cpu_baseline_extract(sample, wl, args.cpu_seconds, cpus)
             elif sample is not None and not (key != "__head__" and results[key]["scaling"] == "strong"):
                 results[key]["cpu_baseline"] = cpu_baseline(sample, wl, args.cpu_seconds, cpus)
+                if key == "__head__" and cpus["affinity_cpus"] > cpus["threads"]:
+                    # the same on one thread per affinity CPU, past the cgroup quota: shows
+                    # whether the quota, not the thread count, bounds the reference
+                    wide = cpu_baseline(sample, wl, max(1.0, args.cpu_seconds / 2),
+                                        dict(cpus, threads=cpus["affinity_cpus"]))
+                    results[key]["cpu_baseline"]["all_affinity_threads"] = {
+                        "threads": wide["cores"], "value": wide["value"], "unit": wide["unit"]}
             else:
                 results[key]["cpu_baseline"] = None
 
