@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the multi-GPU batch split (beatrice_amd/shard.py).
+"""CPU, world_size 2 and 4 over gloo: the multi-GPU batch split (beatrice_amd/shard.py).
 Each rank takes its tile-aligned, byte-balanced shard with rebased descriptors (what
 one GPU would receive), computes it with the oracle standing in for the device, and
 the host-side merge must equal the whole-batch result. No data-path collective:
@@ -50,19 +50,20 @@ def _rank_main(rank, world, port, cfg, n, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,n", [(synth.C3, 30000), (synth.C4, 10001)])
-def test_two_rank_split_matches_whole_batch(cfg, n):
+@pytest.mark.parametrize("cfg,n,world", [(synth.C3, 30000, 2), (synth.C4, 10001, 2), (synth.C3, 20037, 4)])
+def test_rank_split_matches_whole_batch(cfg, n, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, cfg, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cfg, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     ok, bounds = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
     assert ok, bounds
-    assert bounds[0][0] == 0 and bounds[-1][1] == n and bounds[0][1] % 64 == 0
+    assert bounds[0][0] == 0 and bounds[-1][1] == n and all(lo % 64 == 0 for lo, _ in bounds)
+    assert all(bounds[i][1] == bounds[i + 1][0] for i in range(world - 1))
 
 
 def test_bounds_balance_bytes():
