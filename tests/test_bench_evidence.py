@@ -162,6 +162,15 @@ def test_r02_two_rank_line_has_per_rank_entries():
     assert sum(r["packets"] for r in s["per_rank"]) == s["packets_total"] == 1 << 24
 
 
+def test_r02_four_rank_line_splits_the_strong_batch():
+    d = _line(os.path.join(R02, "bench_4rank_one_gpu.json"))
+    assert d["n_gpus"] == 4 and len(d["per_rank"]) == 4 and d["scaling"] == "weak"
+    s = d["configs"]["c3_strong"]
+    parts = [r["packets"] for r in s["per_rank"]]
+    assert sum(parts) == s["packets_total"] == 1 << 24 and all(p % 64 == 0 for p in parts[:-1])
+    assert max(parts) - min(parts) < 1 << 12   # byte-balanced shards of near-equal size here
+
+
 @pytest.mark.parametrize("cfg", ["c2f", "c2", "c3", "c4", "c1"])
 def test_r02_rocprof_stats_agree_with_bench_events(cfg):
     under = _line(os.path.join(R02, "prof", f"{cfg}_bench_under_rocprof.json"))
