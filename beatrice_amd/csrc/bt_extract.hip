@@ -262,6 +262,11 @@ int launch_extract(const ExArgs& a, const ExTable& tab_in, void* stream, void* t
         }
         per_cu = it->second;
     }
+    // At most 5 blocks (20 waves) per CU: with parser_example's table the residency is 8,
+    // and fewer concurrent read/write streams suit HBM better (c1, 16M packets: 0.432 ms
+    // at 8 blocks/CU, 0.383-0.393 at 4, 0.383-0.385 at 5, 0.387-0.389 at 6, 0.425-0.437
+    // at 3, 0.529-0.541 at 2; alternating processes, profiles/r02/ab/c1_grid.txt).
+    per_cu = std::min(per_cu, 5);
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)(cus * per_cu));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

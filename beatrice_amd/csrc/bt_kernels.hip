@@ -1179,14 +1179,15 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
     const uint32_t dyn = F == 2 ? (a.dfa_bytes + 15u) & ~15u : 0u;
     auto go = [&](auto kernel, int resident) {
         int g = grid > 0 ? grid : resident;
-        // Fixed stride: two blocks (8 waves) per CU parse-only, four with a filter. C2
+        // Fixed stride: two blocks (8 waves) per CU parse-only, three with a filter. C2
         // measured 0.416 ms at the residency (7 blocks/CU), 0.403 at 3, 0.387 at 2, 0.56
         // at 1 (4 processes each): fewer concurrent read and write streams suit HBM
-        // better. With the filter (its decision / verdict stores and the slot loop per
-        // tile) the 64-B parse+filter headline measured 0.462 ms at 2 blocks/CU, 0.391 at
-        // 3, 0.379 at 4, 0.44 at 5, 0.40 at 6, 0.375 at 7 (2 passes each): 4 keeps every
-        // wave on exactly 64 tiles of a 16M batch.
-        if (FL >= 0 && grid <= 0) g = std::min(g, (F ? 4 : 2) * cu_count());
+        // better; with the final kernels 0.338-0.341 at 2 against 0.353-0.356 at 3. With
+        // the filter (its decision / verdict stores and the slot loop per tile) the 64-B
+        // parse+filter headline needs more waves: 0.366-0.368 ms at 3 blocks/CU against
+        // 0.378-0.379 at 4 and 0.420-0.426 at 2 (round 2, alternating processes, 3
+        // passes each; round 1's code was best at 4).
+        if (FL >= 0 && grid <= 0) g = std::min(g, (F ? 3 : 2) * cu_count());
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
         if (e0 || e1)
             hipExtLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, e0, e1, 0, a, prog);
