@@ -419,3 +419,22 @@ def test_fixed_stride_headline_kernel_on_reference_fixture(fset):
         assert np.array_equal(out["records"], g["rec"])
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("cfg", [synth.FUZZ, synth.C3])
+def test_random_programs_match_oracle(gpu_ctx, cfg):
+    """40 seeded random programs over the built-in kinds (tests/random_programs.py: the
+    reference's expression quirks, throwing expressions, disabled filters): decision
+    bytes, verdict words and pass lists equal the oracle's, which
+    tests/test_random_programs.py pins against the compiled reference."""
+    from random_programs import random_programs
+    n = 20037
+    data, desc = synth.capture(cfg, n, seed=0x5B + cfg)
+    for i, prog in enumerate(random_programs(0xF117E3 + cfg, 40)):
+        gpu_ctx.compile(prog)
+        out = run_dev(gpu_ctx, data, desc, n, records=False)
+        _, dec, npass = ol.oracle_run(data, desc, n, prog, parse=False)
+        bad = np.nonzero(out["decide"] != dec)[0]
+        assert len(bad) == 0, f"program {i} {prog}: {len(bad)} decisions differ, first {bad[:5]}"
+        assert out["n_pass"] == npass, f"program {i}"
+        check_filter_outputs(out, n)
