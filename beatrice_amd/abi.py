@@ -72,6 +72,9 @@ OPT_SPIN_SYNC = 0x100
 OPT_PAYLOAD_HOST = 0x200
 OPT_WIDE_NEVER = 0x400
 OPT_WIDE_ALWAYS = 0x800
+OPT_PIPELINE = 0x2000
+TIME_KERNEL_EVENTS = 0x1
+TIME_PIPELINED = 0x2
 
 
 DESC_PACKED, DESC_XDP = 0, 1
@@ -140,8 +143,9 @@ class Tpv3Ring(ctypes.Structure):
 EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
+    "bt_parse_filter_device_async",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_record_gather", "bt_record_gather_planes",
+    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
@@ -172,6 +176,8 @@ def lib() -> ctypes.CDLL:
                                                   u32, ctypes.POINTER(u32)]),
         "bt_reserve": (ctypes.c_int, [vp, u32]),
         "bt_parse_filter_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), vp]),
+        "bt_parse_filter_device_async": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), vp,
+                                                        vp]),
         "bt_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_host_register": (ctypes.c_int, [vp, vp, u64, ctypes.POINTER(vp)]),
@@ -186,11 +192,14 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "bt_time_device_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
                                              ctypes.POINTER(Timing)]),
+        "bt_time_device2": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, u32, u32, ctypes.POINTER(Timing)]),
         "bt_proto_span": (ctypes.c_int, [vp, u32, ctypes.POINTER(u64)]),
         "bt_extract_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), vp]),
         "bt_extract": (ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, vp]),
         "bt_time_extract_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), u32,
                                               ctypes.POINTER(Timing)]),
+        "bt_time_extract2": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), u32, u32,
+                                            ctypes.POINTER(Timing)]),
         "bt_record_gather": (None, [vp, u32, u32, vp]),
         "bt_record_gather_planes": (None, [vp, u32, u32, vp]),
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
@@ -361,6 +370,12 @@ class Context:
     def run_device(self, batch: Batch, outs: Outputs, stream=None):
         _check(lib().bt_parse_filter_device(self.h, ctypes.byref(batch), ctypes.byref(outs), stream))
 
+    def run_device_async(self, batch: Batch, outs: Outputs, stream=None, done_event=None):
+        """bt_parse_filter_device_async: the compaction on the context's compaction stream;
+        synchronize() (or done_event, a hipEvent_t) before reading pass_idx / n_pass."""
+        _check(lib().bt_parse_filter_device_async(self.h, ctypes.byref(batch), ctypes.byref(outs), stream,
+                                                  done_event))
+
     def time_device(self, batch: Batch, outs: Outputs, iters: int):
         a, b = ctypes.c_float(0), ctypes.c_float(0)
         _check(lib().bt_time_device(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(a),
@@ -370,6 +385,14 @@ class Context:
     def time_device_ex(self, batch: Batch, outs: Outputs, iters: int) -> Timing:
         t = Timing()
         _check(lib().bt_time_device_ex(self.h, ctypes.byref(batch), ctypes.byref(outs), iters, ctypes.byref(t)))
+        return t
+
+    def time_device2(self, batch: Batch, outs, iters: int, mode: int) -> Timing:
+        """bt_time_device2: outs = a list of Outputs (step i writes outs[i % len(outs)])."""
+        arr = (Outputs * len(outs))(*outs)
+        t = Timing()
+        _check(lib().bt_time_device2(self.h, ctypes.byref(batch), ctypes.cast(arr, ctypes.c_void_p), len(outs), iters,
+                                     mode, ctypes.byref(t)))
         return t
 
     def extract_host(self, frames, fields):
@@ -593,6 +616,7 @@ class DeviceRun:
                             self.d_pidx.ptr if self.d_pidx else None,
                             self.d_npass.ptr if self.d_npass else None)
         ctx.reserve(n)
+        self.alt, self.alt_outs = None, None
 
     def upload_data(self, buf: np.ndarray, offset: int):
         """Bytes of the packet buffer from `offset` on (a capture streamed range by range)."""
@@ -640,8 +664,19 @@ class DeviceRun:
         self.ctx.synchronize()
         return int(self.d_npass.download(np.zeros(1, dtype=np.uint32))[0]) if self.d_npass else 0
 
+    def second_outputs(self) -> Outputs:
+        """A second output set of the same shape (records, decide, verdict, pass_idx,
+        n_pass as this run has them), for pipelined steps that alternate two sets."""
+        if self.alt is None:
+            self.alt = [self.ctx.alloc(b.nbytes) if b is not None else None
+                        for b in (self.d_rec, self.d_ver, self.d_dec, self.d_pidx, self.d_npass)]
+            r, v, d, p, c = (b.ptr if b is not None else None for b in self.alt)
+            self.alt_outs = Outputs(r, self.n, v, d, p, c)
+        return self.alt_outs
+
     def free(self):
-        for b in (self.d_data, self.d_desc, self.d_rec, self.d_dec, self.d_ver, self.d_pidx, self.d_npass):
+        for b in (self.d_data, self.d_desc, self.d_rec, self.d_dec, self.d_ver, self.d_pidx, self.d_npass,
+                  *(self.alt or [])):
             if b is not None:
                 b.free()
 
@@ -680,11 +715,12 @@ class DeviceExtract:
         _check(lib().bt_extract_device(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
                                        ctypes.byref(self.out), stream))
 
-    def time(self, iters: int) -> Timing:
-        """bt_time_extract_ex: `iters` launches, each timed from its own dispatch."""
+    def time(self, iters: int, mode: int = TIME_KERNEL_EVENTS) -> Timing:
+        """bt_time_extract2: `iters` launches; with TIME_KERNEL_EVENTS each is timed from
+        its own dispatch (main_ms), without them only the span is."""
         t = Timing()
-        _check(lib().bt_time_extract_ex(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
-                                        ctypes.byref(self.out), iters, ctypes.byref(t)))
+        _check(lib().bt_time_extract2(self.ctx.h, ctypes.byref(self.batch), self.table, self.nf,
+                                      ctypes.byref(self.out), iters, mode, ctypes.byref(t)))
         return t
 
     def fetch(self):

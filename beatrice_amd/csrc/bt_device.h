@@ -44,8 +44,7 @@ struct MainArgs {
     uint32_t n_cap;            // record plane stride (records)
     uint8_t* records;          // plane-major (or AoS when the AOS variant is launched)
     uint8_t* decide;
-    uint64_t* verdict;
-    uint32_t* tile_pass;       // per-tile pass counts (compaction input)
+    uint64_t* verdict;         // per-tile pass words (also the compaction's input)
     uint32_t blocked;          // tile order: 0 cyclic, 1 one contiguous range per wavefront
     uint32_t nt;               // bit0 non-temporal record stores, bit1 non-temporal header loads,
                                // bit2 / bit3 force two-round / wide loads (A/B)
@@ -71,8 +70,10 @@ enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2, kRecTiled = 3 };
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
                 int grid_blocks, bool prefetch, void* stream, void* timing_start = nullptr,
                 void* timing_stop = nullptr);
-int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
-                   uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream);
+// The ordered compaction: pass_idx = the indices of the set verdict bits, ascending;
+// n_pass = their count. chunk_sums: ceil(ntiles / kChunkTiles) words of workspace.
+int launch_compact(const uint64_t* verdict, uint32_t ntiles, uint32_t* chunk_sums, uint32_t* pass_idx,
+                   uint32_t* n_pass, void* stream);
 int device_grid_blocks(int device);
 
 // ---- user-defined protocol extraction (bt_extract.hip) ----

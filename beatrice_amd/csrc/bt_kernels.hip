@@ -776,10 +776,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             const uint32_t code = filter_packet<FILTER>(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
-            if (lane == 0) {
-                if (a.verdict) a.verdict[t] = pass;
-                if (a.tile_pass) a.tile_pass[t] = (uint32_t)__popcll(pass);
-            }
+            if (lane == 0 && a.verdict) a.verdict[t] = pass;   // also the compaction's input
         }
         // ---- 4. AoS records: the tile's 64 bt_rec are one contiguous 6-KiB range. Each
         // lane's 96 B are written to the wave's LDS image (the row is free once the filter
@@ -1031,8 +1028,6 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
             __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
-            const auto rt = rsrc_of(a.tile_pass ? a.tile_pass + t : nullptr, a.tile_pass ? 4u : 0u);
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)__popcll(pass), rt, lane == 0 ? 0 : (int)kOob, 0, 0);
         }
 
         wave_lds_sync();   // this tile's LDS reads are done
@@ -1044,14 +1039,14 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
 }
 
 // ---- ordered compaction of passing packet indices ---------------------------------
-// K2: chunk_sums[c] = sum of tile_pass over chunk c (kChunkTiles = 256 tiles, one per
-// thread).
-__global__ __launch_bounds__(256) void bt_chunk_sums(const uint32_t* tile_pass, uint32_t ntiles,
+// K2: chunk_sums[c] = the passing packets of chunk c (kChunkTiles = 256 tiles, one per
+// thread): the popcounts of the tiles' verdict words.
+__global__ __launch_bounds__(256) void bt_chunk_sums(const uint64_t* verdict, uint32_t ntiles,
                                                      uint32_t* chunk_sums) {
     static_assert(kChunkTiles == 256, "one tile per thread");
     __shared__ uint32_t red[4];
     const uint32_t t = blockIdx.x * kChunkTiles + threadIdx.x;
-    uint32_t s = t < ntiles ? tile_pass[t] : 0u;
+    uint32_t s = t < ntiles ? (uint32_t)__popcll(verdict[t]) : 0u;
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
@@ -1066,9 +1061,9 @@ __global__ __launch_bounds__(256) void bt_chunk_sums(const uint32_t* tile_pass, 
 // tiles per step keep the LDS reads of the next tiles in flight behind the stores.
 // (The first version had 1024-tile chunks, i.e. 256 blocks = one per CU, and a
 // strided one-tile loop: 34 us on C3.)
-__global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const uint32_t* tile_pass,
-                                                  const uint32_t* chunk_sums, uint32_t nchunks,
-                                                  uint32_t ntiles, uint32_t* pass_idx, uint32_t* n_pass) {
+__global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const uint32_t* chunk_sums,
+                                                  uint32_t nchunks, uint32_t ntiles, uint32_t* pass_idx,
+                                                  uint32_t* n_pass) {
     __shared__ uint32_t tile_off[kChunkTiles];
     __shared__ uint64_t words[kChunkTiles];
     __shared__ uint32_t red[4];
@@ -1076,8 +1071,7 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
     const uint32_t c = blockIdx.x;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t t = c * kChunkTiles + tid;
-    const uint32_t v = t < ntiles ? tile_pass[t] : 0u;   // issued before the prefix loop
-    const uint64_t word = t < ntiles ? verdict[t] : 0ull;
+    const uint64_t word = t < ntiles ? verdict[t] : 0ull;   // issued before the prefix loop
 
     // prefix of earlier chunks (and the grand total for n_pass)
     uint32_t pre = 0, tot = 0;
@@ -1094,6 +1088,7 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
     if (!pass_idx) return;   // count only
     __syncthreads();
 
+    const uint32_t v = (uint32_t)__popcll(word);   // the tile's passing packets
     uint32_t incl = v;   // inclusive wave scan of the tile counts
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
@@ -1257,15 +1252,14 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }
 
-int launch_compact(const uint64_t* verdict, const uint32_t* tile_pass, uint32_t ntiles, uint32_t n,
-                   uint32_t* chunk_sums, uint32_t* pass_idx, uint32_t* n_pass, void* stream) {
-    (void)n;
+int launch_compact(const uint64_t* verdict, uint32_t ntiles, uint32_t* chunk_sums, uint32_t* pass_idx,
+                   uint32_t* n_pass, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     if (nchunks == 0) return BT_OK;
-    hipLaunchKernelGGL(bt_chunk_sums, dim3(nchunks), dim3(256), 0, st, tile_pass, ntiles, chunk_sums);
-    hipLaunchKernelGGL(bt_compact, dim3(nchunks), dim3(256), 0, st, verdict, tile_pass, chunk_sums, nchunks,
-                       ntiles, pass_idx, n_pass);
+    hipLaunchKernelGGL(bt_chunk_sums, dim3(nchunks), dim3(256), 0, st, verdict, ntiles, chunk_sums);
+    hipLaunchKernelGGL(bt_compact, dim3(nchunks), dim3(256), 0, st, verdict, chunk_sums, nchunks, ntiles, pass_idx,
+                       n_pass);
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }
 

@@ -143,11 +143,21 @@ struct bt_ctx {
     bool dfa_used[2] = {false, false};
     int dfa_cur = 0;
 
-    // device workspace for bt_parse_filter_device
+    // device workspace of the compaction: chunk sums, and the verdict words when the
+    // caller asks for none. Double-buffered (consecutive calls alternate). `stream` = the
+    // last stream that queued work touching the buffer; before another stream touches
+    // it, an event recorded at that stream's tail makes the new one wait (stream
+    // switches only: calls that stay on their streams queue no extra packets).
     uint32_t ws_cap = 0;
-    uint32_t* tile_pass = nullptr;
-    uint32_t* chunk_sums = nullptr;
-    uint64_t* verdict = nullptr;
+    struct Ws {
+        uint32_t* chunk_sums = nullptr;
+        uint64_t* verdict = nullptr;
+        hipStream_t stream = nullptr;
+        hipEvent_t sync = nullptr;
+    } ws[2];
+    int ws_next = 0;
+    hipEvent_t main_done[2] = {nullptr, nullptr};   // pipelined: main kernel -> compaction stream
+    hipStream_t cstream = nullptr;     // pipelined compaction (bt_parse_filter_device_async)
 
     // host pipeline
     uint32_t chunk = 0;
@@ -158,6 +168,7 @@ struct bt_ctx {
 
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t pipe_done = nullptr;    // BT_OPT_PIPELINE: the last step's compaction
     std::vector<hipEvent_t> tev;
     // bt_time_device: K steps captured once into one hipGraph, replayed per call
     hipGraphExec_t tgraph = nullptr;
@@ -208,27 +219,64 @@ void host_parallel(bt_ctx* ctx, const std::function<void(unsigned, unsigned)>& f
 
 namespace {
 
+void free_ws(bt_ctx* c) {
+    for (auto& w : c->ws) {
+        if (w.chunk_sums) (void)hipFree(w.chunk_sums);
+        if (w.verdict) (void)hipFree(w.verdict);
+        w.chunk_sums = nullptr; w.verdict = nullptr; w.stream = nullptr;
+    }
+    c->ws_cap = 0;
+}
+
 int ensure_ws(bt_ctx* c, uint32_t n) {
-    if (n <= c->ws_cap) return BT_OK;
+    if (n <= c->ws_cap && c->ws[0].chunk_sums) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
     // a cached BT_OPT_GRAPH timing graph holds the pointers replaced here
     if (c->tgraph) { (void)hipGraphExecDestroy(c->tgraph); c->tgraph = nullptr; }
-    if (c->tile_pass) {   // launches queued on any stream may still use the old workspace
-        HIP_TRY(hipDeviceSynchronize());
-        (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict);
-    }
-    c->tile_pass = nullptr; c->chunk_sums = nullptr; c->verdict = nullptr; c->ws_cap = 0;
-    const uint32_t ntiles = (n + 63) / 64;
+    if (c->ws[0].chunk_sums) HIP_TRY(hipDeviceSynchronize());   // launches on any stream may use it
+    free_ws(c);
+    const uint32_t ntiles = (std::max(n, 1u) + 63) / 64;
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
-    HIP_TRY(hipMalloc(&c->tile_pass, (size_t)ntiles * 4));
-    HIP_TRY(hipMalloc(&c->chunk_sums, (size_t)std::max<uint32_t>(nchunks, 1) * 4));
-    HIP_TRY(hipMalloc(&c->verdict, (size_t)ntiles * 8));
-    c->ws_cap = ntiles * 64 < n ? n : ntiles * 64;
+    for (auto& w : c->ws) {
+        if (!w.sync) HIP_TRY(hipEventCreateWithFlags(&w.sync, hipEventDisableTiming));
+        HIP_TRY(hipMalloc(&w.chunk_sums, (size_t)nchunks * 4));
+        HIP_TRY(hipMalloc(&w.verdict, (size_t)ntiles * 8));
+    }
+    for (auto& e : c->main_done)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ws_cap = ntiles * 64;
     return BT_OK;
 }
 
+// `s` is about to queue work that touches workspace buffer w: if another stream did last,
+// s waits for everything that stream has queued so far.
+int ws_touch(bt_ctx::Ws* w, hipStream_t s) {
+    if (w->stream && w->stream != s) {
+        if (hipEventRecord(w->sync, w->stream) == hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(s, w->sync, 0));
+        } else {   // that stream is gone (destroyed by its owner): wait for the whole device
+            (void)hipGetLastError();
+            HIP_TRY(hipDeviceSynchronize());
+        }
+    }
+    w->stream = s;
+    return BT_OK;
+}
+
+int ensure_cstream(bt_ctx* c) {
+    if (c->cstream) return BT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    return BT_OK;
+}
+
+// One parse+filter(+compaction) pass on `st`. `cst` = the stream of the compaction
+// kernels: st itself, or (pipelined, bt_parse_filter_device_async) the context's
+// compaction stream, which waits for this call's main kernel only, so the next call's
+// main kernel on st runs beside this call's compaction; `done` (may be null) is
+// recorded after the compaction on cst.
 int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st, bool aos,
-               hipEvent_t e0, hipEvent_t e1) {
+               hipEvent_t e0, hipEvent_t e1, hipStream_t cst = nullptr, hipEvent_t done = nullptr) {
     if (!b || !o) return fail(BT_E_INVALID_ARGUMENT, "null batch/outputs");
     if (b->n && !b->base) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer");
     if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
@@ -236,13 +284,20 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     const bool filter = o->verdict || o->decide || o->pass_idx || o->n_pass;
     const bool compact = o->pass_idx || o->n_pass;
     if (!filter && !o->records) return BT_OK;
+    if (!cst) cst = st;
     if (b->n == 0) {
         if (o->n_pass) HIP_TRY(hipMemsetAsync(o->n_pass, 0, 4, st));
+        if (done) HIP_TRY(hipEventRecord(done, st));
         return BT_OK;
     }
+    bt_ctx::Ws* w = nullptr;
+    int wk = 0;
     if (compact) {
         int rc = ensure_ws(c, b->n);
         if (rc) return rc;
+        wk = c->ws_next;
+        w = &c->ws[wk];
+        c->ws_next ^= 1;
     }
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
     MainArgs a{};
@@ -259,16 +314,18 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.n_cap = o->records ? o->n_cap : 0;
     a.records = reinterpret_cast<uint8_t*>(o->records);
     a.decide = o->decide;
-    a.verdict = o->verdict ? o->verdict : (compact ? c->verdict : nullptr);
-    a.tile_pass = compact ? c->tile_pass : nullptr;
+    a.verdict = o->verdict ? o->verdict : (w ? w->verdict : nullptr);
+    if (w && !o->verdict) { int rc = ws_touch(w, st); if (rc) return rc; }   // the main kernel writes w->verdict
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
     a.dfa = c->dfa_dev[c->dfa_cur];
     a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
-    // Cache policy (measured, profiles/r01): non-temporal record stores everywhere
-    // (C2 +3..9 %), non-temporal header loads in descriptor mode (C3 +15 %, C4 +8 %;
-    // they cost C2 a little). BT_OPT_CACHE_DEFAULT turns both off, BT_OPT_NT_* force on.
+    // Cache policy (measured): non-temporal record stores everywhere (C2 +3..9 %,
+    // profiles/r01) and non-temporal header loads (descriptor mode: C3 +15 %, C4 +8 %,
+    // profiles/r01; fixed stride since round 2's kernels: c2f kernel 0.349-0.358 against
+    // 0.364-0.365 ms, C2 0.332-0.337 against 0.347-0.348, profiles/r02/ab/nt_loads_fixed.txt).
+    // BT_OPT_CACHE_DEFAULT turns both off, BT_OPT_NT_* force them on.
     if (c->opts.flags & BT_OPT_CACHE_DEFAULT) a.nt = 0;
-    else a.nt = 1u | (b->desc ? 2u : 0u);
+    else a.nt = 3u;
     if (c->opts.flags & BT_OPT_NT_STORES) a.nt |= 1u;
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
@@ -281,15 +338,24 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     }
     // e0 / e1 time the main kernel from its own dispatch packet (no marker packets: a
     // pair of hipEventRecord around the launch left the GPU idle ~6 us each, per step)
-    int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, e1);
+    const bool piped = compact && cst != st;
+    // pipelined: the compaction stream waits for this main kernel's end, signalled by
+    // the kernel's own dispatch (e1, or main_done)
+    hipEvent_t mend = piped && !e1 ? c->main_done[wk] : e1;
+    int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, mend);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (a.dfa_bytes) {   // the pool this launch reads stays untouched until it has run
         HIP_TRY(hipEventRecord(c->dfa_ev[c->dfa_cur], st));
         c->dfa_used[c->dfa_cur] = true;
     }
     if (compact) {
-        rc = launch_compact(a.verdict, c->tile_pass, a.ntiles, b->n, c->chunk_sums, o->pass_idx, o->n_pass, st);
+        if (piped) HIP_TRY(hipStreamWaitEvent(cst, mend, 0));
+        if ((rc = ws_touch(w, cst))) return rc;
+        rc = launch_compact(a.verdict, a.ntiles, w->chunk_sums, o->pass_idx, o->n_pass, cst);
         if (rc) return fail(rc, "compaction launch failed");
+        if (done) HIP_TRY(hipEventRecord(done, cst));
+    } else if (done) {
+        HIP_TRY(hipEventRecord(done, st));
     }
     return BT_OK;
 }
@@ -405,12 +471,18 @@ void bt_destroy(bt_ctx* c) {
     free_host(c);
     c->pool.reset();
     if (c->tgraph) (void)hipGraphExecDestroy(c->tgraph);
-    if (c->tile_pass) { (void)hipFree(c->tile_pass); (void)hipFree(c->chunk_sums); (void)hipFree(c->verdict); }
+    free_ws(c);
+    for (auto& w : c->ws)
+        if (w.sync) (void)hipEventDestroy(w.sync);
+    for (auto e : c->main_done)
+        if (e) (void)hipEventDestroy(e);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     for (int k = 0; k < 2; ++k) {
         if (c->dfa_dev[k]) (void)hipFree(c->dfa_dev[k]);
         if (c->dfa_ev[k]) (void)hipEventDestroy(c->dfa_ev[k]);
     }
     for (auto e : c->tev) (void)hipEventDestroy(e);
+    if (c->pipe_done) (void)hipEventDestroy(c->pipe_done);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ex_h) (void)hipHostFree(c->ex_h);
@@ -504,6 +576,16 @@ int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, vo
     return run_device(c, b, o, st, false, nullptr, nullptr);
 }
 
+
+int bt_parse_filter_device_async(bt_ctx* c, const bt_batch* b, const bt_outputs* o, void* stream,
+                                 void* done_event) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = ensure_cstream(c)) return rc;
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    return run_device(c, b, o, st, false, nullptr, nullptr, c->cstream, reinterpret_cast<hipEvent_t>(done_event));
+}
+
 // The host side of a timed loop whose launches (K of them, each between the event pair
 // c->tev[2i], c->tev[2i+1]) were enqueued on c->stream after c->ev0 at h0, followed by
 // c->ev1: wait by polling, then fill the breakdown.
@@ -572,52 +654,72 @@ static int ensure_timing_events(bt_ctx* c, uint32_t iters) {
     return BT_OK;
 }
 
-int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
-    if (!c || !b || !o || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
+int bt_time_device2(bt_ctx* c, const bt_batch* b, const bt_outputs* outs, uint32_t n_out, uint32_t iters,
+                    uint32_t mode, bt_timing* t) {
+    if (!c || !b || !outs || !n_out || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
+    if (mode & ~(uint32_t)(BT_TIME_KERNEL_EVENTS | BT_TIME_PIPELINED)) return fail(BT_E_INVALID_ARGUMENT, "unknown mode");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    if (int rc = ensure_timing_events(c, iters)) return rc;
-    // Default: plain launches with an event pair around every main kernel. BT_OPT_GRAPH:
-    // the K steps replay as one hipGraph (no per-kernel events: HIP cannot time events
-    // recorded inside a captured graph), main_ms is then reported as -1.
-    const bool use_graph = (c->opts.flags & BT_OPT_GRAPH) != 0;
+    const bool kev = (mode & BT_TIME_KERNEL_EVENTS) != 0;
+    const bool piped = (mode & BT_TIME_PIPELINED) != 0;
+    if (kev) { if (int rc = ensure_timing_events(c, iters)) return rc; }
+    // BT_OPT_GRAPH: the K steps replay as one hipGraph (no per-kernel events: HIP cannot
+    // time events recorded inside a captured graph), main_ms is then reported as -1.
+    const bool use_graph = (c->opts.flags & BT_OPT_GRAPH) != 0 && !piped;
+    const bt_outputs* o = outs;
     const bool cached = c->tgraph && c->tg_iters == iters && !std::memcmp(&c->tg_batch, b, sizeof(*b)) &&
                         !std::memcmp(&c->tg_out, o, sizeof(*o));
     if (use_graph && !cached) {
-        // Build once (the first call is the caller's untimed warm-up): event pair around
-        // every main-kernel launch + the compaction kernels, K times, in one graph.
+        // Build once (the first call is the caller's untimed warm-up): the main kernel +
+        // the compaction kernels, K times, in one graph.
         if (c->tgraph) { (void)hipGraphExecDestroy(c->tgraph); c->tgraph = nullptr; }
         if (o->pass_idx || o->n_pass) { int rc = ensure_ws(c, b->n); if (rc) return rc; }
         hipGraph_t g = nullptr;
         HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
         int rc = BT_OK;
-        hipError_t e = hipSuccess;
         for (uint32_t i = 0; rc == BT_OK && i < iters; ++i) rc = run_device(c, b, o, c->stream, false, nullptr, nullptr);
         hipError_t ee = hipStreamEndCapture(c->stream, &g);
         if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
-        if (e != hipSuccess || ee != hipSuccess || !g)
-            return fail(BT_E_INTERNAL, "graph capture failed: %s", hipGetErrorString(e != hipSuccess ? e : ee));
-        e = hipGraphInstantiate(&c->tgraph, g, nullptr, nullptr, 0);
+        if (ee != hipSuccess || !g) return fail(BT_E_INTERNAL, "graph capture failed: %s", hipGetErrorString(ee));
+        hipError_t e = hipGraphInstantiate(&c->tgraph, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
         if (e != hipSuccess) { c->tgraph = nullptr; return fail(BT_E_INTERNAL, "hipGraphInstantiate: %s", hipGetErrorString(e)); }
         c->tg_batch = *b;
         c->tg_out = *o;
         c->tg_iters = iters;
     }
+    if (piped) {
+        if (int rc = ensure_cstream(c)) return rc;
+        if (!c->pipe_done) HIP_TRY(hipEventCreateWithFlags(&c->pipe_done, hipEventDisableTiming));
+    }
     const auto h0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
     if (use_graph) {
-        HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(hipGraphLaunch(c->tgraph, c->stream));
-        HIP_TRY(hipEventRecord(c->ev1, c->stream));
     } else {
-        HIP_TRY(hipEventRecord(c->ev0, c->stream));
+        // Step i uses output set i % n_out. Pipelined (bt_parse_filter_device_async per
+        // step): each compaction runs beside the next step's main kernel and the last one
+        // joins c->stream before the closing event. The per-kernel event pairs
+        // (BT_TIME_KERNEL_EVENTS) are recorded by the main kernel's own dispatch; they cost
+        // the GPU ~9 us per launch on gfx950 (tools/calib/boundary.hip), so the bench
+        // times its steps without them and measures the kernel in a second pass.
         for (uint32_t i = 0; i < iters; ++i) {
-            int rc = run_device(c, b, o, c->stream, false, c->tev[2 * i], c->tev[2 * i + 1]);
+            const bt_outputs* oi = outs + (i % n_out);
+            hipEvent_t e0 = kev ? c->tev[2 * i] : nullptr, e1 = kev ? c->tev[2 * i + 1] : nullptr;
+            int rc = piped ? run_device(c, b, oi, c->stream, false, e0, e1, c->cstream,
+                                        i + 1 == iters ? c->pipe_done : nullptr)
+                           : run_device(c, b, oi, c->stream, false, e0, e1);
             if (rc) return rc;
         }
-        HIP_TRY(hipEventRecord(c->ev1, c->stream));
+        if (piped) HIP_TRY(hipStreamWaitEvent(c->stream, c->pipe_done, 0));
     }
-    return finish_timing(c, iters, use_graph, h0, t, "bt_time_device");
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    return finish_timing(c, iters, use_graph || !kev, h0, t, "bt_time_device");
+}
+
+int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
+    const uint32_t mode = BT_TIME_KERNEL_EVENTS | ((c && (c->opts.flags & BT_OPT_PIPELINE)) ? BT_TIME_PIPELINED : 0u);
+    return bt_time_device2(c, b, o, 1, iters, mode, t);
 }
 
 int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
@@ -857,6 +959,7 @@ int bt_synchronize(bt_ctx* c) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->cstream) HIP_TRY(hipStreamSynchronize(c->cstream));
     return BT_OK;
 }
 
@@ -952,9 +1055,11 @@ int bt_extract_device(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, 
     return run_extract(c, b, t, never, out, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
 }
 
-int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
-                       const bt_extract_out* out, uint32_t iters, bt_timing* t) {
+int bt_time_extract2(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
+                     const bt_extract_out* out, uint32_t iters, uint32_t mode, bt_timing* t) {
     if (!c || !b || !out || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
+    if (mode & ~(uint32_t)BT_TIME_KERNEL_EVENTS) return fail(BT_E_INVALID_ARGUMENT, "unknown mode");
+    const bool kev = (mode & BT_TIME_KERNEL_EVENTS) != 0;
     ExTable tab;
     bool never = false;
     int rc = build_table(fields, n_fields, &tab, nullptr, &never);
@@ -962,13 +1067,20 @@ int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields,
     if (never || !b->n) return fail(BT_E_INVALID_ARGUMENT, "nothing to time: empty batch or a span no frame reaches");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = ensure_timing_events(c, iters))) return rc;
+    if (kev && (rc = ensure_timing_events(c, iters))) return rc;
     const auto h0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     for (uint32_t i = 0; i < iters; ++i)
-        if ((rc = run_extract(c, b, tab, never, out, c->stream, c->tev[2 * i], c->tev[2 * i + 1]))) return rc;
+        if ((rc = run_extract(c, b, tab, never, out, c->stream, kev ? c->tev[2 * i] : nullptr,
+                              kev ? c->tev[2 * i + 1] : nullptr)))
+            return rc;
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
-    return finish_timing(c, iters, false, h0, t, "bt_time_extract");
+    return finish_timing(c, iters, !kev, h0, t, "bt_time_extract");
+}
+
+int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
+                       const bt_extract_out* out, uint32_t iters, bt_timing* t) {
+    return bt_time_extract2(c, b, fields, n_fields, out, iters, BT_TIME_KERNEL_EVENTS, t);
 }
 
 int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,

@@ -30,9 +30,15 @@ Captures are generated range by range on the host (bt_synth_fill_range) and stre
 the device, so no rank holds a whole capture in host memory.
 
 Timing: W untimed warm-up steps; then barrier + device sync, K steps, device sync +
-barrier; max over ranks. bt_time_device_ex launches the K steps with an event pair on
-every main kernel (from its own dispatch packet) and waits by polling, and its
-breakdown (enqueue / first event seen / last event seen / GPU span) goes into the line.
+barrier; max over ranks. bt_time_device2 enqueues the K steps between one event pair and
+waits by polling; its breakdown (enqueue / first event seen / last event seen / GPU span)
+goes into the line. Steps with a compaction are pipelined (bt_parse_filter_device_async:
+step i's compaction runs on a second stream beside step i+1's main kernel; two output
+sets alternate, so no step rewrites a verdict buffer its predecessor's compaction still
+reads); every step's outputs are complete when the timed region ends. The main kernel's
+duration (roofline.kernel_ms) comes from a second pass of the same K steps with an event
+pair recorded by every main kernel's own dispatch: those events cost the GPU ~9 us per
+step (tools/calib/boundary.hip), so the timed region carries none.
 The CPU baseline is the reference's own parser + PacketFilter (oracle/_ref, compiled
 from the reference sources) on rank 0, on every host CPU the process may use
 (affinity, bounded by the cgroup CPU quota when there is one), after all GPU timing.
@@ -311,9 +317,15 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
         prog = ctx.compile(wl["filters"])
         if wl.get("payload") and abi.KINDS[prog[0].kind] != "PAYLOAD":
             sys.exit(f"--payload {wl['payload']!r} is not GPU-compilable (kind {abi.KINDS[prog[0].kind]})")
+    # Steps with a compaction run pipelined (bt_parse_filter_device_async: each step's
+    # compaction beside the next step's main kernel) over two alternating output sets.
+    piped = filt and not args.no_pipeline
+    mode = abi.TIME_PIPELINED if piped else 0
+    outs = [run.outs, run.second_outputs()] if piped else [run.outs]
+    timed_mode = mode | (abi.TIME_KERNEL_EVENTS if args.kernel_events_in_timed else 0)
     for _ in range(args.warmup):
         run.run()
-    ctx.time_device_ex(run.batch, run.outs, args.steps)   # untimed: creates the per-launch event pairs
+    ctx.time_device2(run.batch, outs, args.steps, mode | abi.TIME_KERNEL_EVENTS)   # untimed: creates the event pairs
     n_pass = run.n_pass() if filt else 0
     if run.d_rec is None or not n:
         rec_bytes, rec_lines = 0, 0
@@ -336,12 +348,17 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    tm = ctx.time_device_ex(run.batch, run.outs, args.steps)
+    tm = ctx.time_device2(run.batch, outs, args.steps, timed_mode)
     ta = time.perf_counter()
     ctx.synchronize()
     barrier()
     t1 = time.perf_counter()
     step_s = (t1 - t0) / args.steps
+    # The main kernel's duration: the same K steps again, each main kernel between an
+    # event pair recorded by its own dispatch. Those events cost the GPU ~9 us per step
+    # (tools/calib/boundary.hip), so they stay out of the timed region above.
+    tk = tm if args.kernel_events_in_timed else ctx.time_device2(run.batch, outs, args.steps,
+                                                                 mode | abi.TIME_KERNEL_EVENTS)
 
     # algorithmic bytes of one main-kernel launch (SURVEY §8(d), R = the stored slabs):
     # min(len,128) header read + 8 B descriptor (0 for fixed stride) + R + 1 B decision
@@ -352,7 +369,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     # record lines + decisions + verdict words
     floor_read = cap.need_lines * LINE + (0 if wl["fixed"] else 8 * n)
     floor_write = rec_lines * LINE + ((n + (n + 63) // 64 * 8) if filt else 0)
-    main_ms = tm.main_ms
+    main_ms = tk.main_ms
     mine = {"step_s": step_s, "main_ms": main_ms, "n": n, "algo": algo, "pass": n_pass,
             "host_ms": 1e3 * (ta - t0), "tail_ms": 1e3 * (t1 - ta)}
     ranks = [mine]
@@ -375,7 +392,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
             "traffic_floor_read_per_packet": round(floor_read / max(n, 1), 2),
             "traffic_floor_write_per_packet": round(floor_write / max(n, 1), 2),
             "kernel": main_kernel_name(wl, flags), "kernel_ms": round(main_ms, 4),
-            "kernel_ms_min": round(tm.main_min_ms, 4), "kernel_ms_max": round(tm.main_max_ms, 4),
+            "kernel_ms_min": round(tk.main_min_ms, 4), "kernel_ms_max": round(tk.main_max_ms, 4),
             "algorithmic_bytes_per_packet": round(algo / max(n, 1), 2),
             "record_bytes_per_packet": round(rec_bytes / max(n, 1), 2),
             "kernel_mpps": round(n / (main_ms * 1e-3) / 1e6, 1),
@@ -386,7 +403,12 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     timing = tm.as_dict()
     timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4), "host_call_ms": round(mine["host_ms"], 4),
                    "tail_sync_ms": round(mine["tail_ms"], 4),
-                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None})
+                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None,
+                   "pipelined": piped, "output_sets": len(outs),
+                   "kernel_events_in_timed_region": bool(args.kernel_events_in_timed)})
+    timing["kernel_pass"] = {k: v for k, v in tk.as_dict().items()
+                             if k in ("span_ms", "main_ms", "main_min_ms", "main_max_ms", "lead_ms", "gap_ms")}
+    timing["kernel_pass"]["ms_per_step"] = round(tk.span_ms / args.steps, 4)
     out = {"workload": wl["name"], "value": round(value, 2), "unit": "Mpps", "ms_per_step": round(step_max * 1e3, 4),
            "scaling": "strong" if strong else "weak", "packets_per_gpu": n, "packets_total": n_job,
            "pass_fraction": round(n_pass / n, 4) if filt and n else None, "roofline": roof, "timing": timing}
@@ -416,10 +438,11 @@ def measure_extract(name, wl, args, ctx, rank):
         ex.run()
     ctx.synchronize()
     t0 = time.perf_counter()
-    tm = ex.time(args.steps)
+    tm = ex.time(args.steps, abi.TIME_KERNEL_EVENTS if args.kernel_events_in_timed else 0)
     ctx.synchronize()
     t1 = time.perf_counter()
     step_s = (t1 - t0) / args.steps
+    tk = tm if args.kernel_events_in_timed else ex.time(args.steps)   # the kernel pass (see measure)
     span, nf = ex.span, len(fields)
     # algorithmic bytes: the [0, span) prefix read + status byte + one u64 per field + the
     # span-byte image; the floor reads the 128-B lines of those prefixes
@@ -430,23 +453,27 @@ def measure_extract(name, wl, args, ctx, rank):
     wr = n * (1 + 8 * nf + span)
     algo = rd + wr
     floor = lines * LINE + sum(-(-b // LINE) * LINE for b in (n, 8 * nf * n, span * n))
-    achieved = algo / (tm.main_ms * 1e-3) / 1e9
+    achieved = algo / (tk.main_ms * 1e-3) / 1e9
     traffic_rec, traffic_src = load_traffic(args.traffic_json, name, n)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic_rec["traffic"] if traffic_rec else None, "traffic_source": traffic_src,
             "traffic_bytes_per_packet": round(traffic_rec["traffic"] / n, 2) if traffic_rec else None,
             "traffic_floor": floor, "traffic_floor_bytes_per_packet": round(floor / n, 2),
-            "kernel": "bt_extract_tile", "kernel_ms": round(tm.main_ms, 4),
-            "kernel_ms_min": round(tm.main_min_ms, 4), "kernel_ms_max": round(tm.main_max_ms, 4),
-            "algorithmic_bytes_per_packet": round(algo / n, 2), "kernel_mpps": round(n / (tm.main_ms * 1e-3) / 1e6, 1),
+            "kernel": "bt_extract_tile", "kernel_ms": round(tk.main_ms, 4),
+            "kernel_ms_min": round(tk.main_min_ms, 4), "kernel_ms_max": round(tk.main_max_ms, 4),
+            "algorithmic_bytes_per_packet": round(algo / n, 2), "kernel_mpps": round(n / (tk.main_ms * 1e-3) / 1e6, 1),
             "gpu_span_ms_per_step": round(tm.span_ms / args.steps, 4)}
     if traffic_rec:
         roof["traffic_read_per_packet"] = traffic_rec.get("read_per_packet")
         roof["traffic_write_per_packet"] = traffic_rec.get("write_per_packet")
     timing = tm.as_dict()
     timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4),
-                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None})
+                   "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None,
+                   "kernel_events_in_timed_region": bool(args.kernel_events_in_timed)})
+    timing["kernel_pass"] = {k: v for k, v in tk.as_dict().items()
+                             if k in ("span_ms", "main_ms", "main_min_ms", "main_max_ms", "lead_ms", "gap_ms")}
+    timing["kernel_pass"]["ms_per_step"] = round(tk.span_ms / args.steps, 4)
     out = {"workload": wl["name"], "value": round(n / step_s / 1e6, 2), "unit": "Mpps",
            "ms_per_step": round(step_s * 1e3, 4), "scaling": "weak", "packets_per_gpu": n, "packets_total": n,
            "parsed_fraction": round(ok / n, 4), "table": [list(f) for f in fields], "span": span,
@@ -529,6 +556,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--grid-waves", type=int, default=0, help="persistent grid size in wavefronts (0 = auto)")
     ap.add_argument("--no-prefetch", action="store_true", help="A/B: disable the next-tile load prefetch")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="A/B: each step's compaction on the main stream (bt_parse_filter_device)")
+    ap.add_argument("--kernel-events-in-timed", action="store_true",
+                    help="A/B: time the main kernels inside the timed region (round 2's first form)")
     ap.add_argument("--flags", type=int, default=None, help="raw bt_opts.flags (A/B experiments)")
     ap.add_argument("--payload", default=None,
                     help="put a PAYLOAD regex FIRST in the headline's filter program (every IPv4 packet runs "

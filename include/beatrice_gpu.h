@@ -291,6 +291,7 @@ typedef struct bt_opts {
 #define BT_OPT_PAYLOAD_HOST 0x200u /* keep every PAYLOAD filter on the host (std::regex) */
 #define BT_OPT_WIDE_NEVER 0x400u   /* descriptor mode: always two-round loads (A/B only)   */
 #define BT_OPT_WIDE_ALWAYS 0x800u  /* descriptor mode: always wide round A (A/B only)      */
+#define BT_OPT_PIPELINE 0x2000u    /* bt_time_device: steps as bt_parse_filter_device_async */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
@@ -347,6 +348,17 @@ int  bt_reserve(bt_ctx* ctx, uint32_t n);
  * the context's own stream). records != NULL selects parsing; the filter
  * outputs are produced when any of verdict/decide/pass_idx/n_pass is set. */
 int  bt_parse_filter_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, void* stream);
+
+/* Pipelined form for a stream of batches. The main kernel runs on `stream` as above
+ * (records, decide and verdict are complete in stream order); the ordered compaction
+ * (pass_idx, n_pass) runs on the context's own compaction stream once that kernel has
+ * finished, and `done_event` (a hipEvent_t, may be NULL) is recorded after it. The next
+ * call's main kernel on `stream` does not wait for it, so the compaction of batch i runs
+ * beside the parse of batch i + 1. Until done_event completes, the caller must neither
+ * read pass_idx / n_pass nor rewrite this call's verdict buffer (the compaction reads
+ * it): alternate two output sets. */
+int  bt_parse_filter_device_async(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, void* stream,
+                                  void* done_event);
 
 /* Host batch: borrows base/desc for the call, copies through pinned staging in
  * chunks (H2D, kernels, D2H double-buffered on two streams), fills host outputs,
@@ -442,6 +454,7 @@ int  bt_dev_free(bt_ctx* ctx, void* p);
 int  bt_memcpy_h2d(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
+/* Waits for the context's stream and its compaction stream (bt_parse_filter_device_async). */
 int  bt_synchronize(bt_ctx* ctx);
 /* Timing of a device-resident run on the context stream: `iters` steps, each = the
  * main kernel between an event pair + the compaction kernels; returns the event span
@@ -472,6 +485,20 @@ typedef struct bt_timing {
 } bt_timing;
 int  bt_time_device_ex(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t iters,
                        bt_timing* timing);
+/* The general form. Step i writes output set out[i % n_out]. mode:
+ *   BT_TIME_KERNEL_EVENTS  an event pair on every main kernel (main_ms, lead_ms, gap_ms);
+ *                          recorded by the kernel's own dispatch, they cost the GPU ~9 us
+ *                          per step on gfx950, so a throughput loop leaves them out and
+ *                          the kernel is timed in a second call;
+ *   BT_TIME_PIPELINED      the steps as bt_parse_filter_device_async (n_out = 2 keeps the
+ *                          API's rule that a call's verdict buffer is not rewritten
+ *                          before its compaction is done).
+ * bt_time_device_ex = mode BT_TIME_KERNEL_EVENTS (| BT_TIME_PIPELINED under
+ * BT_OPT_PIPELINE), n_out = 1. Without kernel events main_ms.. are -1, lead/gap 0. */
+#define BT_TIME_KERNEL_EVENTS 0x1u
+#define BT_TIME_PIPELINED     0x2u
+int  bt_time_device2(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t n_out,
+                     uint32_t iters, uint32_t mode, bt_timing* timing);
 
 /* ---- user-defined protocols: ProtocolParser with any ProtocolDefinition -------------
  * Replaces ProtocolParser::parsePacketInternal / extractField / extractValue<T>
@@ -534,6 +561,9 @@ int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens,
  * batch or a table whose span no frame can reach (nothing would launch). */
 int  bt_time_extract_ex(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
                         const bt_extract_out* out, uint32_t iters, bt_timing* timing);
+/* The same with a mode (BT_TIME_KERNEL_EVENTS only; without it main_ms.. are -1). */
+int  bt_time_extract2(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
+                      const bt_extract_out* out, uint32_t iters, uint32_t mode, bt_timing* timing);
 
 /* ---- text output --------------------------------------------------------------
  * The text the reference's ParseResult formatters print for every walked layer of

@@ -438,3 +438,66 @@ def test_random_programs_match_oracle(gpu_ctx, cfg):
         assert len(bad) == 0, f"program {i} {prog}: {len(bad)} decisions differ, first {bad[:5]}"
         assert out["n_pass"] == npass, f"program {i}"
         check_filter_outputs(out, n)
+
+
+def test_async_pipeline_batches_match_oracle():
+    """bt_parse_filter_device_async over a stream of 6 different batches (C3 and fixed-stride
+    C2, alternating two output sets as the API asks): each compaction runs on the context's
+    compaction stream beside the next batch's main kernel, with the double-buffered
+    workspace alternating under it. Every batch's records, decisions, verdicts and ordered
+    pass list equal the oracle's."""
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    ctx = abi.Context(0)
+    runs, caps = [], []
+    try:
+        ctx.compile(filters)
+        for i in range(6):
+            n = 50000 + 4099 * i
+            if i % 2:
+                data, desc = synth.capture(synth.C3, n, seed=0xA5 + i)
+                caps.append((data, desc, n, 0))
+                runs.append(abi.DeviceRun(ctx, data, desc, n))
+            else:
+                data, desc = synth.capture(synth.C2, n, seed=0xA5 + i)
+                caps.append((data, None, n, 64))
+                runs.append(abi.DeviceRun(ctx, data, None, n, stride=64))
+        for rnd in range(2):   # two rounds: batch i's outputs rewritten by the second round
+            for r in runs:
+                ctx.run_device_async(r.batch, r.outs)
+        ctx.synchronize()
+        for (data, desc, n, stride), r in zip(caps, runs):
+            out = r.fetch()
+            rec, dec, npass = ol.oracle_run(data, desc, n, filters, stride=stride)
+            assert np.array_equal(out["records"], rec)
+            assert np.array_equal(out["decide"], dec)
+            assert out["n_pass"] == npass
+            check_filter_outputs(out, n)
+    finally:
+        for r in runs:
+            r.free()
+        ctx.close()
+
+
+def test_pipelined_timing_outputs():
+    """BT_OPT_PIPELINE (bench's pipelined steps): after a timed run of 8 steps the outputs
+    are those of one synchronous call."""
+    n = 1 << 20
+    data, desc = synth.capture(synth.C3, n, seed=0x77)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2}]
+    ctx = abi.Context(0, flags=abi.OPT_PIPELINE)
+    try:
+        ctx.compile(filters)
+        r = abi.DeviceRun(ctx, data, desc, n)
+        t = ctx.time_device_ex(r.batch, r.outs, 8)
+        assert t.span_ms > 0 and t.main_ms > 0
+        out = r.fetch()
+        rec, dec, npass = ol.oracle_run(data, desc, n, filters)
+        assert np.array_equal(out["records"], rec) and np.array_equal(out["decide"], dec)
+        assert out["n_pass"] == npass
+        check_filter_outputs(out, n)
+        r.free()
+    finally:
+        ctx.close()
