@@ -156,7 +156,12 @@ struct bt_ctx {
         hipEvent_t sync = nullptr;
     } ws[2];
     int ws_next = 0;
-    hipEvent_t main_done[2] = {nullptr, nullptr};   // pipelined: main kernel -> compaction stream
+    // pipelined: main kernel -> compaction stream. A ring, so that an event is re-recorded
+    // only long after the wait on its previous record has been consumed (re-recording one
+    // of two alternating events cost ~7 us per step, profiles/r02/ab/timing_modes.txt).
+    static constexpr int kMainDone = 8;
+    hipEvent_t main_done[kMainDone] = {};
+    int md_next = 0;
     hipStream_t cstream = nullptr;     // pipelined compaction (bt_parse_filter_device_async)
 
     // host pipeline
@@ -291,12 +296,10 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
         return BT_OK;
     }
     bt_ctx::Ws* w = nullptr;
-    int wk = 0;
     if (compact) {
         int rc = ensure_ws(c, b->n);
         if (rc) return rc;
-        wk = c->ws_next;
-        w = &c->ws[wk];
+        w = &c->ws[c->ws_next];
         c->ws_next ^= 1;
     }
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
@@ -341,7 +344,11 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     const bool piped = compact && cst != st;
     // pipelined: the compaction stream waits for this main kernel's end, signalled by
     // the kernel's own dispatch (e1, or main_done)
-    hipEvent_t mend = piped && !e1 ? c->main_done[wk] : e1;
+    hipEvent_t mend = e1;
+    if (piped && !e1) {
+        mend = c->main_done[c->md_next];
+        c->md_next = (c->md_next + 1) % bt_ctx::kMainDone;
+    }
     int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, mend);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (a.dfa_bytes) {   // the pool this launch reads stays untouched until it has run
