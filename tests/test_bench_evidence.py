@@ -153,6 +153,25 @@ def test_r02_default_line_covers_every_config():
     assert d["value"] == pytest.approx(d["config"]["packets_total"] / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
 
 
+def test_r02_default_line_timing_form():
+    """The committed line's timed region: pipelined compaction over two output sets for
+    the entries with a filter, no per-kernel events inside it, and a kernel pass (events
+    on every main kernel) whose mean is the roofline's kernel_ms and whose steps run as
+    fast as the timed ones (the warm-up leads straight into the timed region)."""
+    d = _line(os.path.join(R02, "bench_default.json"))
+    entries = [("c2f", d)] + list(d["configs"].items())
+    for k, e in entries:
+        t, r = e["timing"], e["roofline"]
+        assert t["kernel_events_in_timed_region"] is False, k
+        assert t["main_ms"] == -1, k   # no kernel events in the timed pass
+        kp = t["kernel_pass"]
+        assert kp["main_ms"] == pytest.approx(r["kernel_ms"], abs=1e-3), k
+        assert kp["main_ms"] <= e["ms_per_step"], k
+        assert e["ms_per_step"] <= 1.04 * kp["ms_per_step"], k
+        if k != "c1":
+            assert t["pipelined"] == (k != "c2") and t["output_sets"] == (1 if k == "c2" else 2), k
+
+
 def test_r02_two_rank_line_has_per_rank_entries():
     d = _line(os.path.join(R02, "bench_2rank_one_gpu.json"))
     assert d["n_gpus"] == 2 and len(d["per_rank"]) == 2
