@@ -393,10 +393,28 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
 // F = 1: no PAYLOAD slot in the program: every slot is evaluated in its uniform-predicate
 // form (bt_device.h DevFilter), one straight-line sequence with no per-kind branches.
 // F = 2: the per-kind evaluator and the GPU DFA for PAYLOAD slots.
+// The first kHotSlots slots of the program, read from the kernel arguments once per wave
+// before the tile loop and kept in registers. The slot loop used to read each slot with
+// a scalar load from the kernel-argument segment and wait for it, once per slot and tile:
+// a memory round trip on the parse's critical path (c2f at 2 blocks/CU: 0.391 ms with
+// the filter evaluated, 0.333 without; tools/gpu_ab_libs_grid.sh).
+constexpr uint32_t kHotSlots = 4;
+struct HotProgram {
+    uint32_t n;
+    DevFilter f[kHotSlots];
+};
+__device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
+    HotProgram h;
+    h.n = prog.n;
+#pragma unroll
+    for (uint32_t k = 0; k < kHotSlots; ++k) h.f[k] = prog.f[k];
+    return h;
+}
+
 template <int F>
-__device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const uint8_t* dfa_lds,
-                                                  uint32_t* lrow, uint64_t my_off, uint32_t len,
-                                                  const uint32_t* w0, bool live, uint32_t& slot) {
+__device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const HotProgram& hot,
+                                                  const uint8_t* dfa_lds, uint32_t* lrow, uint64_t my_off,
+                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot) {
     FilterIn x;
     x.gate = (len >= 34) & (be16_of(w0, 12) == 0x0800u);
     x.proto = byte_of(w0, 23);
@@ -411,17 +429,35 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
     if constexpr (F == 1) {
         const uint32_t pbit = (x.proto == 6 ? 1u : 0u) | (x.proto == 17 ? 2u : 0u) | (x.proto == 1 ? 4u : 0u);
         const bool g4 = x.gate & x.l4_ok;
-        for (uint32_t f = 0; f < prog.n; ++f) {
-            if (__ballot(open) == 0ull) break;
-            const DevFilter& d = prog.f[f];
+        // slot f's result on this packet: 1 pass, 0 reject, 2 throw, 3 host
+        auto result = [&](const DevFilter& d) -> uint32_t {
             const uint32_t sel = d.ctl & 3u, gm = (d.ctl >> 2) & 3u, rm = (d.ctl >> 4) & 3u;   // uniform
             const uint32_t x1 = sel == kSelIp ? x.src : sel == kSelPort ? x.sport : sel == kSelProto ? x.proto : pbit;
             const uint32_t x2 = sel == kSelIp ? x.dst : sel == kSelPort ? x.dport : sel == kSelProto ? x.proto : pbit;
             const bool pred = (((x1 & d.mask) - d.lo) <= d.span) | (((x2 & d.mask) - d.lo) <= d.span);
             const bool g = gm == kGateNone ? true : gm == kGateIpv4 ? x.gate : g4;
-            const uint32_t r = !g ? 0u : rm == kResPred ? (pred ? 1u : 0u) : rm == kResThrow ? 2u : 3u;
-            if (open && r != 1u) {
-                code = r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+            return !g ? 0u : rm == kResPred ? (pred ? 1u : 0u) : rm == kResThrow ? 2u : 3u;
+        };
+        auto decide = [](uint32_t r) {
+            return r == 0u ? BT_DECIDE_REJECT : r == 2u ? BT_DECIDE_THROW : BT_DECIDE_HOST;
+        };
+        // The hot slots side by side: their results are independent, so they are computed
+        // without the early exit's branches (which made one long dependent chain of
+        // compares, lane-mask and branch instructions per slot, which two waves per SIMD
+        // could not hide), then the first slot that did not pass decides (AND chain order).
+        uint32_t r[kHotSlots];
+#pragma unroll
+        for (uint32_t f = 0; f < kHotSlots; ++f) r[f] = f < hot.n ? result(hot.f[f]) : 1u;
+#pragma unroll
+        for (int f = (int)kHotSlots - 1; f >= 0; --f)
+            if (r[f] != 1u) { code = decide(r[f]); slot = (uint32_t)f; }
+        if (!live) { code = BT_DECIDE_PASS; slot = prog.n ? prog.n - 1u : 0u; }
+        open = live && code == BT_DECIDE_PASS;
+        for (uint32_t f = kHotSlots; f < prog.n; ++f) {   // longer programs: the rest from memory
+            if (__ballot(open) == 0ull) break;
+            const uint32_t rf = result(prog.f[f]);
+            if (open && rf != 1u) {
+                code = decide(rf);
                 slot = f;
                 open = false;
             }
@@ -445,6 +481,8 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
     }
     return code;
 }
+
+__device__ uint4 g_zero16[8];                    // source of the loads that read nothing
 
 // Header windows of one 64-packet tile in flight in registers (LOAD stage).
 //  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
@@ -474,7 +512,10 @@ __device__ __forceinline__ uint32_t round_a_end_wide(uint64_t a0, uint32_t sq, u
     return want < line_rem ? want : line_rem;
 }
 
-template <int FIXED_LOG2>
+// LATE (fixed stride, bt_parse_filter_main's late issue): every lane loads, the zero line
+// past n, always non-temporal, so every path issues the same four loads and the loop top
+// can wait for each with a counted vmcnt.
+template <int FIXED_LOG2, bool LATE = false>
 __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint32_t lane, Stage<FIXED_LOG2>& st,
                                             bool wide, uint32_t need_max) {
     const uint32_t p0 = t * 64u;
@@ -490,7 +531,10 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
         for (uint32_t j = 0; j < cpp; ++j) {
             const uint32_t g = j * 64u + lane;
             const bool ok = p0 + (g >> kL) < a.n;
-            st.v[j] = ok ? ld16(span + (uint64_t)g * 16u, a.nt & 2u) : make_uint4(0, 0, 0, 0);
+            if (LATE)
+                st.v[j] = ld16(ok ? span + (uint64_t)g * 16u : reinterpret_cast<const uint8_t*>(g_zero16), true);
+            else
+                st.v[j] = ok ? ld16(span + (uint64_t)g * 16u, a.nt & 2u) : make_uint4(0, 0, 0, 0);
         }
     } else {
         if (a.desc) {
@@ -654,6 +698,17 @@ __device__ __forceinline__ bool round_b(const MainArgs& a, uint32_t t, uint32_t 
     return wide;
 }
 
+constexpr uint32_t kOob = 0x80000000u;           // buffer offset past every range: dropped / reads 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Whether bt_parse_filter_main issues the next tile's loads after the record stores (see
+// the kernel); launch_t sizes the grid by it.
+constexpr bool late_issue(int fixed_log2, int rec, int filter, bool prefetch) {
+    return fixed_log2 >= 0 && !prefetch && rec != kRecAoS && filter == 1;
+}
+
 template <int FIXED_LOG2, int REC, int FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
@@ -690,16 +745,37 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         step = total_waves;
     }
     const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
+    const HotProgram hot = hot_program(prog);
     bool wide = false;   // wave-uniform: previous tile mostly needed chunks 4..7
     Stage<FIXED_LOG2> st;
-    if (PREFETCH && t < t_end) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
+    // Fixed stride (not AoS): the next tile's loads are issued right after this tile's
+    // record stores, so they are in flight while the filter runs; only the decision and
+    // verdict stores (two unconditional buffer stores) follow them, and the loop top waits
+    // with vmcnt(2..5) instead of draining every store. The filter's dependent chain is
+    // then no longer added to each tile's load latency, and the 64-B parse+filter runs at
+    // 2 blocks/CU like the parse alone (c2f kernel 0.327 against 0.343-0.350 ms at 3
+    // blocks/CU without it; profiles/r02/ab/c2f_late_issue.txt). Not with PAYLOAD slots,
+    // whose staging loads would have to wait behind the next tile's loads, and not
+    // parse-only (nothing to overlap: C2 0.321 against 0.319 ms). Its header loads are
+    // always non-temporal (BT_OPT_CACHE_DEFAULT keeps the default policy for the rest).
+    constexpr bool LATE = late_issue(FIXED_LOG2, REC, FILTER, PREFETCH);
+    if ((PREFETCH || LATE) && t < t_end) issue_loads<FIXED_LOG2, LATE>(a, t, lane, st, wide, need_max);
+    if (LATE && FILTER && t < t_end) {
+        // stand-ins for a tile's decision / verdict stores (an empty range: dropped), so
+        // the loop top's wait counts the same operations on the first iteration as later
+        const auto r = rsrc_of(g_zero16, 0u);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, r, 0, 0, 0);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 z = {0u, 0u};
+        __builtin_amdgcn_raw_buffer_store_b64(z, r, 16, 0, 0);
+    }
     for (; t < t_end; t += step) {
         const uint32_t p0 = t * 64u;
         const uint32_t my = p0 + lane;
         const bool live = my < a.n;
 
         // ---- 1. LOAD (this tile's windows -> LDS; next tile's loads go in flight) ----
-        if (!PREFETCH) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
+        if (!PREFETCH && !LATE) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
         stage_to_lds<FIXED_LOG2>(st, img, lane);
         const uint64_t my_off = st.off;
         const uint32_t my_len = st.len;
@@ -770,13 +846,24 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             st16(tile + 64 + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
         }
 
+        if (LATE && t + step < t_end) issue_loads<FIXED_LOG2, LATE>(a, t + step, lane, st, wide, need_max);
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
-            if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
-            if (lane == 0 && a.verdict) a.verdict[t] = pass;   // also the compaction's input
+            if (LATE) {   // unconditional buffer stores: a static count behind the next loads
+                const uint32_t cnt = min(64u, a.n - p0);
+                const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
+                const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict ? 8u : 0u);
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
+            } else {
+                if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
+                if (lane == 0 && a.verdict) a.verdict[t] = pass;   // also the compaction's input
+            }
         }
         // ---- 4. AoS records: the tile's 64 bt_rec are one contiguous 6-KiB range. Each
         // lane's 96 B are written to the wave's LDS image (the row is free once the filter
@@ -815,12 +902,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 // descriptors are loaded one tile ahead. Every path then issues the same operations,
 // so the wait for the next tile's headers is vmcnt(K) with K = this tile's stores:
 // the stores retire in the background.
-__device__ uint4 g_zero16[8];                    // source of the loads that read nothing
-constexpr uint32_t kOob = 0x80000000u;           // buffer offset past every range: dropped / reads 0
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
 
 // The descriptors of tile t as the wave needs them: `me` = this lane's packet (the
 // parse), q[j] = packet j*16 + lane/4 (round A: four lanes per packet). Both are buffer
@@ -963,6 +1045,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     }
     if (t >= t_end) return;   // wave-uniform; no block barrier follows
     const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
+    const HotProgram hot = hot_program(prog);
     bool wide = false;
 
     // prologue: descriptors of t and t + step, round A of t (waited), then stand-ins for
@@ -1019,7 +1102,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
@@ -1182,7 +1265,9 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
         // parse+filter headline needs more waves: 0.366-0.368 ms at 3 blocks/CU against
         // 0.378-0.379 at 4 and 0.420-0.426 at 2 (round 2, alternating processes, 3
         // passes each; round 1's code was best at 4).
-        if (FL >= 0 && grid <= 0) g = std::min(g, (F ? 3 : 2) * cu_count());
+        // With the late issue (bt_parse_filter_main) the filter no longer needs the third
+        // block: c2f 0.327 ms at 2 blocks/CU against 0.343-0.350 at 3 without it.
+        if (FL >= 0 && grid <= 0) g = std::min(g, (F && !late_issue(FL, REC, F, false) ? 3 : 2) * cu_count());
         if ((uint32_t)g > needed) g = (int)(needed ? needed : 1);
         if (e0 || e1)
             hipExtLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, e0, e1, 0, a, prog);
