@@ -1276,10 +1276,17 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
     };
     if constexpr (FL < 0 && (REC == kRecTiled || REC == kRecNone)) {
         if (pf && a.desc && (a.nt & 1u) && use_pipe()) {
+            // At most 2 blocks/CU (the residency is 3): with the filter slots evaluated side
+            // by side, C3 0.491 against 0.498 ms and C4 0.915 against 0.948 at the residency
+            // (profiles/r02/ab/pipe_grid.txt; before that change the residency was level or
+            // better).
+            const int cap2 = 2 * cu_count();
             if (a.desc_words == 1)
-                go(bt_parse_filter_pipe<REC, F, 1>, grid > 0 ? 0 : resident_grid<bt_parse_filter_pipe<REC, F, 1>>(dyn));
+                go(bt_parse_filter_pipe<REC, F, 1>,
+                   grid > 0 ? 0 : std::min(cap2, resident_grid<bt_parse_filter_pipe<REC, F, 1>>(dyn)));
             else
-                go(bt_parse_filter_pipe<REC, F, 2>, grid > 0 ? 0 : resident_grid<bt_parse_filter_pipe<REC, F, 2>>(dyn));
+                go(bt_parse_filter_pipe<REC, F, 2>,
+                   grid > 0 ? 0 : std::min(cap2, resident_grid<bt_parse_filter_pipe<REC, F, 2>>(dyn)));
             return;
         }
     }
