@@ -183,6 +183,12 @@ struct bt_ctx {
     int spin_rc = -1;                  // hipSetDeviceFlags(hipDeviceScheduleSpin) result
     unsigned device_flags = 0;
 
+    // bt_memcpy_h2d / bt_memcpy_d2h: two pinned chunks, so no copy of the caller's
+    // (pageable) memory goes through the runtime's own pageable-copy path
+    std::mutex xfer_mu;
+    uint8_t* xfer_h[2] = {nullptr, nullptr};
+    hipEvent_t xfer_ev[2] = {nullptr, nullptr};
+
     // bt_extract (host lists): pinned + device staging, grown on demand
     uint8_t* ex_h = nullptr;
     uint8_t* ex_d = nullptr;
@@ -494,6 +500,10 @@ void bt_destroy(bt_ctx* c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ex_h) (void)hipHostFree(c->ex_h);
     if (c->ex_d) (void)hipFree(c->ex_d);
+    for (int k = 0; k < 2; ++k) {
+        if (c->xfer_h[k]) (void)hipHostFree(c->xfer_h[k]);
+        if (c->xfer_ev[k]) (void)hipEventDestroy(c->xfer_ev[k]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -550,8 +560,7 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
             HIP_TRY(hipEventCreateWithFlags(&c->dfa_ev[k], hipEventDisableTiming));
         }
         if (c->dfa_used[k]) HIP_TRY(hipEventSynchronize(c->dfa_ev[k]));
-        HIP_TRY(hipMemcpyAsync(c->dfa_dev[k], pool.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (int rc = bt_memcpy_h2d(c, c->dfa_dev[k], pool.data(), pool.size())) return rc;   // staged, synchronous
         c->dfa_used[k] = false;
         c->dfa_cur = k;
     }
@@ -939,18 +948,70 @@ int bt_dev_free(bt_ctx* c, void* p) {
 // Both copies are ordered on the context stream and complete before returning: a
 // pageable hipMemcpy on the null stream may return once the source is staged, and it is
 // not ordered with the context's non-blocking stream.
+}  // extern "C"
+
+namespace {
+
+constexpr size_t kXferChunk = size_t(8) << 20;
+
+int ensure_xfer(bt_ctx* c) {
+    for (int k = 0; k < 2; ++k) {
+        if (!c->xfer_h[k]) HIP_TRY(hipHostMalloc(&c->xfer_h[k], kXferChunk, hipHostMallocDefault));
+        if (!c->xfer_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->xfer_ev[k], hipEventDisableTiming));
+    }
+    return BT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Both copies go through the context's two pinned chunks (host memcpy of chunk k while the
+// DMA of chunk k^1 runs): the caller's memory is usually pageable (numpy arrays, vectors),
+// and the runtime's own pageable-copy path pins and maps such ranges behind the caller's
+// back. One GPU-suite run on a fresh box failed in exactly such an upload with "illegal
+// memory access" while every kernel before it had completed and been checked; with
+// staging, no DMA ever touches memory this library did not allocate.
 int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (bytes && (!dst || !src)) return fail(BT_E_INVALID_ARGUMENT, "null pointer");
+    std::lock_guard<std::mutex> lk(c->xfer_mu);
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    if (int rc = ensure_xfer(c)) return rc;
+    bool used[2] = {false, false};
+    int k = 0;
+    for (uint64_t off = 0; off < bytes; off += kXferChunk, k ^= 1) {
+        const size_t n = (size_t)std::min<uint64_t>(kXferChunk, bytes - off);
+        if (used[k]) HIP_TRY(hipEventSynchronize(c->xfer_ev[k]));   // its last DMA has read it
+        std::memcpy(c->xfer_h[k], static_cast<const uint8_t*>(src) + off, n);
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, c->xfer_h[k], n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->xfer_ev[k], c->stream));
+        used[k] = true;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return BT_OK;
 }
 
 int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (bytes && (!dst || !src)) return fail(BT_E_INVALID_ARGUMENT, "null pointer");
+    std::lock_guard<std::mutex> lk(c->xfer_mu);
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    if (int rc = ensure_xfer(c)) return rc;
+    // chunk i lands in buffer i & 1; chunk i + 1's DMA runs while chunk i is copied out
+    auto issue = [&](uint64_t off, int k) -> int {
+        const size_t n = (size_t)std::min<uint64_t>(kXferChunk, bytes - off);
+        HIP_TRY(hipMemcpyAsync(c->xfer_h[k], static_cast<const uint8_t*>(src) + off, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipEventRecord(c->xfer_ev[k], c->stream));
+        return BT_OK;
+    };
+    if (bytes) { if (int rc = issue(0, 0)) return rc; }
+    int k = 0;
+    for (uint64_t off = 0; off < bytes; off += kXferChunk, k ^= 1) {
+        if (off + kXferChunk < bytes) { if (int rc = issue(off + kXferChunk, k ^ 1)) return rc; }
+        HIP_TRY(hipEventSynchronize(c->xfer_ev[k]));
+        std::memcpy(static_cast<uint8_t*>(dst) + off, c->xfer_h[k], (size_t)std::min<uint64_t>(kXferChunk, bytes - off));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return BT_OK;
 }
