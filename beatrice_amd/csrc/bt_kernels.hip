@@ -398,16 +398,19 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
 // a scalar load from the kernel-argument segment and wait for it, once per slot and tile:
 // a memory round trip on the parse's critical path (c2f at 2 blocks/CU: 0.391 ms with
 // the filter evaluated, 0.333 without; tools/gpu_ab_libs_grid.sh).
-constexpr uint32_t kHotSlots = 4;
+#ifndef BT_HOT_SLOTS
+#define BT_HOT_SLOTS 4
+#endif
+constexpr uint32_t kHotSlots = BT_HOT_SLOTS;
 struct HotProgram {
     uint32_t n;
-    DevFilter f[kHotSlots];
+    DevFilter f[kHotSlots ? kHotSlots : 1u];
 };
 __device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
     HotProgram h;
     h.n = prog.n;
 #pragma unroll
-    for (uint32_t k = 0; k < kHotSlots; ++k) h.f[k] = prog.f[k];
+    for (uint32_t k = 0; k < (kHotSlots ? kHotSlots : 1u); ++k) h.f[k] = prog.f[k];
     return h;
 }
 
@@ -445,14 +448,16 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
         // without the early exit's branches (which made one long dependent chain of
         // compares, lane-mask and branch instructions per slot, which two waves per SIMD
         // could not hide), then the first slot that did not pass decides (AND chain order).
-        uint32_t r[kHotSlots];
+        if constexpr (kHotSlots > 0) {
+            uint32_t r[kHotSlots ? kHotSlots : 1u];
 #pragma unroll
-        for (uint32_t f = 0; f < kHotSlots; ++f) r[f] = f < hot.n ? result(hot.f[f]) : 1u;
+            for (uint32_t f = 0; f < kHotSlots; ++f) r[f] = f < hot.n ? result(hot.f[f]) : 1u;
 #pragma unroll
-        for (int f = (int)kHotSlots - 1; f >= 0; --f)
-            if (r[f] != 1u) { code = decide(r[f]); slot = (uint32_t)f; }
-        if (!live) { code = BT_DECIDE_PASS; slot = prog.n ? prog.n - 1u : 0u; }
-        open = live && code == BT_DECIDE_PASS;
+            for (int f = (int)kHotSlots - 1; f >= 0; --f)
+                if (r[f] != 1u) { code = decide(r[f]); slot = (uint32_t)f; }
+            if (!live) { code = BT_DECIDE_PASS; slot = prog.n ? prog.n - 1u : 0u; }
+            open = live && code == BT_DECIDE_PASS;
+        }
         for (uint32_t f = kHotSlots; f < prog.n; ++f) {   // longer programs: the rest from memory
             if (__ballot(open) == 0ull) break;
             const uint32_t rf = result(prog.f[f]);
