@@ -521,3 +521,34 @@ def test_staged_host_copies_round_trip(gpu_ctx):
         buf.download(back)
         assert not back.any(), size
         buf.free()
+
+
+@pytest.mark.parametrize("layout", ["tiled", "planes", "aos", "filter_only"])
+def test_fixed_stride_layouts_long_program(layout):
+    """The fixed-stride kernel in every output form (its late-issue variant serves tiled,
+    plane-major and filter-only, AoS keeps the plain order) with a 6-slot program, so slots
+    0-3 run from registers side by side and slots 4-5 from the slot-by-slot loop, each
+    deciding for some packets; bit-exact against the oracle."""
+    n = 20037
+    data, _ = synth.capture(synth.C2, n, seed=0x51D)
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 9},
+               {"type": abi.BPF, "expr": "udp tcp", "priority": 8},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 7},
+               {"type": abi.PORT_RANGE, "expr": "0-65535", "priority": 6},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/9", "priority": 5},
+               {"type": abi.PORT_RANGE, "expr": "1000-30000", "priority": 4}]
+    flags = {"tiled": 0, "planes": abi.OPT_RECORDS_PLANES, "aos": abi.OPT_RECORDS_AOS, "filter_only": 0}[layout]
+    ctx = abi.Context(0, flags=flags)
+    try:
+        ctx.compile(filters)
+        out = run_dev(ctx, data, None, n, stride=64, records=layout != "filter_only")
+    finally:
+        ctx.close()
+    rec, dec, npass = ol.oracle_run(data, None, n, filters, stride=64)
+    slots = dec & 0x3F
+    assert (slots[(dec >> 6) == 1] >= 4).any(), "no packet decided by a slot past the hot ones"
+    if layout != "filter_only":
+        assert np.array_equal(out["records"], rec)
+    assert np.array_equal(out["decide"], dec)
+    assert out["n_pass"] == npass
+    check_filter_outputs(out, n)
