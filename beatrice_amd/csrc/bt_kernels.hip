@@ -916,6 +916,17 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 // shuffles per round-A instruction. DW = descriptor words (1 bt_pkt_desc, 2 xdp_desc), a
 // template argument so that no register is written on one format's path and loaded on
 // the other's.
+// Cache policy of the descriptor loads (buffer-load aux bits; 2 = nt). A lane's own
+// descriptor load keeps the default policy and the four round-A loads, which re-read the
+// lines it brings in, are non-temporal: C3 kernel 0.470-0.474 against 0.475-0.488 ms on
+// one box, 0.5 % on another, C4 level; both non-temporal made C3 0.504-0.508
+// (profiles/r02/ab/desc_policy.txt).
+#ifndef BT_DESC_AUX
+#define BT_DESC_AUX 0
+#endif
+#ifndef BT_DESC_AUX_Q
+#define BT_DESC_AUX_Q 2
+#endif
 template <int DW>
 struct TileDesc {
     uint32_t me[DW + 1];
@@ -931,20 +942,20 @@ __device__ __forceinline__ void load_desc_pipe(const MainArgs& a, uint32_t t, bo
     const uint32_t qoff = (lane >> 2) * 8u * DW;
     if constexpr (DW == 1) {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, 0);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, BT_DESC_AUX);
         d.me[0] = v.x; d.me[1] = v.y;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(qoff + j * 128u), 0, 0);
+            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(qoff + j * 128u), 0, BT_DESC_AUX_Q);
             d.q[j][0] = w.x; d.q[j][1] = w.y;
         }
     } else {
         typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(lane * 16u), 0, 0);
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(lane * 16u), 0, BT_DESC_AUX);
         d.me[0] = v.x; d.me[1] = v.y; d.me[2] = v.z;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-            const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(qoff + j * 256u), 0, 0);
+            const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(qoff + j * 256u), 0, BT_DESC_AUX_Q);
             d.q[j][0] = w.x; d.q[j][1] = w.y; d.q[j][2] = w.z;
         }
     }
