@@ -166,7 +166,9 @@ def test_r02_default_line_timing_form():
         assert t["main_ms"] == -1, k   # no kernel events in the timed pass
         kp = t["kernel_pass"]
         assert kp["main_ms"] == pytest.approx(r["kernel_ms"], abs=1e-3), k
-        assert kp["main_ms"] <= e["ms_per_step"], k
+        # the kernel time comes from a second pass of the same steps: it may exceed the timed
+        # pass's step by that pass-to-pass noise (C4: 0.9073 against 0.9072 ms), not more
+        assert kp["main_ms"] <= 1.005 * e["ms_per_step"], k
         assert e["ms_per_step"] <= 1.04 * kp["ms_per_step"], k
         if k != "c1":
             assert t["pipelined"] == (k != "c2") and t["output_sets"] == (1 if k == "c2" else 2), k
