@@ -237,6 +237,9 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
 
 }  // namespace
 
+#ifndef BT_EX_BLOCKS_PER_CU
+#define BT_EX_BLOCKS_PER_CU 4   // grid cap (blocks per CU), a build knob for A/B
+#endif
 int launch_extract(const ExArgs& a, const ExTable& tab_in, void* stream, void* timing_start, void* timing_stop) {
     if (a.ntiles == 0) return BT_OK;
     ExTable tab = tab_in;
@@ -271,11 +274,13 @@ int launch_extract(const ExArgs& a, const ExTable& tab_in, void* stream, void* t
         }
         per_cu = it->second;
     }
-    // At most 5 blocks (20 waves) per CU: with parser_example's table the residency is 8,
+    // With the non-temporal policy, at most 4 blocks (16 waves) per CU: c1 0.333-0.355 ms
+    // against 0.351-0.360 at 5 and 0.380-0.385 at 3 (profiles/r02/ab/extract_policy.txt).
+    // Before it, at most 5: with parser_example's table the residency is 8,
     // and fewer concurrent read/write streams suit HBM better (c1, 16M packets: 0.432 ms
     // at 8 blocks/CU, 0.383-0.393 at 4, 0.383-0.385 at 5, 0.387-0.389 at 6, 0.425-0.437
     // at 3, 0.529-0.541 at 2; alternating processes, profiles/r02/ab/c1_grid.txt).
-    per_cu = std::min(per_cu, 5);
+    per_cu = std::min(per_cu, BT_EX_BLOCKS_PER_CU);
     const uint32_t needed = (a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = std::min<uint32_t>(needed, (uint32_t)(cus * per_cu));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
