@@ -141,11 +141,12 @@ class Tpv3Ring(ctypes.Structure):
 
 
 EXPORTS = [
-    "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_filter_compile",
+    "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_context_device",
+    "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter_device_async",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
-    "bt_synchronize", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
+    "bt_synchronize", "bt_stream_create", "bt_stream_synchronize", "bt_stream_destroy", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
@@ -170,6 +171,7 @@ def lib() -> ctypes.CDLL:
         "bt_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Opts), ctypes.POINTER(vp)]),
         "bt_destroy": (None, [vp]),
         "bt_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "bt_context_device": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, u32]),
         "bt_filter_compile": (ctypes.c_int, [vp, ctypes.POINTER(FilterDesc), u32]),
         "bt_filter_program": (ctypes.c_int, [vp, ctypes.POINTER(FilterSlot), u32, ctypes.POINTER(u32)]),
         "bt_filter_compile_host": (ctypes.c_int, [ctypes.POINTER(FilterDesc), u32, ctypes.POINTER(FilterSlot),
@@ -188,6 +190,9 @@ def lib() -> ctypes.CDLL:
         "bt_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, u64]),
         "bt_memset_d": (ctypes.c_int, [vp, vp, ctypes.c_int, u64]),
         "bt_synchronize": (ctypes.c_int, [vp]),
+        "bt_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        "bt_stream_synchronize": (ctypes.c_int, [vp, vp]),
+        "bt_stream_destroy": (ctypes.c_int, [vp, vp]),
         "bt_time_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "bt_time_device_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs), u32,
@@ -300,15 +305,20 @@ class DeviceBuffer:
         _check(lib().bt_memset_d(self.ctx.h, self.ptr, 0, self.nbytes))
 
     def free(self):
+        """hipFree waits for the device, so an asynchronous kernel fault is reported here:
+        raise it (a swallowed fault resurfaces at some later, unrelated call)."""
         if self.ptr:
-            lib().bt_dev_free(self.ctx.h, self.ptr)
-            self.ptr = None
+            if not self.ctx.h:
+                raise BtError(1, "DeviceBuffer.free after its context was closed")
+            p, self.ptr = self.ptr, None
+            _check(lib().bt_dev_free(self.ctx.h, p))
 
     def __del__(self):
         try:
             self.free()
-        except Exception:
-            pass
+        except Exception as e:   # cannot raise from a finaliser: say so loudly
+            import sys
+            print(f"beatrice_amd.abi: DeviceBuffer finaliser: {e}", file=sys.stderr, flush=True)
 
 
 class Context:
@@ -338,6 +348,13 @@ class Context:
         except Exception:
             pass
 
+    def device_id(self) -> tuple[int, str]:
+        """(HIP ordinal, PCI bus id) of the context's device (bt_context_device)."""
+        d = ctypes.c_int(-1)
+        bus = ctypes.create_string_buffer(64)
+        _check(lib().bt_context_device(self.h, ctypes.byref(d), bus, 64))
+        return d.value, bus.value.decode(errors="replace")
+
     def compile(self, filters):
         arr = filter_descs(filters)
         _check(lib().bt_filter_compile(self.h, arr, len(filters)))
@@ -366,6 +383,18 @@ class Context:
 
     def synchronize(self):
         _check(lib().bt_synchronize(self.h))
+
+    def stream_create(self) -> int:
+        """A caller-owned hipStream_t on the context's device (bt_stream_create)."""
+        p = ctypes.c_void_p(0)
+        _check(lib().bt_stream_create(self.h, ctypes.byref(p)))
+        return p.value
+
+    def stream_synchronize(self, stream: int):
+        _check(lib().bt_stream_synchronize(self.h, stream))
+
+    def stream_destroy(self, stream: int):
+        _check(lib().bt_stream_destroy(self.h, stream))
 
     def run_device(self, batch: Batch, outs: Outputs, stream=None):
         _check(lib().bt_parse_filter_device(self.h, ctypes.byref(batch), ctypes.byref(outs), stream))

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "beatrice_gpu.h"
+#include "bt_bounds.h"
 
 namespace bt {
 
@@ -37,7 +38,7 @@ struct MainArgs {
     const uint8_t* base;
     const uint64_t* desc;      // nullptr: fixed stride
     uint32_t desc_words;       // descriptor stride in u64 words: 1 packed, 2 xdp_desc
-    uint64_t bytes;            // readable size of base (rounded up to 16 by the caller)
+    uint64_t bytes;            // read limit from base: round_up(base + bytes, 16) - base (read_limit)
     uint32_t stride;
     uint32_t n;
     uint32_t ntiles;           // ceil(n / 64): one wavefront tile = 64 packets
@@ -70,11 +71,26 @@ enum RecLayout { kRecNone = 0, kRecPlanes = 1, kRecAoS = 2, kRecTiled = 3 };
 int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool filter,
                 int grid_blocks, bool prefetch, void* stream, void* timing_start = nullptr,
                 void* timing_stop = nullptr);
-// The ordered compaction: pass_idx = the indices of the set verdict bits, ascending;
-// n_pass = their count. chunk_sums: ceil(ntiles / kChunkTiles) words of workspace.
-int launch_compact(const uint64_t* verdict, uint32_t ntiles, uint32_t* chunk_sums, uint32_t* pass_idx,
+// The ordered compaction of an n-packet batch: pass_idx = the indices of the set verdict
+// bits, ascending; n_pass = their count. chunk_sums: ceil(ceil(n / 64) / kChunkTiles) words
+// of workspace.
+int launch_compact(const uint64_t* verdict, uint32_t n, uint32_t* chunk_sums, uint32_t* pass_idx,
                    uint32_t* n_pass, void* stream);
 int device_grid_blocks(int device);
+
+// The limit the kernels' 16-B chunk reads are checked against: chunks sit at 16-B offsets
+// from base, and a chunk may pass the buffer's last byte, but never the end of the
+// 16-B-aligned (absolute address) granule that holds it, so never another page.
+inline uint64_t read_limit(const void* base, uint64_t bytes) {
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    return bytes ? ((b + bytes + 15u) & ~15ull) - b : 0u;
+}
+
+// BT_DEBUG_BOUNDS builds (bt_bounds.h): wait for `stream`, then read and clear the
+// module's log; returns the number of failed checks since the last call (*first = the
+// first one). Release builds return 0 without touching the device.
+uint32_t bounds_take_main(void* stream, BoundsLog* first);
+uint32_t bounds_take_extract(void* stream, BoundsLog* first);
 
 // ---- user-defined protocol extraction (bt_extract.hip) ----
 constexpr uint32_t kExWindow = 256;   // bytes of each packet staged in LDS; fields past it read memory
@@ -94,7 +110,7 @@ struct ExArgs {
     const uint8_t* base;
     const uint64_t* desc;             // nullptr: fixed stride
     uint32_t desc_words;
-    uint64_t bytes;                   // readable size of base (rounded up to 16)
+    uint64_t bytes;                   // read limit from base (read_limit)
     uint32_t stride, n, ntiles;
     uint8_t* status;
     uint64_t* values;

@@ -32,6 +32,10 @@
 #include "bt_device.h"
 
 namespace bt {
+
+// BT_DEBUG_BOUNDS: this module's log of failed bounds checks (bt_bounds.h)
+__device__ BoundsLog g_bounds_extract;
+
 namespace {
 
 // Header loads and the value / image stores are non-temporal: nothing re-reads them, and
@@ -46,10 +50,12 @@ template <class T>
 __device__ __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
 
 // Byte b (< span) of the packet in row `rowb` (byte 0 at row byte s), or from memory when
-// past the staged window.
+// past the staged window. `room` = the bytes readable from the frame's start (the batch's
+// bytes minus its offset): a descriptor whose length runs past the buffer reads zeros
+// there, never past it.
 __device__ __forceinline__ uint32_t byte_at(const uint8_t* rowb, uint32_t s, uint32_t b, uint32_t window,
-                                            const uint8_t* frame) {
-    return b < window ? (uint32_t)rowb[s + b] : (uint32_t)frame[b];
+                                            const uint8_t* frame, uint64_t room) {
+    return b < window ? (uint32_t)rowb[s + b] : b < room ? (uint32_t)frame[b] : 0u;
 }
 
 // The 4 bytes at row byte x (any alignment), low byte first.
@@ -65,13 +71,13 @@ __device__ __forceinline__ uint32_t type_bits(uint32_t type) {
 
 // extractValue<T> (src/parser/ProtocolParser.cpp:385-433) for one field of one packet.
 __device__ __forceinline__ uint64_t decode_field(const ExField& f, const uint32_t* row, uint32_t s, uint32_t window,
-                                                 const uint8_t* frame) {
+                                                 const uint8_t* frame, uint64_t room) {
     const uint8_t* rowb = reinterpret_cast<const uint8_t*>(row);
     const uint32_t type = f.ctl & 0xFFu;   // every test on the table below is wave-uniform
     const bool le = ((f.ctl >> 8) & 0xFFu) == BT_ENDIAN_LITTLE;
     const uint32_t o = f.offset, L = f.length;
     switch (type) {
-    case BT_FT_BOOLEAN: return byte_at(rowb, s, o, window, frame) != 0u ? 1u : 0u;   // fieldData[0] != 0
+    case BT_FT_BOOLEAN: return byte_at(rowb, s, o, window, frame, room) != 0u ? 1u : 0u;   // fieldData[0] != 0
     case BT_FT_BYTES: case BT_FT_STRING: case BT_FT_MAC: case BT_FT_IPV4: case BT_FT_IPV6: case BT_FT_CUSTOM:
         return 0;   // the bytes themselves (image)
     default: break;
@@ -95,7 +101,7 @@ __device__ __forceinline__ uint64_t decode_field(const ExField& f, const uint32_
     for (uint32_t i = 0; i < L; ++i) {
         const uint32_t sh = (8u * i) & m;
         if (sh >= w) continue;   // lands past the type's width: cut anyway
-        const uint64_t b = byte_at(rowb, s, o + (le ? i : L - 1u - i), window, frame);
+        const uint64_t b = byte_at(rowb, s, o + (le ? i : L - 1u - i), window, frame, room);
         v |= b << sh;
     }
     return w == 64u ? v : (v & ((1ull << w) - 1ull));
@@ -162,7 +168,8 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
                 const uint32_t qe = (uint32_t)__shfl((int)((uint32_t)off & 15u) + (int)wl, (int)q);   // s + wl of q
                 const uint32_t c = 4u * g + (lane & 3u);
                 const uint64_t addr = (qo & ~15ull) + 16ull * c;
-                const bool want = 16u * c < qe && addr + 16ull <= a.bytes;
+                const bool want = 16u * c < qe && addr + 16ull <= a.bytes &&
+                                  BT_IN(&g_bounds_extract, kSiteExLoad, addr + 15u, a.bytes);
                 v[j] = want ? ld16_nt(a.base + addr) : make_uint4(0, 0, 0, 0);
                 dst[j] = q * row_dw + 4u * c;
                 keep[j] = want;   // 16 c < s + wl <= 15 + window: inside the row
@@ -182,13 +189,16 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
 
         // ---- DECODE: one u64 per numeric field per packet, field-major ----
         const uint8_t* frame = a.base + off;
+        const uint64_t room = off < a.bytes ? a.bytes - off : 0u;
         if (a.values && live) {
             for (uint32_t f = 0; f < tab.n; ++f) {
-                const uint64_t v = ok ? decode_field(tab.f[f], row, s, window, frame) : 0ull;
-                st_nt(a.values + (uint64_t)f * a.n_cap + my, v);
+                const uint64_t v = ok ? decode_field(tab.f[f], row, s, window, frame, room) : 0ull;
+                if (BT_IN(&g_bounds_extract, kSiteExValue, (uint64_t)f * a.n_cap + my, (uint64_t)tab.n * a.n_cap))
+                    st_nt(a.values + (uint64_t)f * a.n_cap + my, v);
             }
         }
-        if (a.status && live) a.status[my] = ok ? 0u : 9u;   // ParseStatus SUCCESS / PACKET_TOO_SHORT
+        if (a.status && live && BT_IN(&g_bounds_extract, kSiteExStatus, my, a.n))
+            a.status[my] = ok ? 0u : 9u;   // ParseStatus SUCCESS / PACKET_TOO_SHORT
 
         // ---- IMAGE: the tile's packets' [0, span) bytes as one contiguous region ----
         if (a.image && span) {
@@ -214,7 +224,8 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
                         const uint32_t nx = (mn & 0x100u) ? row_word(img + (j + 1u) * row_dw, mn & 15u) : 0u;
                         word = (word & ((1u << (8u * k)) - 1u)) | (nx << (8u * k));
                     }
-                    st_nt(reinterpret_cast<uint32_t*>(out + q), word);
+                    if (BT_IN(&g_bounds_extract, kSiteExImage, (uint64_t)p0 * span + q + 3u, (uint64_t)a.n * span))
+                        st_nt(reinterpret_cast<uint32_t*>(out + q), word);
                 }
                 q0 = nd * 4u;
             }
@@ -225,8 +236,10 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
                 const uint32_t m = meta[j];
                 uint32_t val = 0;
                 if (m & 0x100u)
-                    val = b < window ? (uint32_t)rows8[4u * j * row_dw + (m & 15u) + b] : (uint32_t)a.base[offs[j] + b];
-                out[q] = (uint8_t)val;
+                    val = b < window ? (uint32_t)rows8[4u * j * row_dw + (m & 15u) + b]
+                        : offs[j] + b < a.bytes ? (uint32_t)a.base[offs[j] + b] : 0u;
+                if (BT_IN(&g_bounds_extract, kSiteExImage, (uint64_t)p0 * span + q, (uint64_t)a.n * span))
+                    out[q] = (uint8_t)val;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -236,6 +249,24 @@ __global__ __launch_bounds__(kBlock) void bt_extract_tile(ExArgs a, ExTable tab)
 }
 
 }  // namespace
+
+uint32_t bounds_take_extract(void* stream, BoundsLog* first) {
+#ifdef BT_DEBUG_BOUNDS
+    if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) != hipSuccess) return 0;
+    BoundsLog log{};
+    if (hipMemcpyFromSymbol(&log, HIP_SYMBOL(g_bounds_extract), sizeof(log)) != hipSuccess) return 0;
+    if (log.count) {
+        const BoundsLog zero{};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bounds_extract), &zero, sizeof(zero));
+        if (first) *first = log;
+    }
+    return log.count;
+#else
+    (void)stream;
+    (void)first;
+    return 0;
+#endif
+}
 
 #ifndef BT_EX_BLOCKS_PER_CU
 #define BT_EX_BLOCKS_PER_CU 4   // grid cap (blocks per CU), a build knob for A/B

@@ -35,6 +35,10 @@
 #include "bt_device.h"
 
 namespace bt {
+
+// BT_DEBUG_BOUNDS: this module's log of failed bounds checks (bt_bounds.h)
+__device__ BoundsLog g_bounds_main;
+
 namespace {
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) {
@@ -535,7 +539,8 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
 #pragma unroll
         for (uint32_t j = 0; j < cpp; ++j) {
             const uint32_t g = j * 64u + lane;
-            const bool ok = p0 + (g >> kL) < a.n;
+            const bool ok = p0 + (g >> kL) < a.n &&
+                            BT_IN(&g_bounds_main, kSiteFixedLoad, (uint64_t)p0 * a.stride + g * 16u + 15u, a.bytes);
             if (LATE)
                 st.v[j] = ld16(ok ? span + (uint64_t)g * 16u : reinterpret_cast<const uint8_t*>(g_zero16), true);
             else
@@ -728,7 +733,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     const uint32_t* row = img + lane * kRow;
     if (FILTER == 2 && a.dfa_bytes) {   // uniform: the whole block copies the pool once
         const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
-        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u && BT_IN(&g_bounds_main, kSitePayload, 16u * k, kDfaPoolMax); k += kBlock)
+            dyn_lds[k] = src[k];
         __syncthreads();
     }
     const uint8_t* dfa_lds = reinterpret_cast<const uint8_t*>(dyn_lds);
@@ -815,11 +821,12 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                     // last one of each region.
                     uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
                     const uint64_t below = (1ull << lane) - 1ull;
+                    const bool rec_in = BT_IN(&g_bounds_main, kSiteRecord, t, (a.n_cap + 63u) / 64u);
 #pragma unroll
                     for (uint32_t k = 0; k < BT_REC_SLABS; ++k) {
                         const uint64_t mk = __ballot(k < ns);
                         if (mk == 0ull) break;   // ns only falls: no lane needs a later slab
-                        if (k < ns)
+                        if (k < ns && rec_in)
                             st16(tile + k * 64 + (k < 2u ? lane : (uint32_t)__popcll(mk & below)),
                                  make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
                     }
@@ -829,7 +836,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                     uint4* dst = reinterpret_cast<uint4*>(a.records) + (uint64_t)my;
 #pragma unroll
                     for (uint32_t k = 0; k < BT_REC_SLABS; ++k)
-                        if (k < 2u || __ballot(k < ns) != 0ull)
+                        if ((k < 2u || __ballot(k < ns) != 0ull) && BT_IN(&g_bounds_main, kSiteRecord, my, a.n_cap))
                             st16(dst + (uint64_t)k * a.n_cap,
                                  make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]), a.nt & 1u);
                 }
@@ -847,8 +854,10 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             // the last tile's unused slots: a zero slab 1 reads as a 2-slab record, so a
             // reader can rebuild the slab-k packing of the tile without knowing n
             uint4* tile = reinterpret_cast<uint4*>(a.records) + (uint64_t)t * (BT_REC_SLABS * 64);
-            st16(tile + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
-            st16(tile + 64 + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
+            if (BT_IN(&g_bounds_main, kSiteRecord, t, (a.n_cap + 63u) / 64u)) {
+                st16(tile + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
+                st16(tile + 64 + lane, make_uint4(0, 0, 0, 0), a.nt & 1u);
+            }
         }
 
         if (LATE && t + step < t_end) issue_loads<FIXED_LOG2, LATE>(a, t + step, lane, st, wide, need_max);
@@ -861,13 +870,15 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
                 const uint32_t cnt = min(64u, a.n - p0);
                 const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
-                const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict ? 8u : 0u);
+                const bool v_in = BT_IN(&g_bounds_main, kSiteVerdict, t, a.ntiles);
+                const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict && v_in ? 8u : 0u);
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
             } else {
-                if (a.decide && live) a.decide[my] = (uint8_t)((code << 6) | slot);
-                if (lane == 0 && a.verdict) a.verdict[t] = pass;   // also the compaction's input
+                if (a.decide && live && BT_IN(&g_bounds_main, kSiteDecide, my, a.n)) a.decide[my] = (uint8_t)((code << 6) | slot);
+                if (lane == 0 && a.verdict && BT_IN(&g_bounds_main, kSiteVerdict, t, a.ntiles))
+                    a.verdict[t] = pass;   // also the compaction's input
             }
         }
         // ---- 4. AoS records: the tile's 64 bt_rec are one contiguous 6-KiB range. Each
@@ -887,7 +898,9 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
 #pragma unroll
             for (uint32_t i = 0; i < BT_REC_SLABS; ++i) {
                 const uint32_t q = i * 64u + lane;
-                if (q < q_end) st16(dst + q, lrec[q], a.nt & 1u);
+                if (q < q_end && BT_IN(&g_bounds_main, kSiteRecord, (uint64_t)p0 * BT_REC_SLABS + q,
+                                       (uint64_t)a.n_cap * BT_REC_SLABS))
+                    st16(dst + q, lrec[q], a.nt & 1u);
             }
         }
         wave_lds_sync();   // the next tile overwrites this wave's image
@@ -1041,7 +1054,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     const uint32_t* row = img + lane * kRow;
     if (FILTER == 2 && a.dfa_bytes) {
         const uint4* src = reinterpret_cast<const uint4*>(a.dfa);
-        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u; k += kBlock) dyn_lds[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < (a.dfa_bytes + 15u) / 16u && BT_IN(&g_bounds_main, kSitePayload, 16u * k, kDfaPoolMax); k += kBlock)
+            dyn_lds[k] = src[k];
         __syncthreads();
     }
     const uint8_t* dfa_lds = reinterpret_cast<const uint8_t*>(dyn_lds);
@@ -1104,7 +1118,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
 #pragma unroll
                 for (int k = 0; k < 8; ++k) p.r[k] = 0u;
             }
-            const auto r = rsrc_of(a.records + (uint64_t)t * (BT_REC_SLABS * 64 * 16), BT_REC_SLABS * 64 * 16);
+            const bool rec_in = BT_IN(&g_bounds_main, kSiteRecord, t, (a.n_cap + 63u) / 64u);
+            const auto r = rsrc_of(a.records + (uint64_t)t * (BT_REC_SLABS * 64 * 16), rec_in ? BT_REC_SLABS * 64 * 16 : 0u);
             const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
             for (uint32_t k = 0; k < BT_REC_SLABS; ++k) {
@@ -1123,7 +1138,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
-            const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict ? 8u : 0u);
+            const bool v_in = BT_IN(&g_bounds_main, kSiteVerdict, t, a.ntiles);
+            const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict && v_in ? 8u : 0u);
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
             __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
@@ -1141,7 +1157,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
 // K2: chunk_sums[c] = the passing packets of chunk c (kChunkTiles = 256 tiles, one per
 // thread): the popcounts of the tiles' verdict words.
 __global__ __launch_bounds__(256) void bt_chunk_sums(const uint64_t* verdict, uint32_t ntiles,
-                                                     uint32_t* chunk_sums) {
+                                                     uint32_t* chunk_sums, uint32_t nchunks) {
     static_assert(kChunkTiles == 256, "one tile per thread");
     __shared__ uint32_t red[4];
     const uint32_t t = blockIdx.x * kChunkTiles + threadIdx.x;
@@ -1149,7 +1165,8 @@ __global__ __launch_bounds__(256) void bt_chunk_sums(const uint64_t* verdict, ui
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) chunk_sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0 && BT_IN(&g_bounds_main, kSiteChunkSums, blockIdx.x, nchunks))
+        chunk_sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // K3: block c scans its chunk's 256 tile counts, adds the prefix of earlier chunks and
@@ -1161,7 +1178,7 @@ __global__ __launch_bounds__(256) void bt_chunk_sums(const uint64_t* verdict, ui
 // (The first version had 1024-tile chunks, i.e. 256 blocks = one per CU, and a
 // strided one-tile loop: 34 us on C3.)
 __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const uint32_t* chunk_sums,
-                                                  uint32_t nchunks, uint32_t ntiles, uint32_t* pass_idx,
+                                                  uint32_t nchunks, uint32_t ntiles, uint32_t n, uint32_t* pass_idx,
                                                   uint32_t* n_pass) {
     __shared__ uint32_t tile_off[kChunkTiles];
     __shared__ uint64_t words[kChunkTiles];
@@ -1210,7 +1227,8 @@ __global__ __launch_bounds__(256) void bt_compact(const uint64_t* verdict, const
         for (uint32_t k = 0; k < 4u; ++k) { w4[k] = words[first + i + k]; o4[k] = tile_off[first + i + k]; }
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k)
-            if ((w4[k] >> lane) & 1ull)
+            if (((w4[k] >> lane) & 1ull) &&
+                BT_IN(&g_bounds_main, kSitePassIdx, o4[k] + (uint32_t)__popcll(w4[k] & below_mask), n))
                 pass_idx[o4[k] + (uint32_t)__popcll(w4[k] & below_mask)] = (c * kChunkTiles + first + i + k) * 64u + lane;
     }
 }
@@ -1360,15 +1378,34 @@ int launch_main(const MainArgs& a, const DevProgram& prog, int rec_layout, bool 
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
 }
 
-int launch_compact(const uint64_t* verdict, uint32_t ntiles, uint32_t* chunk_sums, uint32_t* pass_idx,
+int launch_compact(const uint64_t* verdict, uint32_t n, uint32_t* chunk_sums, uint32_t* pass_idx,
                    uint32_t* n_pass, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t ntiles = (n + 63u) / 64u;
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     if (nchunks == 0) return BT_OK;
-    hipLaunchKernelGGL(bt_chunk_sums, dim3(nchunks), dim3(256), 0, st, verdict, ntiles, chunk_sums);
-    hipLaunchKernelGGL(bt_compact, dim3(nchunks), dim3(256), 0, st, verdict, chunk_sums, nchunks, ntiles, pass_idx,
+    hipLaunchKernelGGL(bt_chunk_sums, dim3(nchunks), dim3(256), 0, st, verdict, ntiles, chunk_sums, nchunks);
+    hipLaunchKernelGGL(bt_compact, dim3(nchunks), dim3(256), 0, st, verdict, chunk_sums, nchunks, ntiles, n, pass_idx,
                        n_pass);
     return hipGetLastError() == hipSuccess ? BT_OK : BT_E_INTERNAL;
+}
+
+uint32_t bounds_take_main(void* stream, BoundsLog* first) {
+#ifdef BT_DEBUG_BOUNDS
+    if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) != hipSuccess) return 0;
+    BoundsLog log{};
+    if (hipMemcpyFromSymbol(&log, HIP_SYMBOL(g_bounds_main), sizeof(log)) != hipSuccess) return 0;
+    if (log.count) {
+        const BoundsLog zero{};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bounds_main), &zero, sizeof(zero));
+        if (first) *first = log;
+    }
+    return log.count;
+#else
+    (void)stream;
+    (void)first;
+    return 0;
+#endif
 }
 
 int device_grid_blocks(int device) {

@@ -137,22 +137,28 @@ struct bt_ctx {
     DevProgram prog{};
     std::vector<uint8_t> dfa_pool;     // BT_K_PAYLOAD tables of the current program
     // PAYLOAD DFA pools, double-buffered: a recompile writes the buffer no queued launch
-    // uses (dfa_ev[k] is recorded after every launch that reads dfa_dev[k])
+    // uses. Every stream that launched a kernel reading dfa_dev[k] has its own event in
+    // dfa_readers[k], recorded right after that launch; a recompile that reuses buffer k
+    // waits for all of them (a single event would only cover the last stream).
     uint8_t* dfa_dev[2] = {nullptr, nullptr};
-    hipEvent_t dfa_ev[2] = {nullptr, nullptr};
-    bool dfa_used[2] = {false, false};
+    std::vector<std::pair<hipStream_t, hipEvent_t>> dfa_readers[2];
+    std::vector<hipEvent_t> dfa_spare;   // events of cleared reader lists, reused
     int dfa_cur = 0;
 
     // device workspace of the compaction: chunk sums, and the verdict words when the
-    // caller asks for none. Double-buffered (consecutive calls alternate). `stream` = the
-    // last stream that queued work touching the buffer; before another stream touches
-    // it, an event recorded at that stream's tail makes the new one wait (stream
-    // switches only: calls that stay on their streams queue no extra packets).
+    // caller asks for none. Double-buffered (consecutive calls alternate). `last` = the
+    // last stream that queued work touching the buffer (compared, never used, unless the
+    // context owns it); before another stream touches it, that stream waits for `sync`:
+    // recorded right after the work when `last` is a caller's stream (which may be
+    // destroyed before the next touch), or at the switch when it is one of the context's
+    // own streams (which live as long as the context). Calls that stay on the context's
+    // streams queue no extra packets.
     uint32_t ws_cap = 0;
     struct Ws {
         uint32_t* chunk_sums = nullptr;
         uint64_t* verdict = nullptr;
-        hipStream_t stream = nullptr;
+        hipStream_t last = nullptr;
+        bool lazy = false;             // sync not recorded yet (last is a context stream)
         hipEvent_t sync = nullptr;
     } ws[2];
     int ws_next = 0;
@@ -174,6 +180,7 @@ struct bt_ctx {
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t pipe_done = nullptr;    // BT_OPT_PIPELINE: the last step's compaction
+    hipEvent_t pipe_step = nullptr;    // pipelined with one output set: each step's compaction
     std::vector<hipEvent_t> tev;
     // bt_time_device: K steps captured once into one hipGraph, replayed per call
     hipGraphExec_t tgraph = nullptr;
@@ -188,6 +195,7 @@ struct bt_ctx {
     std::mutex xfer_mu;
     uint8_t* xfer_h[2] = {nullptr, nullptr};
     hipEvent_t xfer_ev[2] = {nullptr, nullptr};
+    hipEvent_t xfer_after = nullptr;   // the compaction stream's tail (after_cstream)
 
     // bt_extract (host lists): pinned + device staging, grown on demand
     uint8_t* ex_h = nullptr;
@@ -234,7 +242,7 @@ void free_ws(bt_ctx* c) {
     for (auto& w : c->ws) {
         if (w.chunk_sums) (void)hipFree(w.chunk_sums);
         if (w.verdict) (void)hipFree(w.verdict);
-        w.chunk_sums = nullptr; w.verdict = nullptr; w.stream = nullptr;
+        w.chunk_sums = nullptr; w.verdict = nullptr; w.last = nullptr; w.lazy = false;
     }
     c->ws_cap = 0;
 }
@@ -259,18 +267,24 @@ int ensure_ws(bt_ctx* c, uint32_t n) {
     return BT_OK;
 }
 
+bool ctx_stream(const bt_ctx* c, hipStream_t s) { return s == c->stream || (c->cstream && s == c->cstream); }
+
 // `s` is about to queue work that touches workspace buffer w: if another stream did last,
-// s waits for everything that stream has queued so far.
-int ws_touch(bt_ctx::Ws* w, hipStream_t s) {
-    if (w->stream && w->stream != s) {
-        if (hipEventRecord(w->sync, w->stream) == hipSuccess) {
-            HIP_TRY(hipStreamWaitEvent(s, w->sync, 0));
-        } else {   // that stream is gone (destroyed by its owner): wait for the whole device
-            (void)hipGetLastError();
-            HIP_TRY(hipDeviceSynchronize());
-        }
+// s waits for everything that stream had queued on w.
+int ws_touch(bt_ctx* c, bt_ctx::Ws* w, hipStream_t s) {
+    if (w->last && w->last != s) {
+        if (w->lazy) HIP_TRY(hipEventRecord(w->sync, w->last));   // a context stream: alive
+        HIP_TRY(hipStreamWaitEvent(s, w->sync, 0));
     }
-    w->stream = s;
+    (void)c;
+    return BT_OK;
+}
+
+// `s` has just queued work touching w.
+int ws_done(bt_ctx* c, bt_ctx::Ws* w, hipStream_t s) {
+    w->last = s;
+    w->lazy = ctx_stream(c, s);
+    if (!w->lazy) HIP_TRY(hipEventRecord(w->sync, s));   // a caller's stream: record now
     return BT_OK;
 }
 
@@ -278,6 +292,31 @@ int ensure_cstream(bt_ctx* c) {
     if (c->cstream) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    return BT_OK;
+}
+
+// BT_DEBUG_BOUNDS builds: after a launch, wait and read the kernels' bounds logs
+// (bt_bounds.h); a failed check becomes BT_E_INTERNAL naming the first one.
+int check_bounds(hipStream_t st, hipStream_t cst, const char* what) {
+#ifdef BT_DEBUG_BOUNDS
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return BT_OK;   // graph capture
+    BoundsLog f{};
+    uint32_t k = bounds_take_main(st, &f);
+    if (!k && cst && cst != st) k = bounds_take_main(cst, &f);
+    if (!k) k = bounds_take_extract(st, &f);
+    if (k) {
+        fprintf(stderr, "BT_DEBUG_BOUNDS: %s: %u failed checks, first %s (site %u) block %u thread %u index %llu "
+                "limit %llu\n", what, k, bounds_site_name(f.site), f.site, f.block, f.lane,
+                (unsigned long long)f.index, (unsigned long long)f.limit);
+        return fail(BT_E_INTERNAL, "BT_DEBUG_BOUNDS: %s: %u failed checks, first %s index %llu limit %llu", what, k,
+                    bounds_site_name(f.site), (unsigned long long)f.index, (unsigned long long)f.limit);
+    }
+#else
+    (void)st;
+    (void)cst;
+    (void)what;
+#endif
     return BT_OK;
 }
 
@@ -309,6 +348,18 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
         c->ws_next ^= 1;
     }
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
+    // The readable range of base is part of the contract: descriptor batches must state it
+    // (a descriptor past it then reads zeros instead of arbitrary memory); fixed-stride
+    // batches default to n * stride.
+    uint64_t bytes = b->bytes;
+    if (b->desc) {
+        if (!bytes) return fail(BT_E_INVALID_ARGUMENT, "descriptor batch with bytes == 0 (the readable size of base)");
+    } else {
+        const uint64_t need = (uint64_t)b->n * b->stride;
+        if (!bytes) bytes = need;
+        else if (bytes < need) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride batch: bytes %llu < n * stride %llu",
+                                           (unsigned long long)bytes, (unsigned long long)need);
+    }
     MainArgs a{};
     a.base = b->base;
     a.desc = static_cast<const uint64_t*>(b->desc);
@@ -317,14 +368,12 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.stride = b->stride;
     a.n = b->n;
     a.ntiles = (b->n + 63) / 64;
-    uint64_t bytes = b->bytes;
-    if (!bytes) bytes = b->desc ? ~0ull : (uint64_t)b->n * b->stride;
-    a.bytes = bytes == ~0ull ? bytes : (bytes + 15) & ~15ull;
+    a.bytes = read_limit(b->base, bytes);
     a.n_cap = o->records ? o->n_cap : 0;
     a.records = reinterpret_cast<uint8_t*>(o->records);
     a.decide = o->decide;
     a.verdict = o->verdict ? o->verdict : (w ? w->verdict : nullptr);
-    if (w && !o->verdict) { int rc = ws_touch(w, st); if (rc) return rc; }   // the main kernel writes w->verdict
+    if (w && !o->verdict) { int rc = ws_touch(c, w, st); if (rc) return rc; }   // the main kernel writes w->verdict
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
     a.dfa = c->dfa_dev[c->dfa_cur];
     a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
@@ -357,20 +406,30 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     }
     int rc = launch_main(a, c->prog, rec, filter, c->grid, !(c->opts.flags & BT_OPT_NO_PREFETCH), st, e0, mend);
     if (rc) return fail(rc, "main kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (w && !o->verdict) { if ((rc = ws_done(c, w, st))) return rc; }
     if (a.dfa_bytes) {   // the pool this launch reads stays untouched until it has run
-        HIP_TRY(hipEventRecord(c->dfa_ev[c->dfa_cur], st));
-        c->dfa_used[c->dfa_cur] = true;
+        auto& rd = c->dfa_readers[c->dfa_cur];
+        auto it = std::find_if(rd.begin(), rd.end(), [st](const auto& x) { return x.first == st; });
+        if (it == rd.end()) {
+            hipEvent_t e = nullptr;
+            if (!c->dfa_spare.empty()) { e = c->dfa_spare.back(); c->dfa_spare.pop_back(); }
+            else HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            rd.emplace_back(st, e);
+            it = rd.end() - 1;
+        }
+        HIP_TRY(hipEventRecord(it->second, st));
     }
     if (compact) {
         if (piped) HIP_TRY(hipStreamWaitEvent(cst, mend, 0));
-        if ((rc = ws_touch(w, cst))) return rc;
-        rc = launch_compact(a.verdict, a.ntiles, w->chunk_sums, o->pass_idx, o->n_pass, cst);
+        if ((rc = ws_touch(c, w, cst))) return rc;
+        rc = launch_compact(a.verdict, b->n, w->chunk_sums, o->pass_idx, o->n_pass, cst);
         if (rc) return fail(rc, "compaction launch failed");
+        if ((rc = ws_done(c, w, cst))) return rc;
         if (done) HIP_TRY(hipEventRecord(done, cst));
     } else if (done) {
         HIP_TRY(hipEventRecord(done, st));
     }
-    return BT_OK;
+    return check_bounds(st, cst, "parse+filter");
 }
 
 void free_host(bt_ctx* c) {
@@ -477,6 +536,16 @@ int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
     return BT_OK;
 }
 
+int bt_context_device(const bt_ctx* c, int* device, char* pci_bus_id, uint32_t cap) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    if (device) *device = c->device;
+    if (pci_bus_id) {
+        if (cap < 16) return fail(BT_E_INVALID_ARGUMENT, "pci_bus_id buffer of %u bytes (need >= 16)", cap);
+        HIP_TRY(hipDeviceGetPCIBusId(pci_bus_id, (int)cap, c->device));
+    }
+    return BT_OK;
+}
+
 void bt_destroy(bt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -492,8 +561,10 @@ void bt_destroy(bt_ctx* c) {
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     for (int k = 0; k < 2; ++k) {
         if (c->dfa_dev[k]) (void)hipFree(c->dfa_dev[k]);
-        if (c->dfa_ev[k]) (void)hipEventDestroy(c->dfa_ev[k]);
+        for (auto& r : c->dfa_readers[k]) (void)hipEventDestroy(r.second);
     }
+    for (auto e : c->dfa_spare) (void)hipEventDestroy(e);
+    if (c->pipe_step) (void)hipEventDestroy(c->pipe_step);
     for (auto e : c->tev) (void)hipEventDestroy(e);
     if (c->pipe_done) (void)hipEventDestroy(c->pipe_done);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -504,6 +575,7 @@ void bt_destroy(bt_ctx* c) {
         if (c->xfer_h[k]) (void)hipHostFree(c->xfer_h[k]);
         if (c->xfer_ev[k]) (void)hipEventDestroy(c->xfer_ev[k]);
     }
+    if (c->xfer_after) (void)hipEventDestroy(c->xfer_after);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -555,13 +627,13 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
         // that still read it (with the old program) are waited for first
         HIP_TRY(hipSetDevice(c->device));
         const int k = c->dfa_cur ^ 1;
-        if (!c->dfa_dev[k]) {
-            HIP_TRY(hipMalloc(&c->dfa_dev[k], kDfaPoolMax));
-            HIP_TRY(hipEventCreateWithFlags(&c->dfa_ev[k], hipEventDisableTiming));
+        if (!c->dfa_dev[k]) HIP_TRY(hipMalloc(&c->dfa_dev[k], kDfaPoolMax));
+        for (auto& r : c->dfa_readers[k]) {   // every stream's last launch that read buffer k
+            HIP_TRY(hipEventSynchronize(r.second));
+            c->dfa_spare.push_back(r.second);
         }
-        if (c->dfa_used[k]) HIP_TRY(hipEventSynchronize(c->dfa_ev[k]));
+        c->dfa_readers[k].clear();
         if (int rc = bt_memcpy_h2d(c, c->dfa_dev[k], pool.data(), pool.size())) return rc;   // staged, synchronous
-        c->dfa_used[k] = false;
         c->dfa_cur = k;
     }
     // a cached BT_OPT_GRAPH timing graph holds the old program: drop it
@@ -707,6 +779,7 @@ int bt_time_device2(bt_ctx* c, const bt_batch* b, const bt_outputs* outs, uint32
     if (piped) {
         if (int rc = ensure_cstream(c)) return rc;
         if (!c->pipe_done) HIP_TRY(hipEventCreateWithFlags(&c->pipe_done, hipEventDisableTiming));
+        if (!c->pipe_step) HIP_TRY(hipEventCreateWithFlags(&c->pipe_step, hipEventDisableTiming));
     }
     const auto h0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -719,11 +792,15 @@ int bt_time_device2(bt_ctx* c, const bt_batch* b, const bt_outputs* outs, uint32
         // (BT_TIME_KERNEL_EVENTS) are recorded by the main kernel's own dispatch; they cost
         // the GPU ~9 us per launch on gfx950 (tools/calib/boundary.hip), so the bench
         // times its steps without them and measures the kernel in a second pass.
+        // With one output set, step i + 1's main kernel would rewrite the verdict words
+        // step i's compaction reads: it waits for that compaction (no overlap, no race).
+        const bool serial = piped && n_out == 1;
         for (uint32_t i = 0; i < iters; ++i) {
             const bt_outputs* oi = outs + (i % n_out);
             hipEvent_t e0 = kev ? c->tev[2 * i] : nullptr, e1 = kev ? c->tev[2 * i + 1] : nullptr;
+            if (serial && i) HIP_TRY(hipStreamWaitEvent(c->stream, c->pipe_step, 0));
             int rc = piped ? run_device(c, b, oi, c->stream, false, e0, e1, c->cstream,
-                                        i + 1 == iters ? c->pipe_done : nullptr)
+                                        i + 1 == iters ? c->pipe_done : serial ? c->pipe_step : nullptr)
                            : run_device(c, b, oi, c->stream, false, e0, e1);
             if (rc) return rc;
         }
@@ -922,7 +999,9 @@ int bt_host_register(bt_ctx* c, void* host, uint64_t bytes, void** dev_alias) {
 int bt_host_unregister(bt_ctx* c, void* host) {
     if (!c || !host) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // every queued kernel that may read or write the range (the context stream, the
+    // compaction stream, callers' streams) has finished before its mapping goes away
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipHostUnregister(host));
     return BT_OK;
 }
@@ -941,18 +1020,28 @@ int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {
 
 int bt_dev_free(bt_ctx* c, void* p) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
-    if (p) HIP_TRY(hipFree(p));
+    if (!p) return BT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipFree(p));   // implicitly waits for the device: no queued kernel still uses p
     return BT_OK;
 }
 
-// Both copies are ordered on the context stream and complete before returning: a
-// pageable hipMemcpy on the null stream may return once the source is staged, and it is
-// not ordered with the context's non-blocking stream.
 }  // extern "C"
 
 namespace {
 
 constexpr size_t kXferChunk = size_t(8) << 20;
+
+// The copies run on the context stream; work queued on the compaction stream
+// (bt_parse_filter_device_async) is waited for first, so a copy issued after an async call
+// sees its pass list. Work on a caller's own stream is the caller's to synchronise.
+int after_cstream(bt_ctx* c) {
+    if (!c->cstream) return BT_OK;
+    if (!c->xfer_after) HIP_TRY(hipEventCreateWithFlags(&c->xfer_after, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->xfer_after, c->cstream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->xfer_after, 0));
+    return BT_OK;
+}
 
 int ensure_xfer(bt_ctx* c) {
     for (int k = 0; k < 2; ++k) {
@@ -967,17 +1056,15 @@ int ensure_xfer(bt_ctx* c) {
 extern "C" {
 
 // Both copies go through the context's two pinned chunks (host memcpy of chunk k while the
-// DMA of chunk k^1 runs): the caller's memory is usually pageable (numpy arrays, vectors),
-// and the runtime's own pageable-copy path pins and maps such ranges behind the caller's
-// back. One GPU-suite run on a fresh box failed in exactly such an upload with "illegal
-// memory access" while every kernel before it had completed and been checked; with
-// staging, no DMA ever touches memory this library did not allocate.
+// DMA of chunk k^1 runs), so no DMA touches the caller's (usually pageable) memory; they
+// are ordered after the context's streams (after_cstream) and complete before returning.
 int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (bytes && (!dst || !src)) return fail(BT_E_INVALID_ARGUMENT, "null pointer");
     std::lock_guard<std::mutex> lk(c->xfer_mu);
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = ensure_xfer(c)) return rc;
+    if (int rc = after_cstream(c)) return rc;
     bool used[2] = {false, false};
     int k = 0;
     for (uint64_t off = 0; off < bytes; off += kXferChunk, k ^= 1) {
@@ -998,6 +1085,7 @@ int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
     std::lock_guard<std::mutex> lk(c->xfer_mu);
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = ensure_xfer(c)) return rc;
+    if (int rc = after_cstream(c)) return rc;
     // chunk i lands in buffer i & 1; chunk i + 1's DMA runs while chunk i is copied out
     auto issue = [&](uint64_t off, int k) -> int {
         const size_t n = (size_t)std::min<uint64_t>(kXferChunk, bytes - off);
@@ -1018,8 +1106,34 @@ int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
 
 int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = after_cstream(c)) return rc;
     HIP_TRY(hipMemsetAsync(dst, value, bytes, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return BT_OK;
+}
+
+int bt_stream_create(bt_ctx* c, void** stream) {
+    if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return BT_OK;
+}
+
+int bt_stream_synchronize(bt_ctx* c, void* stream) {
+    if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return BT_OK;
+}
+
+int bt_stream_destroy(bt_ctx* c, void* stream) {
+    if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
     return BT_OK;
 }
 
@@ -1075,6 +1189,15 @@ int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, cons
     if (o->values && o->n_cap < b->n) return fail(BT_E_INVALID_ARGUMENT, "values n_cap %u < n %u", o->n_cap, b->n);
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
     if (!b->n) return BT_OK;
+    uint64_t bytes = b->bytes;   // as run_device: mandatory with descriptors
+    if (b->desc) {
+        if (!bytes) return fail(BT_E_INVALID_ARGUMENT, "descriptor batch with bytes == 0 (the readable size of base)");
+    } else {
+        const uint64_t need = (uint64_t)b->n * b->stride;
+        if (!bytes) bytes = need;
+        else if (bytes < need) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride batch: bytes %llu < n * stride %llu",
+                                           (unsigned long long)bytes, (unsigned long long)need);
+    }
     if (never) {   // no frame reaches the span: every packet PACKET_TOO_SHORT, no field
         if (o->status) HIP_TRY(hipMemsetAsync(o->status, 9, b->n, st));
         if (o->values) for (uint32_t k = 0; k < t.n; ++k)
@@ -1085,9 +1208,7 @@ int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, cons
     a.base = b->base;
     a.desc = static_cast<const uint64_t*>(b->desc);
     a.desc_words = b->desc_format == BT_DESC_XDP ? 2u : 1u;
-    uint64_t bytes = b->bytes;
-    if (!bytes) bytes = b->desc ? ~0ull : (uint64_t)b->n * b->stride;
-    a.bytes = bytes == ~0ull ? bytes : (bytes + 15) & ~15ull;
+    a.bytes = read_limit(b->base, bytes);
     a.stride = b->stride;
     a.n = b->n;
     a.ntiles = (b->n + 63) / 64;
@@ -1097,7 +1218,7 @@ int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, cons
     a.n_cap = o->n_cap;
     const int rc = launch_extract(a, t, st, e0, e1);
     if (rc) return fail(rc, "extract kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-    return BT_OK;
+    return check_bounds(st, nullptr, "extract");
 }
 
 }  // namespace

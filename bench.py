@@ -4,6 +4,12 @@
     python bench.py [--gpus N --steps K --warmup W] [--config c2f|c2|c3|c4] [--configs LIST|none]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+--gpus N without a launcher (WORLD_SIZE unset) starts the N rank processes itself, before
+anything touches a GPU (subprocess, never exec), rank r on device r, rendezvous on
+127.0.0.1; under a launcher --gpus must equal WORLD_SIZE. Every rank checks that the ranks
+drive distinct devices (PCI bus ids) unless BT_BENCH_DEVICE pins them all to one device (a
+multi-rank rehearsal on a 1-GPU box, reported as such in the line).
+
 A step = one bt_parse_filter_device() pass over one synthetic 16M-packet batch that is
 already resident in HBM (the reference's batch entry it replaces:
 PacketFilter::applyFilters(const std::vector<Packet>&), src/PacketFilter.cpp:121-130,
@@ -545,6 +551,69 @@ def cpu_baseline(sample, wl, seconds, cpus):
                       f"instances, disjoint shards"}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus n` with no launcher: run this script as n rank processes (RANK = LOCAL_RANK
+    = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1) and return the worst exit code. This process
+    never touches a GPU. A rank that fails ends the others (they would wait at a barrier)."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        time.sleep(0.1)
+    return worst
+
+
+def check_devices(ctx, dist, world) -> dict:
+    """Every rank's (host, PCI bus id); distinct unless BT_BENCH_DEVICE pins all ranks to
+    one device. Returns what the line reports about it."""
+    import socket
+    ordinal, bus = ctx.device_id()
+    me = (socket.gethostname(), bus)
+    ids = [me]
+    if dist is not None:
+        ids = [None] * world
+        dist.all_gather_object(ids, me)
+    distinct = len(set(ids))
+    pinned = "BT_BENCH_DEVICE" in os.environ
+    if distinct != world and not pinned:
+        sys.exit(f"bench.py: {world} ranks drive only {distinct} distinct device(s) {sorted(set(ids))}; "
+                 f"set BT_BENCH_DEVICE for a one-device rehearsal")
+    return {"devices_distinct": distinct, "pci_bus_ids": [b for _, b in ids],
+            "rehearsal_one_device": bool(pinned and world > 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -575,6 +644,15 @@ def main():
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} (the launcher's rank count)")
+    if os.environ.get("BT_BENCH_SPAWN_CHECK"):   # tests: the launcher's env, no GPU touched
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
+              flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -587,6 +665,7 @@ def main():
     # BT_BENCH_DEVICE: put every rank on one device (multi-rank rehearsal on a 1-GPU box)
     device = int(os.environ.get("BT_BENCH_DEVICE", local))
     ctx = abi.Context(device, grid_waves=args.grid_waves, flags=flags)
+    devices = check_devices(ctx, dist, world)
 
     head = dict(WORKLOADS[args.config])
     if args.outputs is not None:
@@ -649,7 +728,7 @@ def main():
             "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64, streamed to HBM)",
             "config": {"workload": h["workload"], "packets_per_gpu": h["packets_per_gpu"],
                        "packets_total": h["packets_total"], "parallelism": f"batch split x{world}",
-                       "pass_fraction": h.get("pass_fraction")},
+                       "pass_fraction": h.get("pass_fraction"), **devices},
             "roofline": h["roofline"],
             "cpu_baseline": h.get("cpu_baseline"),
             "timing": h["timing"],

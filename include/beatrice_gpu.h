@@ -330,6 +330,9 @@ const char* bt_last_error(void);              /* thread-local message of the las
 int  bt_create(int device, const bt_opts* opts, bt_ctx** out);
 void bt_destroy(bt_ctx* ctx);
 int  bt_device_count(int* out);
+/* The context's device: its HIP ordinal and PCI bus id ("0000:05:00.0"; cap >= 16), so
+ * that processes sharing a node can check they drive distinct GPUs. */
+int  bt_context_device(const bt_ctx* ctx, int* device, char* pci_bus_id, uint32_t cap);
 
 /* Compile the enabled filters: stable sort by priority (descending), parse each
  * expression once. The C++ adapter (beatrice_amd/host) passes filters already in
@@ -456,6 +459,12 @@ int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
 /* Waits for the context's stream and its compaction stream (bt_parse_filter_device_async). */
 int  bt_synchronize(bt_ctx* ctx);
+/* Caller-owned streams on the context's device (a hipStream_t, non-blocking) for the
+ * `stream` arguments above, for hosts that cannot create one themselves. Destroying a
+ * stream waits for its work. */
+int  bt_stream_create(bt_ctx* ctx, void** stream);
+int  bt_stream_synchronize(bt_ctx* ctx, void* stream);
+int  bt_stream_destroy(bt_ctx* ctx, void* stream);
 /* Timing of a device-resident run on the context stream: `iters` steps, each = the
  * main kernel between an event pair + the compaction kernels; returns the event span
  * per step and the mean main-kernel time. With BT_OPT_GRAPH the steps are captured
