@@ -73,6 +73,7 @@ OPT_PAYLOAD_HOST = 0x200
 OPT_WIDE_NEVER = 0x400
 OPT_WIDE_ALWAYS = 0x800
 OPT_PIPELINE = 0x2000
+OPT_GROUP_SHARED_DEVICE = 0x4000
 TIME_KERNEL_EVENTS = 0x1
 TIME_PIPELINED = 0x2
 
@@ -151,6 +152,8 @@ EXPORTS = [
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3",
+    "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
+    "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
 ]
 
 _lib = None
@@ -218,6 +221,14 @@ def lib() -> ctypes.CDLL:
         "bt_format_records": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, ctypes.POINTER(u64), vp]),
         "bt_record_unpack": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, ctypes.POINTER(u64)]),
         "bt_record_slabs": (u32, [vp]),
+        "bt_group_create": (ctypes.c_int, [vp, u32, ctypes.POINTER(Opts), ctypes.POINTER(vp)]),
+        "bt_group_destroy": (None, [vp]),
+        "bt_group_size": (u32, [vp]),
+        "bt_group_member": (vp, [vp, u32]),
+        "bt_group_filter_compile": (ctypes.c_int, [vp, ctypes.POINTER(FilterDesc), u32]),
+        "bt_group_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_group_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_group_split": (ctypes.c_int, [vp, u32, u32, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):   # an older build under BT_LIB_PATH (A/B runs); tests check EXPORTS
@@ -452,6 +463,76 @@ class Context:
         data = np.ascontiguousarray(data)
         desc = np.ascontiguousarray(desc, dtype=np.uint64)
         _check(lib().bt_parse_filter(self.h, p(data), p(desc), n, p(rec), p(ver), p(dec), p(pidx), p(npass)))
+        out = {"records": rec, "verdict": ver, "decide": dec}
+        if filters:
+            out["pass_idx"] = pidx[: int(npass[0])]
+            out["n_pass"] = int(npass[0])
+        return out
+
+
+def group_split(lens: np.ndarray, parts: int) -> list[tuple[int, int]]:
+    """bt_group_split (host only): the members' [lo, hi) packet ranges."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    b = np.zeros(parts + 1, np.uint32)
+    _check(lib().bt_group_split(lens.ctypes.data if len(lens) else None, len(lens), parts, b.ctypes.data))
+    return [(int(b[k]), int(b[k + 1])) for k in range(parts)]
+
+
+class Group:
+    """bt_group: one context per device in this process."""
+
+    def __init__(self, devices, host_chunk_packets: int = 0, flags: int = 0, host_threads: int = 0):
+        opts = Opts()
+        opts.host_chunk_packets = host_chunk_packets
+        opts.flags = flags
+        opts.host_threads = host_threads
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p(0)
+        _check(lib().bt_group_create(devs, len(devices), ctypes.byref(opts), ctypes.byref(h)))
+        self.h = h.value
+        self.devices = list(devices)
+
+    def close(self):
+        if self.h:
+            lib().bt_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(lib().bt_group_size(self.h))
+
+    def compile(self, filters):
+        arr = filter_descs(filters)
+        _check(lib().bt_group_filter_compile(self.h, arr, len(filters)))
+
+    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
+        """bt_group_parse_filter over host buffers (the same outputs as Context.run_host)."""
+        return self._run(lambda *o: lib().bt_group_parse_filter(self.h, data.ctypes.data, desc.ctypes.data,
+                                                                len(desc), *o),
+                         len(desc), records, filters, keep=(np.ascontiguousarray(data),))
+
+    def run_ptrs(self, frames, records=True, filters=True):
+        """bt_group_parse_filter_ptrs over a list of frames (the std::vector<Packet> form)."""
+        bufs = [np.frombuffer(bytes(f), np.uint8) if len(f) else np.zeros(1, np.uint8) for f in frames]
+        ptrs = (ctypes.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
+        lens = np.array([len(f) for f in frames], np.uint32)
+        return self._run(lambda *o: lib().bt_group_parse_filter_ptrs(self.h, ptrs, lens.ctypes.data, len(frames), *o),
+                         len(frames), records, filters, keep=(bufs, lens))
+
+    def _run(self, call, n, records, filters, keep=()):
+        rec = np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None
+        ver = np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None
+        dec = np.zeros(n, dtype=np.uint8) if filters else None
+        pidx = np.zeros(max(n, 1), dtype=np.uint32) if filters else None
+        npass = np.zeros(1, dtype=np.uint32) if filters else None
+        p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        _check(call(p(rec), p(ver), p(dec), p(pidx), p(npass)))
+        del keep
         out = {"records": rec, "verdict": ver, "decide": dec}
         if filters:
             out["pass_idx"] = pidx[: int(npass[0])]

@@ -1,13 +1,26 @@
 // bt_host.h — runtime services shared by the host-only translation units of
-// libbeatrice_gpu.so (bt_ring.cpp): the thread-local error slot behind
-// bt_last_error() and the context's host thread pool.
+// libbeatrice_gpu.so (bt_ring.cpp, bt_group.cpp): the thread-local error slot behind
+// bt_last_error(), the context's host thread pool, and filter programs.
 #pragma once
 
 #include <functional>
+#include <vector>
 
 #include "beatrice_gpu.h"
 
 namespace bt {
+
+// A compiled PacketFilter program: the slots (bt_filter_compile_host) and the DFA tables
+// of its BT_K_PAYLOAD slots. compile_program is host-only; install_program puts it on a
+// context's device (bt_filter_compile = both; a group compiles once, installs on each).
+struct CompiledProgram {
+    std::vector<bt_filter_slot> slots;
+    std::vector<uint8_t> dfa_pool;
+};
+int compile_program(const bt_filter_desc* f, uint32_t n, uint32_t ctx_flags, CompiledProgram* out);
+int install_program(bt_ctx* c, const CompiledProgram& p);
+uint32_t ctx_flags(const bt_ctx* c);
+int ctx_device(const bt_ctx* c);
 
 // Sets bt_last_error() and returns `code`.
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

@@ -589,17 +589,22 @@ int bt_filter_compile_host(const bt_filter_desc* f, uint32_t n, bt_filter_slot* 
     return BT_OK;
 }
 
-int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
-    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+}  // extern "C"
+
+namespace bt {
+
+// The host half of bt_filter_compile: the slots, and the PAYLOAD regexes the DFA compiler
+// takes turned into BT_K_PAYLOAD slots with their tables in one pool (copied into each
+// block's LDS, so capped at kDfaPoolMax). No device is touched: a group compiles once and
+// installs the result on every member.
+int compile_program(const bt_filter_desc* f, uint32_t n, uint32_t ctx_flags, CompiledProgram* out) {
     std::vector<bt_filter_slot> slots(BT_MAX_FILTERS);
     uint32_t m = 0;
     int rc = bt_filter_compile_host(f, n, slots.data(), BT_MAX_FILTERS, &m);
     if (rc) return rc;
     slots.resize(m);
-    // PAYLOAD regexes the DFA compiler takes run on the GPU (BT_K_PAYLOAD); the pool of
-    // their tables is copied into each block's LDS, so it is capped at kDfaPoolMax.
     std::vector<uint8_t> pool;
-    if (!(c->opts.flags & BT_OPT_PAYLOAD_HOST)) {
+    if (!(ctx_flags & BT_OPT_PAYLOAD_HOST)) {
         for (auto& s : slots) {
             const bt_filter_desc& d = f[s.source_index];
             if (s.kind != BT_K_HOST || d.type != BT_FILTER_PAYLOAD || !d.expression) continue;
@@ -621,10 +626,16 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
             s.b = size;
         }
     }
+    out->slots = std::move(slots);
+    out->dfa_pool = std::move(pool);
+    return BT_OK;
+}
+
+// The device half: the DFA pool into the buffer no queued launch reads (launches on any
+// stream that still read it, with the old program, are waited for first), then the slots.
+int install_program(bt_ctx* c, const CompiledProgram& p) {
     std::lock_guard<std::mutex> lk(c->mu);
-    if (!pool.empty()) {
-        // write the pool into the buffer no queued launch reads: launches on any stream
-        // that still read it (with the old program) are waited for first
+    if (!p.dfa_pool.empty()) {
         HIP_TRY(hipSetDevice(c->device));
         const int k = c->dfa_cur ^ 1;
         if (!c->dfa_dev[k]) HIP_TRY(hipMalloc(&c->dfa_dev[k], kDfaPoolMax));
@@ -633,15 +644,29 @@ int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
             c->dfa_spare.push_back(r.second);
         }
         c->dfa_readers[k].clear();
-        if (int rc = bt_memcpy_h2d(c, c->dfa_dev[k], pool.data(), pool.size())) return rc;   // staged, synchronous
+        if (int rc = bt_memcpy_h2d(c, c->dfa_dev[k], p.dfa_pool.data(), p.dfa_pool.size())) return rc;   // synchronous
         c->dfa_cur = k;
     }
     // a cached BT_OPT_GRAPH timing graph holds the old program: drop it
     if (c->tgraph) { (void)hipGraphExecDestroy(c->tgraph); c->tgraph = nullptr; }
-    c->dfa_pool = std::move(pool);
-    c->slots = slots;
-    to_device_program(c->slots.data(), m, &c->prog);
+    c->dfa_pool = p.dfa_pool;
+    c->slots = p.slots;
+    to_device_program(c->slots.data(), (uint32_t)c->slots.size(), &c->prog);
     return BT_OK;
+}
+
+uint32_t ctx_flags(const bt_ctx* c) { return c->opts.flags; }
+int ctx_device(const bt_ctx* c) { return c->device; }
+
+}  // namespace bt
+
+extern "C" {
+
+int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
+    if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
+    CompiledProgram p;
+    if (int rc = compile_program(f, n, c->opts.flags, &p)) return rc;
+    return install_program(c, p);
 }
 
 int bt_filter_program(const bt_ctx* c, bt_filter_slot* out, uint32_t cap, uint32_t* n_slots) {

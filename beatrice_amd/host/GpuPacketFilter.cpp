@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <memory>
 #include <regex>
 #include <stdexcept>
@@ -59,12 +60,35 @@ bool payload_match(const std::regex& re, const uint8_t* d, size_t len) {
 
 }  // namespace
 
-GpuPacketFilter::GpuPacketFilter(int device, const bt_opts* opts) {
-    if (bt_create(device, opts, &ctx_) != BT_OK)
-        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+std::vector<int> GpuPacketFilter::devicesFromEnv(int fallback) {
+    std::vector<int> d;
+    if (const char* e = std::getenv("BEATRICE_GPU_DEVICES")) {
+        std::string s(e);
+        size_t at = 0;
+        while (at < s.size()) {
+            const size_t comma = s.find(',', at);
+            const std::string tok = s.substr(at, comma == std::string::npos ? std::string::npos : comma - at);
+            if (!tok.empty()) d.push_back(std::stoi(tok));
+            if (comma == std::string::npos) break;
+            at = comma + 1;
+        }
+    }
+    if (d.empty()) d.push_back(fallback);
+    return d;
 }
 
-GpuPacketFilter::~GpuPacketFilter() { bt_destroy(ctx_); }
+GpuPacketFilter::GpuPacketFilter(int device, const bt_opts* opts) { open(devicesFromEnv(device), opts); }
+
+GpuPacketFilter::GpuPacketFilter(const std::vector<int>& devices, const bt_opts* opts) { open(devices, opts); }
+
+void GpuPacketFilter::open(const std::vector<int>& devices, const bt_opts* opts) {
+    if (devices.empty()) throw std::invalid_argument("GpuPacketFilter: empty device list");
+    if (bt_group_create(devices.data(), (uint32_t)devices.size(), opts, &group_) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    ctx_ = bt_group_member(group_, 0);
+}
+
+GpuPacketFilter::~GpuPacketFilter() { bt_group_destroy(group_); }
 
 Result<void> GpuPacketFilter::addFilter(const std::string& name, const FilterConfig& config) {
     std::lock_guard<std::mutex> lock(filtersMutex_);   // :19-31
@@ -148,7 +172,7 @@ void GpuPacketFilter::compileLocked() {
         descs[i].priority = c.priority;
         descs[i].has_custom_func = sortedFilters[i].second->customFunc ? 1 : 0;
     }
-    if (bt_filter_compile(ctx_, descs.data(), (uint32_t)descs.size()) != BT_OK)
+    if (bt_group_filter_compile(group_, descs.data(), (uint32_t)descs.size()) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
     std::vector<bt_filter_slot> slots(BT_MAX_FILTERS);
     uint32_t m = 0;
@@ -202,7 +226,8 @@ uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
     return (BT_DECIDE_PASS << 6) | (program_.empty() ? 0u : (uint32_t)program_.size() - 1);
 }
 
-void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide) {
+void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
+                               std::vector<bt_rec>* records) {
     const uint32_t n = (uint32_t)packets.size();
     std::vector<const uint8_t*> ptrs(n);
     std::vector<uint32_t> lens(n);
@@ -211,8 +236,9 @@ void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<u
         lens[i] = (uint32_t)packets[i].length();
     }
     decide.assign(n, 0);
-    if (bt_parse_filter_ptrs(ctx_, ptrs.data(), lens.data(), n, nullptr, nullptr, decide.data(), nullptr,
-                             nullptr) != BT_OK)
+    if (records) records->resize(n);
+    if (bt_group_parse_filter_ptrs(group_, ptrs.data(), lens.data(), n, records ? records->data() : nullptr, nullptr,
+                                   decide.data(), nullptr, nullptr) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
 }
 
@@ -227,6 +253,8 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
     runBatch(packets, decide);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
+    const auto t1 = std::chrono::steady_clock::now();
+    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
     for (size_t i = 0; i < packets.size(); ++i) {
         uint32_t d = decide[i];
         if ((d >> 6) == BT_DECIDE_HOST) d = resolveHost(packets[i], d & 63u);
@@ -247,6 +275,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
         updateStats(r.filterName, r.passed, per);
         results.push_back(std::move(r));
     }
+    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return results;
 }
 
@@ -263,6 +292,8 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
     runBatch(packets, v.decide);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
+    const auto t1 = std::chrono::steady_clock::now();
+    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
     const std::string none;
     for (size_t i = 0; i < packets.size(); ++i) {
         uint32_t d = v.decide[i];
@@ -273,18 +304,21 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
         if (passed) v.pass_idx.push_back((uint32_t)i);
         updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
     }
+    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return v;
 }
 
-GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<Packet>& packets) {
+GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<Packet>& packets, bool withRecords) {
     Verdicts v;
     std::lock_guard<std::mutex> lock(filtersMutex_);
     if (dirty_) compileLocked();
     if (packets.empty()) return v;
     const auto t0 = std::chrono::steady_clock::now();
-    runBatch(packets, v.decide);
+    runBatch(packets, v.decide, withRecords ? &v.records : nullptr);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
+    const auto t1 = std::chrono::steady_clock::now();
+    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
     const std::string none;
     for (size_t i = 0; i < packets.size(); ++i) {
         uint32_t d = v.decide[i];
@@ -305,6 +339,7 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<P
         if (passed) v.pass_idx.push_back((uint32_t)i);
         updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
     }
+    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return v;
 }
 

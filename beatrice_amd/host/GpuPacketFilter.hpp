@@ -14,6 +14,9 @@
 //   * PAYLOAD (std::regex) and CUSTOM (std::function) filters are evaluated here on
 //     the host, with the reference's semantics, for the packets that reach them.
 // processingTime is the amortised batch time (the reference's value is a wall clock).
+// Several devices: a device list (or BEATRICE_GPU_DEVICES=0,1,... for the default
+// constructor) makes the filter drive a bt_group — the program compiled once, every batch
+// split across the devices (include/beatrice_gpu.h, "several devices in one process").
 #pragma once
 
 #include <cstdint>
@@ -36,8 +39,10 @@ public:
     using FilterResult = beatrice::PacketFilter::FilterResult;
     using FilterStats = beatrice::PacketFilter::FilterStats;
 
-    // Throws std::runtime_error when no MI355X is available (no CPU fallback).
+    // Throws std::runtime_error when no MI355X is available (no CPU fallback). The default
+    // device list is BEATRICE_GPU_DEVICES (e.g. "0,1,2,3") when set, else {device}.
     explicit GpuPacketFilter(int device = 0, const bt_opts* opts = nullptr);
+    explicit GpuPacketFilter(const std::vector<int>& devices, const bt_opts* opts = nullptr);
     ~GpuPacketFilter();
     GpuPacketFilter(const GpuPacketFilter&) = delete;
     GpuPacketFilter& operator=(const GpuPacketFilter&) = delete;
@@ -59,6 +64,8 @@ public:
         std::vector<uint8_t> decide;     // (code << 6) | slot
         std::vector<uint32_t> pass_idx;  // ascending
         std::vector<uint32_t> error_idx; // classifyPerPacket only: packets whose evaluation threw
+        std::vector<bt_rec> records;     // withRecords: each packet's parse record, from the same
+                                         // kernel pass (the reference's parsePacket per walked layer)
     };
     Verdicts classify(const std::vector<Packet>& packets);
 
@@ -69,7 +76,8 @@ public:
     // callback) is listed in error_idx with decide code BT_DECIDE_THROW and, as in the
     // reference, does not update the stats; every other packet is classified and counted.
     // Never throws for a filter; throws std::runtime_error if the device fails.
-    Verdicts classifyPerPacket(const std::vector<Packet>& packets);
+    // withRecords: the same kernel pass also parses every packet (Verdicts::records).
+    Verdicts classifyPerPacket(const std::vector<Packet>& packets, bool withRecords = false);
 
     // Zero-copy form over frames the device already sees (a capture ring registered
     // with bt_host_register): runs parse+filter over `batch` into `out` (device-visible
@@ -79,9 +87,21 @@ public:
     std::vector<uint32_t> classifyMapped(const bt_batch& batch, const bt_outputs& out, uint8_t* decideHost,
                                          uint64_t* verdictHost, const std::function<Packet(uint32_t)>& packetOf);
 
+    // Where the last batch call's time went: the device pass (host gather, H2D, kernels,
+    // D2H over every device of the group) and the host's work after it (PAYLOAD / CUSTOM
+    // resumption, FilterResults, stats).
+    struct BatchTiming {
+        double device_s = 0, host_s = 0;
+    };
+    BatchTiming lastBatchTiming() const { return timing_; }
+
     // Evaluation order of the enabled filters (names), as applyFilters uses it.
     std::vector<std::string> evaluationOrder();
-    bt_ctx* context() const { return ctx_; }
+    bt_ctx* context() const { return ctx_; }          // the first device's context
+    bt_group* group() const { return group_; }
+    uint32_t deviceCount() const { return bt_group_size(group_); }
+    // The devices BEATRICE_GPU_DEVICES names ({fallback} when unset or empty).
+    static std::vector<int> devicesFromEnv(int fallback);
 
 private:
     struct FilterEntry {
@@ -98,9 +118,12 @@ private:
     // host continuation for packets the device left at a PAYLOAD/CUSTOM slot
     uint32_t resolveHost(const Packet& p, uint32_t first_slot);
     [[noreturn]] void rethrow(const Slot& s) const;
-    void runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide);
+    void runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide, std::vector<bt_rec>* records = nullptr);
     void updateStats(const std::string& filterName, bool passed, std::chrono::microseconds t);
 
+    void open(const std::vector<int>& devices, const bt_opts* opts);
+
+    bt_group* group_ = nullptr;
     bt_ctx* ctx_ = nullptr;
     std::unordered_map<std::string, FilterEntry> filters_;
     mutable std::mutex filtersMutex_;
@@ -108,6 +131,7 @@ private:
     mutable std::mutex statsMutex_;
     bool dirty_ = true;
     std::vector<Slot> program_;
+    BatchTiming timing_;
 };
 
 }  // namespace gpu

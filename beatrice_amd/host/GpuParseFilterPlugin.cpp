@@ -5,6 +5,10 @@
 //
 // Configuration (environment, read in onStart):
 //   BEATRICE_GPU_DEVICE    device index (default 0)
+//   BEATRICE_GPU_DEVICES   device list "0,1,2,..." (overrides BEATRICE_GPU_DEVICE): every batch
+//                          is split across the devices (bt_group, one process)
+//   BEATRICE_GPU_RECORDS   1: the kernel pass also parses every packet; the sink gets each
+//                          packet's bt_rec (gpu_verdict_batch.records)
 //   BEATRICE_GPU_BATCH     packets per GPU batch (default 65536)
 //   BEATRICE_GPU_FLUSH_US  a partial batch is classified at the latest this many
 //                          microseconds after its first packet arrived, by the plugin's
@@ -54,6 +58,7 @@ public:
             std::lock_guard<std::mutex> lk(mu_);
             const int device = env_int("BEATRICE_GPU_DEVICE", 0);
             batch_ = (size_t)std::max(1, env_int("BEATRICE_GPU_BATCH", 65536));
+            records_ = env_int("BEATRICE_GPU_RECORDS", 0) != 0;
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
             filter_ = std::make_unique<GpuPacketFilter>(device);
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
@@ -207,7 +212,7 @@ private:
             }
         } advance{this};
         if (!filter_) return;
-        const auto v = filter_->classifyPerPacket(batch);
+        const auto v = filter_->classifyPerPacket(batch, records_);
         processed_ += batch.size();
         passed_ += v.pass_idx.size();
         errors_ += v.error_idx.size();
@@ -223,6 +228,7 @@ private:
     std::chrono::steady_clock::time_point first_;
     size_t batch_ = 65536;
     int flush_us_ = 2000;
+    bool records_ = false;
     uint64_t next_seq_ = 0, done_seq_ = 0;
     bool stop_ = true;
     std::thread flusher_;
@@ -260,7 +266,33 @@ extern "C" void gpu_plugin_set_sink(beatrice::IPacketPlugin* p, gpu_verdict_sink
         }
         gpu_verdict_batch c{seq, (uint32_t)b.size(), frames.data(), lens.data(), v.decide.data(),
                             v.pass_idx.data(), (uint32_t)v.pass_idx.size(), v.error_idx.data(),
-                            (uint32_t)v.error_idx.size()};
+                            (uint32_t)v.error_idx.size(), v.records.empty() ? nullptr : v.records.data()};
         fn(user, &c);
     });
+}
+
+extern "C" uint32_t gpu_batch_layers(const gpu_verdict_batch* b, uint32_t i, gpu_walked_layer* out, uint32_t cap) {
+    if (!b || !b->records || i >= b->n) return 0;
+    const bt_rec& r = b->records[i];
+    gpu_walked_layer l[6];
+    uint32_t k = 0;
+    auto add = [&](const char* name, uint32_t off, int32_t tag, uint32_t bit) {
+        l[k++] = {name, off, tag, (r.ok & bit) ? 1u : 0u};
+    };
+    add("ethernet", 0, -1, BT_L_ETH);   // the walk (DESIGN.md R-WALK), from the record's bitmaps
+    if (r.present & BT_L_VLAN0) add("vlan", 12, 0, BT_L_VLAN0);
+    if (r.present & BT_L_VLAN1) add("vlan", 16, 1, BT_L_VLAN1);
+    if (r.present & BT_L_IPV4) add("ipv4", r.l3_off, -1, BT_L_IPV4);
+    if (r.present & BT_L_IPV6) add("ipv6", r.l3_off, -1, BT_L_IPV6);
+    if (r.present & BT_L_TCP) add("tcp", r.l4_off, -1, BT_L_TCP);
+    if (r.present & BT_L_UDP) add("udp", r.l4_off, -1, BT_L_UDP);
+    if (r.present & BT_L_ICMP) add("icmp", r.l4_off, -1, BT_L_ICMP);
+    for (uint32_t j = 0; j < k && j < cap && out; ++j) out[j] = l[j];
+    return k;
+}
+
+extern "C" int gpu_batch_format(const gpu_verdict_batch* b, uint32_t i, uint32_t fmt, char* out, uint64_t cap,
+                                uint64_t* out_len) {
+    if (!b || !b->records || i >= b->n) return BT_E_INVALID_ARGUMENT;
+    return bt_format_records(nullptr, b->records + i, 1, fmt, out, cap, out_len, nullptr);
 }

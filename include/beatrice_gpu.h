@@ -292,6 +292,7 @@ typedef struct bt_opts {
 #define BT_OPT_WIDE_NEVER 0x400u   /* descriptor mode: always two-round loads (A/B only)   */
 #define BT_OPT_WIDE_ALWAYS 0x800u  /* descriptor mode: always wide round A (A/B only)      */
 #define BT_OPT_PIPELINE 0x2000u    /* bt_time_device: steps as bt_parse_filter_device_async */
+#define BT_OPT_GROUP_SHARED_DEVICE 0x4000u /* bt_group_create: allow a device listed twice (tests) */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
@@ -450,6 +451,32 @@ int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_b
 /* Hands `count` blocks starting at first_block back to the kernel (TP_STATUS_KERNEL,
  * release-ordered). Call it once the device has finished reading them. */
 int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);
+
+/* ---- several devices in one process -------------------------------
+ * The reference runs one daemon process whose capture threads feed one plugin set
+ * (src/BeatriceContext.cpp:215-278, src/PluginManager.cpp:158-188). A group is one
+ * context per device (its own streams, pinned staging and host threads). The filter
+ * program is compiled once on the host and installed on every member. A host batch is
+ * split into contiguous ranges that start on 64-packet boundaries and balance the bytes
+ * each member stages (bt_group_split), every member runs its range concurrently, and the
+ * outputs land in the caller's arrays exactly as bt_parse_filter / _ptrs write them for
+ * the whole batch (pass indices in ascending order). No data crosses devices. */
+typedef struct bt_group bt_group;
+int      bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out);
+void     bt_group_destroy(bt_group* group);
+uint32_t bt_group_size(const bt_group* group);
+bt_ctx*  bt_group_member(bt_group* group, uint32_t k);   /* member k's context (device k) */
+int      bt_group_filter_compile(bt_group* group, const bt_filter_desc* filters, uint32_t n);
+int      bt_group_parse_filter(bt_group* group, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n,
+                               bt_rec* records, uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx,
+                               uint32_t* n_pass);
+int      bt_group_parse_filter_ptrs(bt_group* group, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                                    bt_rec* records, uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx,
+                                    uint32_t* n_pass);
+/* The split (host only): bounds[0..parts] with bounds[0] = 0, bounds[parts] = n, every
+ * inner bound a multiple of 64, member k taking [bounds[k], bounds[k+1]); balanced by the
+ * cost min(len, 128) + 8 + 96 bytes per packet (beatrice_amd/shard.py:shard_bounds). */
+int      bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* bounds);
 
 /* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
 int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);

@@ -7,11 +7,20 @@
  * the verdicts (another plugin, the application) installs a verdict sink on the
  * IPacketPlugin* the manager created: it is called once per classified batch, in arrival
  * order, on the thread that classified it (an onPacket caller or the plugin's flush
- * thread). All pointers are valid for the duration of the call only. */
+ * thread). All pointers are valid for the duration of the call only.
+ *
+ * With BEATRICE_GPU_RECORDS=1 the same kernel pass also parses every packet, and the sink
+ * sees each packet's bt_rec: the fields of every walked layer as the reference's
+ * ProtocolParser::parsePacket(slice, name) returns them (include/beatrice_gpu.h). The
+ * helpers below turn a record into its walked layers or into the reference's ParseResult
+ * text, as PluginManager::processPackets consumers (src/PluginManager.cpp:173-188) would
+ * get from calling the parser themselves. */
 #ifndef BEATRICE_GPU_PLUGIN_H
 #define BEATRICE_GPU_PLUGIN_H
 
 #include <stdint.h>
+
+#include "beatrice_gpu.h"
 
 #ifdef __cplusplus
 namespace beatrice { class IPacketPlugin; }
@@ -31,7 +40,15 @@ typedef struct gpu_verdict_batch {
     uint32_t n_pass;
     const uint32_t* error_idx;         /* indices of the packets whose evaluation threw       */
     uint32_t n_error;                  /* (counted in IPacketPlugin::getErrorCount)          */
+    const bt_rec* records;             /* BEATRICE_GPU_RECORDS=1: packet i's parse record; else NULL */
 } gpu_verdict_batch;
+
+typedef struct gpu_walked_layer {      /* one layer of the walk (DESIGN.md R-WALK)           */
+    const char* name;                  /* "ethernet" "vlan" "ipv4" "ipv6" "tcp" "udp" "icmp" */
+    uint32_t offset;                   /* the slice's start in the frame                     */
+    int32_t tag;                       /* VLAN tag index 0 / 1, -1 for other layers          */
+    uint32_t parsed;                   /* 1 SUCCESS, 0 PACKET_TOO_SHORT (no fields)          */
+} gpu_walked_layer;
 
 typedef void (*gpu_verdict_sink_fn)(void* user, const gpu_verdict_batch* batch);
 
@@ -42,6 +59,14 @@ void gpu_plugin_set_sink(gpu_plugin* plugin, gpu_verdict_sink_fn fn, void* user)
 void gpu_plugin_flush(gpu_plugin* plugin);
 /* Packets that passed every filter so far. */
 uint64_t gpu_plugin_passed(const gpu_plugin* plugin);
+/* Packet i's walked layers (records != NULL): writes min(count, cap) entries, returns the
+ * count (0 without records). */
+uint32_t gpu_batch_layers(const gpu_verdict_batch* batch, uint32_t i, gpu_walked_layer* out, uint32_t cap);
+/* The reference's ParseResult text of every walked layer of packet i (fmt = BT_FMT_*),
+ * bt_format_records on its record: out == NULL asks for the size. BT_E_INVALID_ARGUMENT
+ * without records or with a short buffer (*out_len = the size needed). */
+int gpu_batch_format(const gpu_verdict_batch* batch, uint32_t i, uint32_t fmt, char* out, uint64_t cap,
+                     uint64_t* out_len);
 
 #ifdef __cplusplus
 }

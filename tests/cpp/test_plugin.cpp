@@ -17,9 +17,16 @@
 //            applyFilters call) and every other packet is classified;
 //   sink     the verdict sink sees every batch once, in order, and each packet's verdict
 //            and deciding filter equal the reference's FilterResult;
-//   threads  onPacket from 4 threads at once: every packet is classified exactly once.
+//   threads  onPacket from 4 threads at once: every packet is classified exactly once;
+//   records  (test_plugin records DATA DESC REC, files written by tests/test_cpp_adapter.py
+//            from a reference golden capture) with BEATRICE_GPU_RECORDS=1 the sink's bt_rec
+//            of every packet equals the golden record the compiled reference's parser
+//            produced, and gpu_batch_layers / gpu_batch_format agree with the record.
 // Prints one line per check; exit status 0 = all passed.
 #include <dlfcn.h>
+
+#include <fstream>
+#include <iterator>
 
 #include <atomic>
 #include <chrono>
@@ -121,6 +128,10 @@ private:
     bool running_ = false;
 };
 
+// the plugin's record hooks, looked up with dlsym like the others
+static uint32_t (*g_batch_layers)(const gpu_verdict_batch*, uint32_t, gpu_walked_layer*, uint32_t) = nullptr;
+static int (*g_batch_format)(const gpu_verdict_batch*, uint32_t, uint32_t, char*, uint64_t, uint64_t*) = nullptr;
+
 // ---- PluginManager's call sequence ----------------------------------------------------
 struct Host {
     void* handle = nullptr;
@@ -135,6 +146,8 @@ struct Host {
         auto create = reinterpret_cast<Create>(dlsym(handle, "createPlugin"));   // :67-68
         set_sink = reinterpret_cast<decltype(set_sink)>(dlsym(handle, "gpu_plugin_set_sink"));
         flush = reinterpret_cast<decltype(flush)>(dlsym(handle, "gpu_plugin_flush"));
+        g_batch_layers = reinterpret_cast<decltype(g_batch_layers)>(dlsym(handle, "gpu_batch_layers"));
+        g_batch_format = reinterpret_cast<decltype(g_batch_format)>(dlsym(handle, "gpu_batch_format"));
         if (!create || !set_sink || !flush) return false;
         plugin = create();                                                  // :79
         plugin->onStart();                                                  // :95
@@ -312,7 +325,98 @@ static bool threads_case(const char* so, FakeBackend& be) {
     return true;
 }
 
+static std::vector<uint8_t> slurp(const char* path) {
+    std::ifstream f(path, std::ios::binary);
+    return std::vector<uint8_t>(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+}
+
+// The sink's records against the golden records of the same frames.
+static bool records_case(const char* so, const char* data_path, const char* desc_path, const char* rec_path) {
+    const auto data = slurp(data_path), dbytes = slurp(desc_path), want = slurp(rec_path);
+    const size_t n = dbytes.size() / 8;
+    CHECK(n > 0 && want.size() == n * sizeof(bt_rec), "records: %zu descriptors, %zu record bytes", n, want.size());
+    std::vector<uint64_t> desc(n);
+    std::memcpy(desc.data(), dbytes.data(), n * 8);
+    setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|3|udp;net|IP_RANGE|2|10.0.0.0/8;ports|PORT_RANGE|1|1000-2000;", 1);
+    setenv("BEATRICE_GPU_BATCH", "1000", 1);
+    setenv("BEATRICE_GPU_FLUSH_US", "5000", 1);
+    setenv("BEATRICE_GPU_RECORDS", "1", 1);
+    Host h;
+    CHECK(h.load(so), "records: load %s", so);
+    CHECK(g_batch_layers && g_batch_format, "records: the plugin exports no gpu_batch_layers / gpu_batch_format");
+    struct RecSink {
+        std::mutex mu;
+        std::vector<bt_rec> recs;
+        std::atomic<uint64_t> packets{0};
+        uint64_t layer_bad = 0, format_bad = 0, with_records = 0;
+        static void call(void* user, const gpu_verdict_batch* b) {
+            auto* s = static_cast<RecSink*>(user);
+            std::lock_guard<std::mutex> lk(s->mu);
+            if (b->records) {
+                ++s->with_records;
+                s->recs.insert(s->recs.end(), b->records, b->records + b->n);
+                for (uint32_t i = 0; i < b->n; ++i) {
+                    gpu_walked_layer l[8];
+                    const uint32_t k = g_batch_layers(b, i, l, 8);
+                    const bt_rec& r = b->records[i];
+                    // every present layer listed once, Ethernet first; parsed = the ok bit
+                    uint32_t present = 0;
+                    for (uint32_t j = 0; j < k; ++j) present += l[j].parsed <= 1;
+                    if (k < 1 || std::strcmp(l[0].name, "ethernet") != 0 || present != k ||
+                        k != 1u + (uint32_t)__builtin_popcount(r.present & ~BT_L_ETH))
+                        ++s->layer_bad;
+                    uint64_t need = 0;
+                    if (g_batch_format(b, i, BT_FMT_JSON, nullptr, 0, &need) != BT_OK || need == 0) {
+                        ++s->format_bad;
+                        continue;
+                    }
+                    std::string t(need, '\0'), u(need, '\0');
+                    uint64_t got = 0, got2 = 0;
+                    if (g_batch_format(b, i, BT_FMT_JSON, t.data(), need, &got) != BT_OK ||
+                        bt_format_records(nullptr, &r, 1, BT_FMT_JSON, u.data(), need, &got2, nullptr) != BT_OK ||
+                        t != u)
+                        ++s->format_bad;
+                }
+            }
+            s->packets += b->n;
+        }
+    } sink;
+    h.set_sink(h.plugin, &RecSink::call, &sink);
+    for (size_t i = 0; i < n; ++i) {
+        Packet p(std::shared_ptr<const uint8_t[]>(data.data() + (desc[i] & 0xFFFFFFFFFFFFull), [](const uint8_t*) {}),
+                 (size_t)(desc[i] >> 48));
+        h.processPacket(p);
+    }
+    h.flush(h.plugin);
+    const auto limit = Clock::now() + std::chrono::seconds(10);
+    while (sink.packets < n && Clock::now() < limit) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    CHECK(sink.packets == n && sink.recs.size() == n, "records: sink saw %lu packets, %zu records of %zu",
+          (unsigned long)sink.packets.load(), sink.recs.size(), n);
+    size_t bad = 0, first = n;
+    for (size_t i = 0; i < n; ++i)
+        if (std::memcmp(&sink.recs[i], want.data() + i * sizeof(bt_rec), sizeof(bt_rec)) != 0) {
+            if (!bad) first = i;
+            ++bad;
+        }
+    CHECK(bad == 0, "records: %zu records differ from the golden (reference) records, first %zu", bad, first);
+    CHECK(sink.layer_bad == 0 && sink.format_bad == 0, "records: %lu layer lists, %lu formats wrong",
+          (unsigned long)sink.layer_bad, (unsigned long)sink.format_bad);
+    unsetenv("BEATRICE_GPU_RECORDS");
+    h.unload();
+    std::printf("ok   records  %zu packets through the plugin with BEATRICE_GPU_RECORDS=1: every sink record = the "
+                "reference's (golden), gpu_batch_layers / gpu_batch_format consistent (%lu batches)\n",
+                n, (unsigned long)sink.with_records);
+    return true;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 5 && std::strcmp(argv[1], "records") == 0) {
+        const char* so = std::getenv("BT_PLUGIN_SO") ? std::getenv("BT_PLUGIN_SO")
+                                                     : "beatrice_amd/libgpu_parse_filter_plugin.so";
+        const bool ok = records_case(so, argv[2], argv[3], argv[4]);
+        std::printf(ok && !g_fail ? "ALL OK\n" : "FAILURES\n");
+        return ok && !g_fail ? 0 : 1;
+    }
     const char* so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
     int ndev = 0;
     if (bt_device_count(&ndev) != BT_OK || ndev == 0) {

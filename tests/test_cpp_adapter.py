@@ -32,3 +32,25 @@ def test_plugin_in_the_reference_pipeline():
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "ALL OK" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["c3", "c4", "edge"])
+def test_plugin_sink_records_equal_reference_goldens(cap, tmp_path):
+    """BEATRICE_GPU_RECORDS=1: the plugin's sink hands out each packet's parse record from
+    the same kernel pass; tests/cpp/test_plugin compares them with the golden records the
+    compiled reference's ProtocolParser produced for the same frames."""
+    from conftest import load_golden
+    g, _ = load_golden(cap)
+    paths = []
+    for k in ("data", "desc", "rec"):
+        p = tmp_path / f"{k}.bin"
+        g[k].tofile(p)
+        paths.append(str(p))
+    b = os.path.join(ROOT, "tests", "cpp", "test_plugin")
+    assert os.path.exists(b), "tests/cpp/test_plugin not built (make -C tests/cpp in the build container)"
+    env = dict(os.environ, BT_PLUGIN_SO=os.path.join(ROOT, "beatrice_amd", "libgpu_parse_filter_plugin.so"))
+    r = subprocess.run([b, "records", *paths], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "ALL OK" in r.stdout

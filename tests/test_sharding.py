@@ -74,3 +74,21 @@ def test_bounds_balance_bytes():
         cost = [int((np.minimum(ln[lo:hi], 128) + 104).sum()) for lo, hi in b]
         assert max(cost) / (sum(cost) / w) < 1.01
         assert all(lo % 64 == 0 for lo, _ in b)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_group_split_equals_shard_bounds(seed):
+    """bt_group_split (the in-process multi-device split, C++) restates shard.shard_bounds
+    exactly: the same tile-aligned, byte-balanced ranges for any lengths and member count."""
+    from beatrice_amd import abi
+    rng = np.random.default_rng(seed)
+    for n in (0, 1, 63, 64, 65, 1000, 20037, int(rng.integers(1, 300000))):
+        lens = rng.choice([0, 14, 60, 64, 128, 512, 1500, 9000, 65535], size=n).astype(np.uint32)
+        for parts in (1, 2, 3, 4, 7, 8):
+            assert abi.group_split(lens, parts) == shard.shard_bounds(lens, parts), (n, parts)
+
+
+def test_native_group_split_rejects_bad_arguments():
+    from beatrice_amd import abi
+    with pytest.raises(abi.BtError):
+        abi.group_split(np.zeros(10, np.uint32), 0)

@@ -1,0 +1,246 @@
+// surface_bench.cpp — what an integrator gets from the drop-in C++ surfaces, timed next
+// to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
+// integrator calls").
+//
+//   surface_bench [all|filter|ref|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
+//
+// For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
+// (the reference's batch type, include/beatrice/Packet.hpp) and C3's 5-tuple filter set:
+//   ref       beatrice::PacketFilter::applyFilters(const std::vector<Packet>&) — the
+//             reference's batch entry (src/PacketFilter.cpp:121-130), compiled from its
+//             own sources — on T threads, one PacketFilter per thread on its own shard
+//             (and on 1 thread);
+//   apply     GpuPacketFilter::applyFilters(const std::vector<Packet>&) -> vector<FilterResult>,
+//             whole capture per call, with the split of the call into the device pass
+//             (host gather -> H2D -> kernels -> D2H) and the host's FilterResult / stats work;
+//   classify  GpuPacketFilter::classify(const std::vector<Packet>&) (decisions + pass list);
+//   plugin    libgpu_parse_filter_plugin.so through createPlugin(): onPacket from 1 and from
+//             T threads (PluginManager::processPacket's per-packet call), until the verdict
+//             sink has seen every packet.
+// One JSON object per line. The parity of every surface is tests/cpp/test_adapter.cpp's
+// and test_plugin.cpp's job; this tool only times them.
+#include <dlfcn.h>
+#include <sched.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../beatrice_amd/host/GpuPacketFilter.hpp"
+#include "beatrice/IPacketPlugin.hpp"
+#include "beatrice/PacketFilter.hpp"
+#include "beatrice_gpu_plugin.h"
+
+extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
+extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
+
+using beatrice::Packet;
+using beatrice::PacketFilter;
+using beatrice::gpu::GpuPacketFilter;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+// CPUs this process may use: the affinity set bounded by the cgroup v2 CPU quota.
+int usable_cpus() {
+    cpu_set_t set;
+    int aff = 1;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) aff = CPU_COUNT(&set);
+    std::ifstream f("/sys/fs/cgroup/cpu.max");
+    std::string q, p;
+    if (f >> q >> p && q != "max") {
+        const int quota = (int)(std::stod(q) / std::stod(p));
+        if (quota >= 1) return std::min(aff, quota);
+    }
+    return aff;
+}
+
+struct Capture {
+    const char* name;
+    std::vector<uint8_t> data;
+    std::vector<uint64_t> desc;
+    std::vector<Packet> packets;
+};
+
+Capture capture(const char* name, int cfg, uint32_t n, uint64_t seed) {
+    Capture c;
+    c.name = name;
+    c.desc.resize(n);
+    c.data.resize(bt_synth_layout(cfg, n, seed, c.desc.data()));
+    bt_synth_fill(cfg, n, seed, c.desc.data(), c.data.data(), 16);
+    c.packets.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* f = c.data.data() + (c.desc[i] & 0xFFFFFFFFFFFFull);
+        c.packets.emplace_back(std::shared_ptr<const uint8_t[]>(f, [](const uint8_t*) {}), (size_t)(c.desc[i] >> 48));
+    }
+    return c;
+}
+
+const std::vector<std::tuple<std::string, int, int, std::string>> kC3Set = {
+    {"proto", 1, 3, "udp"}, {"net", 2, 2, "10.0.0.0/8"}, {"ports", 3, 1, "1000-2000"}};
+
+template <class F>
+void add_set(F& f) {
+    for (auto& [name, type, prio, expr] : kC3Set) {
+        PacketFilter::FilterConfig c;
+        c.type = static_cast<PacketFilter::FilterType>(type);
+        c.priority = prio;
+        c.expression = expr;
+        f.addFilter(name, c);
+    }
+}
+
+void line(const char* surface, const Capture& c, int threads, double pps, const std::string& extra = "") {
+    std::printf("{\"surface\": \"%s\", \"config\": \"%s\", \"threads\": %d, \"mpps\": %.4f, \"packets\": %zu%s%s}\n",
+                surface, c.name, threads, pps / 1e6, c.packets.size(), extra.empty() ? "" : ", ", extra.c_str());
+    std::fflush(stdout);
+}
+
+// The reference's batch entry on T threads, each with its own PacketFilter and shard.
+void bench_ref(const Capture& c, int threads, double seconds) {
+    std::atomic<uint64_t> done{0};
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    const auto t0 = Clock::now();
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            PacketFilter pf;
+            add_set(pf);
+            const size_t lo = c.packets.size() * t / threads, hi = c.packets.size() * (t + 1) / threads;
+            const std::vector<Packet> shard(c.packets.begin() + lo, c.packets.begin() + hi);
+            const size_t chunk = 4096;
+            std::vector<Packet> part;
+            for (size_t at = 0; !stop.load(std::memory_order_relaxed); at = (at + chunk) % shard.size()) {
+                part.assign(shard.begin() + at, shard.begin() + std::min(shard.size(), at + chunk));
+                auto r = pf.applyFilters(part);
+                done += r.size();
+                if (t == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+            }
+        });
+    for (auto& x : th) x.join();
+    const double el = secs(t0, Clock::now());
+    line("ref PacketFilter::applyFilters(vector<Packet>)", c, threads, done / el,
+         "\"seconds\": " + std::to_string(el));
+}
+
+void bench_gpu_filter(const Capture& c, double seconds, const char* which) {
+    GpuPacketFilter f;
+    add_set(f);
+    const bool apply = std::strcmp(which, "apply") == 0;
+    // warm-up: device init, program compile, staging allocation
+    if (apply) (void)f.applyFilters(c.packets);
+    else (void)f.classify(c.packets);
+    uint64_t done = 0, passed = 0;
+    double dev_s = 0, host_s = 0;
+    const auto t0 = Clock::now();
+    while (secs(t0, Clock::now()) < seconds) {
+        if (apply) {
+            auto r = f.applyFilters(c.packets);
+            done += r.size();
+            passed += r.empty() ? 0 : r[0].passed;
+        } else {
+            auto v = f.classify(c.packets);
+            done += v.decide.size();
+            passed += v.pass_idx.size();
+        }
+        const auto tm = f.lastBatchTiming();
+        dev_s += tm.device_s;
+        host_s += tm.host_s;
+    }
+    const double el = secs(t0, Clock::now());
+    char extra[256];
+    std::snprintf(extra, sizeof(extra), "\"devices\": %u, \"device_pass_s\": %.4f, \"host_post_s\": %.4f, "
+                  "\"seconds\": %.3f", f.deviceCount(), dev_s, host_s, el);
+    line(apply ? "GpuPacketFilter::applyFilters(vector<Packet>) -> vector<FilterResult>"
+               : "GpuPacketFilter::classify(vector<Packet>)",
+         c, 0, done / el, extra);
+    (void)passed;
+}
+
+void bench_plugin(const Capture& c, int threads, const char* so) {
+    void* h = dlopen(so, RTLD_LAZY);
+    if (!h) {
+        std::fprintf(stderr, "dlopen %s: %s\n", so, dlerror());
+        std::exit(3);
+    }
+    auto create = reinterpret_cast<beatrice::IPacketPlugin* (*)()>(dlsym(h, "createPlugin"));
+    auto set_sink = reinterpret_cast<void (*)(gpu_plugin*, gpu_verdict_sink_fn, void*)>(dlsym(h, "gpu_plugin_set_sink"));
+    auto flush = reinterpret_cast<void (*)(gpu_plugin*)>(dlsym(h, "gpu_plugin_flush"));
+    setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|3|udp;net|IP_RANGE|2|10.0.0.0/8;ports|PORT_RANGE|1|1000-2000;", 1);
+    if (!getenv("BEATRICE_GPU_BATCH")) setenv("BEATRICE_GPU_BATCH", "65536", 1);
+    beatrice::IPacketPlugin* p = create();
+    p->onStart();
+    std::atomic<uint64_t> seen{0};
+    set_sink(p, [](void* u, const gpu_verdict_batch* b) { *static_cast<std::atomic<uint64_t>*>(u) += b->n; }, &seen);
+    auto feed = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            Packet pk = c.packets[i];
+            try {
+                p->onPacket(pk);   // PluginManager::processPacket (src/PluginManager.cpp:158-171)
+            } catch (const std::exception&) {
+            }
+        }
+    };
+    feed(0, std::min<size_t>(c.packets.size(), 70000));   // warm-up: device init
+    flush(p);
+    while (seen < std::min<size_t>(c.packets.size(), 70000)) std::this_thread::yield();
+    seen = 0;
+    const auto t0 = Clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] { feed(c.packets.size() * t / threads, c.packets.size() * (t + 1) / threads); });
+    for (auto& x : th) x.join();
+    const auto t_fed = Clock::now();
+    flush(p);
+    while (seen < c.packets.size()) std::this_thread::yield();
+    const auto t1 = Clock::now();
+    char extra[160];
+    std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"batch\": %s", secs(t0, t_fed),
+                  secs(t0, t1), getenv("BEATRICE_GPU_BATCH"));
+    line("plugin onPacket -> verdict sink", c, threads, c.packets.size() / secs(t0, t1), extra);
+    p->onStop();
+    set_sink(p, nullptr, nullptr);
+    delete p;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string what = argc > 1 ? argv[1] : "all";
+    uint32_t n2 = 1u << 22, n3 = 1u << 21;
+    double seconds = 3.0;
+    int threads = usable_cpus();
+    const char* so = "beatrice_amd/libgpu_parse_filter_plugin.so";
+    for (int i = 2; i + 1 < argc; i += 2) {
+        if (!std::strcmp(argv[i], "--packets")) n2 = n3 = (uint32_t)std::atol(argv[i + 1]);
+        else if (!std::strcmp(argv[i], "--seconds")) seconds = std::atof(argv[i + 1]);
+        else if (!std::strcmp(argv[i], "--threads")) threads = std::atoi(argv[i + 1]);
+        else if (!std::strcmp(argv[i], "--plugin")) so = argv[i + 1];
+    }
+    std::fprintf(stderr, "surface_bench: %d usable CPUs\n", threads);
+    const Capture caps[2] = {capture("c2", 2, n2, 0xC2), capture("c3", 3, n3, 0xC3)};
+    for (const Capture& c : caps) {
+        if (what == "all" || what == "filter" || what == "ref") {
+            bench_ref(c, 1, seconds);
+            bench_ref(c, threads, seconds);
+        }
+        if (what == "all" || what == "filter") {
+            bench_gpu_filter(c, seconds, "apply");
+            bench_gpu_filter(c, seconds, "classify");
+        }
+        if (what == "all" || what == "plugin") {
+            bench_plugin(c, 1, so);
+            bench_plugin(c, threads, so);
+        }
+    }
+    return 0;
+}
