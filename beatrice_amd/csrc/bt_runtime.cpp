@@ -1138,6 +1138,12 @@ int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
     return BT_OK;
 }
 
+int bt_host_parallel(bt_ctx* c, void (*fn)(void*, uint32_t, uint32_t), void* user) {
+    if (!c || !fn) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    bt::host_parallel(c, [&](unsigned w, unsigned T) { fn(user, w, T); });
+    return BT_OK;
+}
+
 int bt_stream_create(bt_ctx* c, void** stream) {
     if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));

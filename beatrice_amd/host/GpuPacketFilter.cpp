@@ -14,6 +14,8 @@ namespace gpu {
 
 namespace {
 
+const std::string kPassedReason = "Packet passed all filters";   // src/PacketFilter.cpp:102-105
+
 uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 uint32_t be32(const uint8_t* p) { return (be16(p) << 16) | be16(p + 2); }
 
@@ -146,15 +148,6 @@ void GpuPacketFilter::resetStats() {
     stats_ = FilterStats{};
 }
 
-void GpuPacketFilter::updateStats(const std::string& filterName, bool passed, std::chrono::microseconds t) {
-    std::lock_guard<std::mutex> lock(statsMutex_);   // :374-386
-    stats_.packetsProcessed++;
-    if (passed) stats_.packetsPassed++;
-    else stats_.packetsDropped++;
-    stats_.totalProcessingTime += t;
-    stats_.filterCounts[filterName]++;
-}
-
 void GpuPacketFilter::compileLocked() {
     // The reference's own ordering (:63-73): enabled entries in unordered_map iteration
     // order, then std::sort by priority (descending). Same container, same calls.
@@ -178,9 +171,11 @@ void GpuPacketFilter::compileLocked() {
     uint32_t m = 0;
     bt_filter_program(ctx_, slots.data(), BT_MAX_FILTERS, &m);
     program_.clear();
+    rejectReason_.clear();
     for (uint32_t k = 0; k < m; ++k) {
         const auto& src = sortedFilters[slots[k].source_index];
         program_.push_back(Slot{src.first, src.second, slots[k]});
+        rejectReason_.push_back("Filter " + src.first + " rejected packet");   // :106-110
     }
     dirty_ = false;
 }
@@ -226,25 +221,114 @@ uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
     return (BT_DECIDE_PASS << 6) | (program_.empty() ? 0u : (uint32_t)program_.size() - 1);
 }
 
+namespace {
+
+// fn(lo, hi) over [0, n) split across the context's host threads (bt_host_parallel).
+template <class Fn>
+void parallel_ranges(bt_ctx* ctx, size_t n, Fn&& fn) {
+    struct U {
+        Fn* fn;
+        size_t n;
+    } u{&fn, n};
+    bt_host_parallel(ctx, [](void* p, uint32_t w, uint32_t T) {
+        auto* x = static_cast<U*>(p);
+        const size_t lo = x->n * w / T, hi = x->n * (w + 1) / T;
+        if (lo < hi) (*x->fn)(lo, hi);
+    }, &u);
+}
+
+}  // namespace
+
 void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
                                std::vector<bt_rec>* records) {
     const uint32_t n = (uint32_t)packets.size();
-    std::vector<const uint8_t*> ptrs(n);
-    std::vector<uint32_t> lens(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        ptrs[i] = packets[i].data();
-        lens[i] = (uint32_t)packets[i].length();
-    }
-    decide.assign(n, 0);
+    ptrs_.resize(n);
+    lens_.resize(n);
+    parallel_ranges(ctx_, n, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            ptrs_[i] = packets[i].data();
+            lens_[i] = (uint32_t)packets[i].length();
+        }
+    });
+    decide.resize(n);
     if (records) records->resize(n);
-    if (bt_group_parse_filter_ptrs(group_, ptrs.data(), lens.data(), n, records ? records->data() : nullptr, nullptr,
+    if (bt_group_parse_filter_ptrs(group_, ptrs_.data(), lens_.data(), n, records ? records->data() : nullptr, nullptr,
                                    decide.data(), nullptr, nullptr) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
 }
 
+// The host's pass over a batch's decisions, in packet order: PAYLOAD / CUSTOM slots the
+// device handed over are resumed here (serially: a CUSTOM callback is the caller's code),
+// and the stats are tallied per deciding slot, to be applied once (flushTally). `onThrow`
+// decides what a throwing packet does: stop the scan there (applyFilters / classify, which
+// rethrow after the earlier packets' stats, as the reference's per-packet loop does) or
+// record it and go on (classifyPerPacket).
+struct GpuPacketFilter::Tally {
+    uint64_t counted = 0, passed = 0;
+    std::vector<uint64_t> rejected;
+    size_t stop = 0;        // packets scanned (== n unless a throw stopped the scan)
+    bool threw = false;
+};
+
+GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
+                                            std::vector<uint32_t>* pass_idx, std::vector<uint32_t>* error_idx) {
+    Tally t;
+    t.rejected.assign(program_.size() + 1, 0);
+    const size_t n = packets.size();
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t d = decide[i];
+        if ((d >> 6) == BT_DECIDE_HOST) {
+            if (error_idx) {
+                try {
+                    d = resolveHost(packets[i], d & 63u);
+                } catch (...) {   // a CUSTOM callback threw for this packet
+                    d = (BT_DECIDE_THROW << 6) | (d & 63u);
+                }
+            } else {
+                d = resolveHost(packets[i], d & 63u);
+            }
+            decide[i] = (uint8_t)d;
+        }
+        const uint32_t code = d >> 6, slot = d & 63u;
+        if (code == BT_DECIDE_THROW) {
+            if (!error_idx) {
+                t.stop = i;
+                t.threw = true;
+                return t;
+            }
+            error_idx->push_back((uint32_t)i);
+            continue;
+        }
+        ++t.counted;
+        if (code == BT_DECIDE_PASS) {
+            ++t.passed;
+            if (pass_idx) pass_idx->push_back((uint32_t)i);
+        } else {
+            ++t.rejected[slot];
+        }
+    }
+    t.stop = n;
+    return t;
+}
+
+// updateStats (src/PacketFilter.cpp:374-386) for every counted packet of the tally at once.
+void GpuPacketFilter::flushTally(const Tally& t, std::chrono::microseconds per) {
+    std::lock_guard<std::mutex> lock(statsMutex_);
+    stats_.packetsProcessed += t.counted;
+    stats_.packetsPassed += t.passed;
+    stats_.packetsDropped += t.counted - t.passed;
+    stats_.totalProcessingTime += per * (int64_t)t.counted;
+    if (program_.empty()) {   // FilterResult::filterName stays "" (:102-111)
+        if (t.counted) stats_.filterCounts[""] += t.counted;
+        return;
+    }
+    if (t.passed) stats_.filterCounts[program_.back().name] += t.passed;
+    for (size_t s = 0; s < program_.size(); ++s)
+        if (t.rejected[s]) stats_.filterCounts[program_[s].name] += t.rejected[s];
+}
+
 std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const std::vector<Packet>& packets) {
     std::vector<FilterResult> results;
-    results.reserve(packets.size());
     std::lock_guard<std::mutex> lock(filtersMutex_);
     if (dirty_) compileLocked();
     if (packets.empty()) return results;
@@ -255,26 +339,30 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
-    for (size_t i = 0; i < packets.size(); ++i) {
-        uint32_t d = decide[i];
-        if ((d >> 6) == BT_DECIDE_HOST) d = resolveHost(packets[i], d & 63u);
-        const uint32_t code = d >> 6, slot = d & 63u;
-        if (code == BT_DECIDE_THROW) rethrow(program_[slot]);   // earlier packets are already counted
-        FilterResult r;
-        r.passed = code == BT_DECIDE_PASS;
-        if (!program_.empty()) {   // :102-111
-            if (r.passed) {
-                r.filterName = program_.back().name;
-                r.reason = "Packet passed all filters";
-            } else {
-                r.filterName = program_[slot].name;
-                r.reason = "Filter " + r.filterName + " rejected packet";
+    const Tally t = scan(packets, decide, nullptr, nullptr);
+    // The FilterResults of the packets before any throw (:102-111), built on the host
+    // threads from per-slot strings made once per program: the reference's vector is the
+    // result either way, its strings are copied rather than concatenated per packet.
+    results.resize(t.stop);
+    parallel_ranges(ctx_, t.stop, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            FilterResult& r = results[i];
+            const uint32_t code = decide[i] >> 6, slot = decide[i] & 63u;
+            r.passed = code == BT_DECIDE_PASS;
+            if (!program_.empty()) {
+                if (r.passed) {
+                    r.filterName = program_.back().name;
+                    r.reason = kPassedReason;
+                } else {
+                    r.filterName = program_[slot].name;
+                    r.reason = rejectReason_[slot];
+                }
             }
+            r.processingTime = per;
         }
-        r.processingTime = per;
-        updateStats(r.filterName, r.passed, per);
-        results.push_back(std::move(r));
-    }
+    });
+    flushTally(t, per);
+    if (t.threw) rethrow(program_[decide[t.stop] & 63u]);   // earlier packets are counted
     timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return results;
 }
@@ -294,16 +382,9 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
-    const std::string none;
-    for (size_t i = 0; i < packets.size(); ++i) {
-        uint32_t d = v.decide[i];
-        if ((d >> 6) == BT_DECIDE_HOST) v.decide[i] = (uint8_t)(d = resolveHost(packets[i], d & 63u));
-        const uint32_t code = d >> 6, slot = d & 63u;
-        if (code == BT_DECIDE_THROW) rethrow(program_[slot]);
-        const bool passed = code == BT_DECIDE_PASS;
-        if (passed) v.pass_idx.push_back((uint32_t)i);
-        updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
-    }
+    const Tally t = scan(packets, v.decide, &v.pass_idx, nullptr);
+    flushTally(t, per);
+    if (t.threw) rethrow(program_[v.decide[t.stop] & 63u]);
     timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return v;
 }
@@ -319,26 +400,8 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<P
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
-    const std::string none;
-    for (size_t i = 0; i < packets.size(); ++i) {
-        uint32_t d = v.decide[i];
-        if ((d >> 6) == BT_DECIDE_HOST) {
-            try {
-                d = resolveHost(packets[i], d & 63u);
-            } catch (...) {   // a CUSTOM callback threw for this packet
-                d = (BT_DECIDE_THROW << 6) | (d & 63u);
-            }
-            v.decide[i] = (uint8_t)d;
-        }
-        const uint32_t code = d >> 6, slot = d & 63u;
-        if (code == BT_DECIDE_THROW) {
-            v.error_idx.push_back((uint32_t)i);
-            continue;
-        }
-        const bool passed = code == BT_DECIDE_PASS;
-        if (passed) v.pass_idx.push_back((uint32_t)i);
-        updateStats(program_.empty() ? none : (passed ? program_.back().name : program_[slot].name), passed, per);
-    }
+    const Tally t = scan(packets, v.decide, &v.pass_idx, &v.error_idx);
+    flushTally(t, per);
     timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return v;
 }

@@ -119,7 +119,10 @@ private:
     uint32_t resolveHost(const Packet& p, uint32_t first_slot);
     [[noreturn]] void rethrow(const Slot& s) const;
     void runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide, std::vector<bt_rec>* records = nullptr);
-    void updateStats(const std::string& filterName, bool passed, std::chrono::microseconds t);
+    struct Tally;
+    Tally scan(const std::vector<Packet>& packets, std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
+               std::vector<uint32_t>* error_idx);
+    void flushTally(const Tally& t, std::chrono::microseconds per);
 
     void open(const std::vector<int>& devices, const bt_opts* opts);
 
@@ -131,6 +134,9 @@ private:
     mutable std::mutex statsMutex_;
     bool dirty_ = true;
     std::vector<Slot> program_;
+    std::vector<std::string> rejectReason_;   // per slot: "Filter <name> rejected packet"
+    std::vector<const uint8_t*> ptrs_;        // runBatch's gather list, reused across batches
+    std::vector<uint32_t> lens_;
     BatchTiming timing_;
 };
 

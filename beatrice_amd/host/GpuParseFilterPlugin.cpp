@@ -55,14 +55,14 @@ public:
         stopFlusher();
         {
             std::lock_guard<std::mutex> g(gpu_mu_);
-            std::lock_guard<std::mutex> lk(mu_);
-            const int device = env_int("BEATRICE_GPU_DEVICE", 0);
             batch_ = (size_t)std::max(1, env_int("BEATRICE_GPU_BATCH", 65536));
             records_ = env_int("BEATRICE_GPU_RECORDS", 0) != 0;
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
-            filter_ = std::make_unique<GpuPacketFilter>(device);
+            filter_ = std::make_unique<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
-            pending_.reserve(batch_);
+        }
+        {
+            std::lock_guard<std::mutex> lk(flush_mu_);
             stop_ = false;
         }
         flusher_ = std::thread([this] { flushLoop(); });
@@ -75,27 +75,37 @@ public:
         filter_.reset();
     }
 
-    // onPacket may run on several context threads at once (src/BeatriceContext.cpp:215-278).
-    // A full batch is swapped out under mu_ and classified outside it, so the other
-    // threads keep appending to a fresh batch while the GPU works.
+    // onPacket runs on several context threads at once (src/BeatriceContext.cpp:215-278).
+    // Each thread appends to its own shard of the pending batch (its lock is contended only
+    // by the flush thread), so the threads do not serialise on one lock per packet: with a
+    // single pending vector, 16 threads ran at 1.1 Mpps against 8.6 Mpps for one
+    // (tools/surfaces, round 3). A full shard is classified outside its lock, by the thread
+    // that filled it, while the others keep appending.
     void onPacket(Packet& packet) override {
         if (!enabled_) return;
+        Shard& sh = shards_[shardOfThisThread()];
         std::vector<Packet> full;
         uint64_t seq = 0;
+        bool armed = false;
         {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (pending_.empty()) {
-                first_ = std::chrono::steady_clock::now();
-                cv_.notify_one();              // the flush thread arms this batch's deadline
+            std::lock_guard<std::mutex> lk(sh.mu);
+            if (sh.pending.empty()) {
+                sh.first.store(Clock::now().time_since_epoch().count(), std::memory_order_relaxed);
+                armed = true;
             }
-            pending_.push_back(packet);        // shares the immutable bytes, no copy
-            if (pending_.size() >= batch_) seq = takeLocked(full);
+            sh.pending.push_back(packet);        // shares the immutable bytes, no copy
+            if (sh.pending.size() >= batch_) seq = takeLocked(sh, full);
+        }
+        if (armed && full.empty()) {             // the flush thread arms this shard's deadline
+            std::lock_guard<std::mutex> lk(flush_mu_);
+            ++armed_;
+            cv_.notify_one();
         }
         if (!full.empty()) classifyBatch(full, seq);
     }
 
     std::string getName() const override { return "gpu_parse_filter"; }
-    std::string getVersion() const override { return "1.1.0"; }
+    std::string getVersion() const override { return "1.2.0"; }
     std::string getDescription() const override {
         return "MI355X parse + PacketFilter stage (gfx950 kernels behind the beatrice_gpu C-ABI)";
     }
@@ -109,16 +119,18 @@ public:
         if (filter_) filter_->resetStats();
     }
 
-    // Classifies the partial batch now (the flush thread does this on its own after
+    // Classifies every partial shard now (the flush thread does this on its own after
     // BEATRICE_GPU_FLUSH_US).
     void flush() {
-        std::vector<Packet> full;
-        uint64_t seq = 0;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (!pending_.empty()) seq = takeLocked(full);
+        for (Shard& sh : shards_) {
+            std::vector<Packet> full;
+            uint64_t seq = 0;
+            {
+                std::lock_guard<std::mutex> lk(sh.mu);
+                if (!sh.pending.empty()) seq = takeLocked(sh, full);
+            }
+            if (!full.empty()) classifyBatch(full, seq);
         }
-        if (!full.empty()) classifyBatch(full, seq);
     }
 
     void setVerdictSink(Sink s) {
@@ -129,39 +141,70 @@ public:
     GpuPacketFilter* filter() { return filter_.get(); }
 
 private:
+    using Clock = std::chrono::steady_clock;
+    static constexpr size_t kShards = 32;
+    struct Shard {
+        std::mutex mu;
+        std::vector<Packet> pending;
+        std::atomic<int64_t> first{0};   // arrival of the pending batch's first packet (ticks)
+    };
+
     static int env_int(const char* k, int d) {
         const char* v = std::getenv(k);
         return v ? std::atoi(v) : d;
     }
 
-    // Hands the pending batch out with the next sequence number (mu_ held).
-    uint64_t takeLocked(std::vector<Packet>& out) {
-        out.swap(pending_);
-        pending_.reserve(batch_);
-        return next_seq_++;
+    static size_t shardOfThisThread() {
+        static std::atomic<size_t> next{0};
+        thread_local const size_t mine = next.fetch_add(1, std::memory_order_relaxed) % kShards;
+        return mine;
     }
 
-    // The flush thread: sleeps until the pending batch's deadline (first packet + flush_us)
-    // or a stop, and classifies a batch that is still partial then.
+    // Hands the shard's pending batch out with the next sequence number (sh.mu held).
+    uint64_t takeLocked(Shard& sh, std::vector<Packet>& out) {
+        out.swap(sh.pending);
+        sh.pending.reserve(std::min<size_t>(batch_, 4096));
+        sh.first.store(0, std::memory_order_relaxed);
+        return next_seq_.fetch_add(1);
+    }
+
+    // The flush thread: sleeps until the earliest deadline (first packet + flush_us) of any
+    // non-empty shard, or a stop, and classifies the shards still partial then.
     void flushLoop() {
-        std::unique_lock<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(flush_mu_);
         while (!stop_) {
-            if (pending_.empty()) {
-                cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
+            int64_t earliest = 0;
+            for (Shard& sh : shards_) {
+                const int64_t f = sh.first.load(std::memory_order_relaxed);
+                if (f && (!earliest || f < earliest)) earliest = f;
+            }
+            if (!earliest) {
+                const uint64_t seen = armed_;
+                cv_.wait(lk, [&] { return stop_ || armed_ != seen; });
                 continue;
             }
-            const auto deadline = first_ + std::chrono::microseconds(flush_us_);
-            if (std::chrono::steady_clock::now() < deadline) {
+            const auto deadline = Clock::time_point(Clock::duration(earliest)) + std::chrono::microseconds(flush_us_);
+            if (Clock::now() < deadline) {
                 cv_.wait_until(lk, deadline);
                 continue;
             }
-            std::vector<Packet> full;
-            const uint64_t seq = takeLocked(full);
             lk.unlock();
-            try {
-                classifyBatch(full, seq);
-            } catch (const std::exception&) {   // the device failed: nobody to throw to here
-                errors_ += full.size();
+            const int64_t due = (Clock::now() - std::chrono::microseconds(flush_us_)).time_since_epoch().count();
+            for (Shard& sh : shards_) {
+                const int64_t f = sh.first.load(std::memory_order_relaxed);
+                if (!f || f > due) continue;
+                std::vector<Packet> full;
+                uint64_t seq = 0;
+                {
+                    std::lock_guard<std::mutex> sl(sh.mu);
+                    if (!sh.pending.empty()) seq = takeLocked(sh, full);
+                }
+                if (full.empty()) continue;
+                try {
+                    classifyBatch(full, seq);
+                } catch (const std::exception&) {   // the device failed: nobody to throw to here
+                    errors_ += full.size();
+                }
             }
             lk.lock();
         }
@@ -169,7 +212,7 @@ private:
 
     void stopFlusher() {
         {
-            std::lock_guard<std::mutex> lk(mu_);
+            std::lock_guard<std::mutex> lk(flush_mu_);
             stop_ = true;
         }
         cv_.notify_all();
@@ -219,17 +262,18 @@ private:
         if (sink_) sink_(seq, batch, v);
     }
 
-    std::mutex mu_;                    // pending_, first_, next_seq_, stop_
-    std::condition_variable cv_;       // wakes the flush thread
+    Shard shards_[kShards];
+    std::mutex flush_mu_;              // stop_, armed_ (the flush thread's wake-ups)
+    std::condition_variable cv_;
+    uint64_t armed_ = 0;               // shards that went from empty to pending
     std::mutex gpu_mu_;                // filter_, sink_, done_seq_ (one batch on the device at a time)
     std::condition_variable order_cv_;
     std::unique_ptr<GpuPacketFilter> filter_;
-    std::vector<Packet> pending_;
-    std::chrono::steady_clock::time_point first_;
     size_t batch_ = 65536;
     int flush_us_ = 2000;
     bool records_ = false;
-    uint64_t next_seq_ = 0, done_seq_ = 0;
+    std::atomic<uint64_t> next_seq_{0};
+    uint64_t done_seq_ = 0;
     bool stop_ = true;
     std::thread flusher_;
     Sink sink_;

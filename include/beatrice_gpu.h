@@ -486,6 +486,10 @@ int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
 /* Waits for the context's stream and its compaction stream (bt_parse_filter_device_async). */
 int  bt_synchronize(bt_ctx* ctx);
+/* Runs fn(user, w, workers) once on each of the context's host threads (w = 0 .. workers-1,
+ * the caller is worker 0) and returns when all have: the pool that gathers and drains the
+ * host-batch pipeline, lent to host-side post-processing of a batch. */
+int  bt_host_parallel(bt_ctx* ctx, void (*fn)(void* user, uint32_t worker, uint32_t workers), void* user);
 /* Caller-owned streams on the context's device (a hipStream_t, non-blocking) for the
  * `stream` arguments above, for hosts that cannot create one themselves. Destroying a
  * stream waits for its work. */
