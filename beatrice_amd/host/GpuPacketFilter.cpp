@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <exception>
 #include <memory>
 #include <regex>
 #include <stdexcept>
@@ -267,7 +268,14 @@ struct GpuPacketFilter::Tally {
     uint64_t counted = 0, passed = 0;
     std::vector<uint64_t> rejected;
     size_t stop = 0;        // packets scanned (== n unless a throw stopped the scan)
-    bool threw = false;
+    bool threw = false;     // packet `stop` throws: its filter's std::stoi exception ...
+    std::exception_ptr ex;  // ... or the exception its CUSTOM callback threw
+    // after the stats of the packets before it are applied, as the reference's per-packet
+    // loop leaves them (src/PacketFilter.cpp:116, 121-130)
+    void rethrowIfAny(const GpuPacketFilter& f, const std::vector<uint8_t>& decide) const {
+        if (ex) std::rethrow_exception(ex);
+        if (threw) f.rethrow(f.program_[decide[stop] & 63u]);
+    }
 };
 
 GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
@@ -285,7 +293,13 @@ GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets,
                     d = (BT_DECIDE_THROW << 6) | (d & 63u);
                 }
             } else {
-                d = resolveHost(packets[i], d & 63u);
+                try {
+                    d = resolveHost(packets[i], d & 63u);
+                } catch (...) {
+                    t.stop = i;
+                    t.ex = std::current_exception();
+                    return t;
+                }
             }
             decide[i] = (uint8_t)d;
         }
@@ -362,7 +376,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
         }
     });
     flushTally(t, per);
-    if (t.threw) rethrow(program_[decide[t.stop] & 63u]);   // earlier packets are counted
+    t.rethrowIfAny(*this, decide);   // earlier packets are counted
     timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return results;
 }
@@ -384,7 +398,7 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
     timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
     const Tally t = scan(packets, v.decide, &v.pass_idx, nullptr);
     flushTally(t, per);
-    if (t.threw) rethrow(program_[v.decide[t.stop] & 63u]);
+    t.rethrowIfAny(*this, v.decide);
     timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     return v;
 }
