@@ -12,6 +12,7 @@
 #include <iomanip>
 #include <sstream>
 #include <stdexcept>
+#include <type_traits>
 
 namespace beatrice {
 namespace gpu {
@@ -264,6 +265,7 @@ GpuProtocolParser::GpuProtocolParser(const parser::ProtocolParser::ParserConfig&
     : config_(config) {
     if (bt_create(device, opts, &ctx_) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+    if (config_.enablePerformanceMetrics) profiling_ = true;   // :31-35
 }
 
 GpuProtocolParser::~GpuProtocolParser() { bt_destroy(ctx_); }
@@ -390,6 +392,143 @@ std::string to_string_of(const FieldValue& v) {
         return v.formatted.empty() ? "formatted" : v.formatted;
     default: return "unknown";
     }
+}
+
+// ---- the reference's ParseResult text, for any ParseResult ---------------------------
+// FieldValue::toHexString / toJsonString (src/parser/ParserResult.cpp:50-108) and
+// ParseResult::toJsonString / toXmlString / toCsvString / toHumanReadableString (:214-349),
+// restated on an appender: what ProtocolParser::formatPacket returns (ProtocolParser.cpp:
+// 145-157). bt_format_records writes the same text straight from GPU records for the
+// builtin walk; this one takes whatever ParseResult the caller holds (a user table's,
+// one the caller built or edited).
+struct Text {
+    std::string s;
+    Text& operator<<(const std::string& x) { s += x; return *this; }
+    Text& operator<<(const char* x) { s += x; return *this; }
+    Text& operator<<(char c) { s += c; return *this; }
+    template <class I, class = std::enable_if_t<std::is_integral_v<I>>>
+    Text& operator<<(I v) { s += std::to_string(v); return *this; }
+};
+
+std::string hex_string_of(const FieldValue& v) {   // toHexString (:50-64)
+    if (!v.valid) return "INVALID";
+    if (v.type != FieldValueType::BYTES) return v.rawHex;
+    const auto& b = std::get<std::vector<uint8_t>>(v.value);
+    static const char* d = "0123456789abcdef";
+    std::string s;
+    for (size_t i = 0; i < std::min(b.size(), size_t(16)); ++i) {
+        s += d[b[i] >> 4];
+        s += d[b[i] & 15];
+        s += ' ';
+    }
+    if (b.size() > 16) s += "...";
+    return s;
+}
+
+void value_json(const FieldValue& v, Text& o) {   // toJsonString (:66-108)
+    if (!v.valid) {
+        o << "null";
+        return;
+    }
+    o << "{\"type\":\"" << (int)v.type << "\",\"value\":";
+    switch (v.type) {
+    case FieldValueType::UINT8: case FieldValueType::UINT16: case FieldValueType::UINT32: case FieldValueType::UINT64:
+    case FieldValueType::INT8: case FieldValueType::INT16: case FieldValueType::INT32: case FieldValueType::INT64:
+    case FieldValueType::FLOAT32: case FieldValueType::FLOAT64: case FieldValueType::BOOLEAN:
+        o << to_string_of(v);
+        break;
+    case FieldValueType::STRING: o << '"' << std::get<std::string>(v.value) << '"'; break;
+    case FieldValueType::BYTES: o << '"' << hex_string_of(v) << '"'; break;
+    default: o << '"' << to_string_of(v) << '"'; break;
+    }
+    if (!v.rawHex.empty()) o << ",\"raw_hex\":\"" << v.rawHex << '"';
+    if (!v.formatted.empty()) o << ",\"formatted\":\"" << v.formatted << '"';
+    o << ",\"parse_time\":" << (long long)v.parseTime.count() << '}';
+}
+
+std::string result_text(const ParseResult& r, uint32_t fmt) {
+    Text o;
+    switch (fmt) {
+    case BT_FMT_JSON: {
+        o << "{\"status\":" << (int)r.status << ",\"protocol_name\":\"" << r.protocolName
+          << "\",\"protocol_version\":\"" << r.protocolVersion << "\",\"packet_length\":" << r.packetLength
+          << ",\"parsed_bytes\":" << r.parsedBytes << ",\"total_parse_time\":" << (long long)r.totalParseTime.count()
+          << ",\"total_validation_time\":" << (long long)r.totalValidationTime.count() << ",\"fields\":{";
+        bool first = true;
+        for (const auto& [name, v] : r.fields) {
+            if (!first) o << ',';
+            first = false;
+            o << '"' << name << "\":";
+            value_json(v, o);
+        }
+        o << "},\"validation_results\":[";
+        first = true;
+        for (const auto& vr : r.validationResults) {
+            if (!first) o << ',';
+            first = false;
+            o << "{\"field_name\":\"" << vr.fieldName << "\",\"valid\":" << (vr.valid ? "true" : "false")
+              << ",\"error_message\":\"" << vr.errorMessage << "\",\"validation_time\":"
+              << (long long)vr.validationTime.count() << '}';
+        }
+        o << ']';
+        if (!r.errorMessage.empty()) o << ",\"error_message\":\"" << r.errorMessage << '"';
+        o << '}';
+        break;
+    }
+    case BT_FMT_XML:
+        o << "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<parse_result>\n  <status>" << (int)r.status
+          << "</status>\n  <protocol_name>" << r.protocolName << "</protocol_name>\n  <protocol_version>"
+          << r.protocolVersion << "</protocol_version>\n  <packet_length>" << r.packetLength
+          << "</packet_length>\n  <parsed_bytes>" << r.parsedBytes << "</parsed_bytes>\n  <total_parse_time>"
+          << (long long)r.totalParseTime.count() << "</total_parse_time>\n  <total_validation_time>"
+          << (long long)r.totalValidationTime.count() << "</total_validation_time>\n  <fields>\n";
+        for (const auto& [name, v] : r.fields) {
+            o << "    <field name=\"" << name << "\">\n      <value>" << to_string_of(v) << "</value>\n      <type>"
+              << (int)v.type << "</type>\n";
+            if (!v.rawHex.empty()) o << "      <raw_hex>" << v.rawHex << "</raw_hex>\n";
+            o << "    </field>\n";
+        }
+        o << "  </fields>\n";
+        if (!r.validationResults.empty()) {
+            o << "  <validation_results>\n";
+            for (const auto& vr : r.validationResults) {
+                o << "    <result field=\"" << vr.fieldName << "\" valid=\"" << (vr.valid ? "true" : "false") << "\">\n";
+                if (!vr.errorMessage.empty()) o << "      <error>" << vr.errorMessage << "</error>\n";
+                o << "    </result>\n";
+            }
+            o << "  </validation_results>\n";
+        }
+        if (!r.errorMessage.empty()) o << "  <error_message>" << r.errorMessage << "</error_message>\n";
+        o << "</parse_result>";
+        break;
+    case BT_FMT_CSV:
+        o << "Field,Value,Type,Valid,ParseTime\n";
+        for (const auto& [name, v] : r.fields)
+            o << name << ',' << to_string_of(v) << ',' << (int)v.type << ',' << (v.valid ? "true" : "false") << ','
+              << (long long)v.parseTime.count() << '\n';
+        break;
+    default:   // human
+        o << "Protocol: " << r.protocolName << " v" << r.protocolVersion << "\nStatus: "
+          << (r.isSuccess() ? "SUCCESS" : "FAILED") << "\nPacket Length: " << r.packetLength
+          << " bytes\nParsed Bytes: " << r.parsedBytes << " bytes\nParse Time: " << (long long)r.totalParseTime.count()
+          << " \xce\xbcs\nValidation Time: " << (long long)r.totalValidationTime.count() << " \xce\xbcs\n\nFields:\n";
+        for (const auto& [name, v] : r.fields) {
+            o << "  " << name << ": " << to_string_of(v);
+            if (!v.formatted.empty()) o << " (" << v.formatted << ')';
+            o << '\n';
+        }
+        if (!r.validationResults.empty()) {
+            o << "\nValidation Results:\n";
+            for (const auto& vr : r.validationResults) {
+                o << "  " << vr.fieldName << ": " << (vr.valid ? "PASS" : "FAIL");
+                if (!vr.errorMessage.empty()) o << " - " << vr.errorMessage;
+                o << '\n';
+            }
+        }
+        if (!r.errorMessage.empty()) o << "\nError: " << r.errorMessage << '\n';
+        break;
+    }
+    return std::move(o.s);
 }
 
 bool validate_field(const FieldValue& v, const parser::FieldDefinition& f) {
@@ -590,7 +729,10 @@ std::vector<std::string> GpuProtocolParser::getSupportedProtocols() const {   //
     return names;
 }
 
-void GpuProtocolParser::setConfig(const parser::ProtocolParser::ParserConfig& config) { config_ = config; }
+void GpuProtocolParser::setConfig(const parser::ProtocolParser::ParserConfig& config) {   // :163-168
+    config_ = config;
+    if (config_.enablePerformanceMetrics) profiling_ = true;
+}
 
 GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets,
                                            const parser::ProtocolDefinition& protocol) {
@@ -674,6 +816,89 @@ bool GpuProtocolParser::validatePacket(const std::vector<uint8_t>& packet, const
 
 bool GpuProtocolParser::validatePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol) {
     return parsePacket(packet, protocol).isSuccess();
+}
+
+// ---- the rest of ProtocolParser's surface (include/parser/ProtocolParser.hpp:56-93) ----
+
+std::unique_ptr<GpuProtocolParser> GpuProtocolParser::create(const parser::ProtocolParser::ParserConfig& config,
+                                                             int device, const bt_opts* opts) {   // :10-12
+    return std::make_unique<GpuProtocolParser>(config, device, opts);
+}
+
+std::string GpuProtocolParser::formatPacket(const ParseResult& result, const std::string& format) {   // :145-157
+    const uint32_t fmt = format == "xml" ? BT_FMT_XML : format == "csv" ? BT_FMT_CSV
+                       : format == "human" ? BT_FMT_HUMAN : BT_FMT_JSON;   // anything else: json
+    return result_text(result, fmt);
+}
+
+std::vector<uint8_t> GpuProtocolParser::serializePacket(const ParseResult& result) { return result.rawData; }   // :159-161
+
+std::vector<std::string> GpuProtocolParser::getSupportedFormats() const { return {"json", "xml", "csv", "human"}; }
+
+// :205-228. Like the reference, the callbacks are kept for the registered protocol and
+// nothing calls them (formatPacket does not consult them).
+bool GpuProtocolParser::addCustomValidator(const std::string& protocolName,
+                                           std::function<bool(const std::vector<uint8_t>&, const ParseResult&)> validator) {
+    std::unique_lock<std::shared_mutex> lk(protocols_mu_);
+    if (protocols_.find(protocolName) == protocols_.end()) return false;
+    customValidators_[protocolName] = std::move(validator);
+    return true;
+}
+
+bool GpuProtocolParser::addCustomFormatter(const std::string& protocolName,
+                                           std::function<std::string(const ParseResult&)> formatter) {
+    std::unique_lock<std::shared_mutex> lk(protocols_mu_);
+    if (protocols_.find(protocolName) == protocols_.end()) return false;
+    customFormatters_[protocolName] = std::move(formatter);
+    return true;
+}
+
+// ProtocolParser::bytesToHex / formatMacAddress / formatIPv4Address / formatIPv6Address /
+// formatTimestamp (:591-640)
+std::string GpuProtocolParser::bytesToHex(const std::vector<uint8_t>& bytes) const { return hex(bytes.data(), bytes.size()); }
+std::string GpuProtocolParser::formatMacAddress(const std::vector<uint8_t>& bytes) const { return fmt_mac(bytes); }
+std::string GpuProtocolParser::formatIPv4Address(const std::vector<uint8_t>& bytes) const {
+    return bytes.size() == 4 ? fmt_ipv4(bytes.data()) : "invalid";
+}
+std::string GpuProtocolParser::formatIPv6Address(const std::vector<uint8_t>& bytes) const {
+    return bytes.size() == 16 ? fmt_ipv6(bytes.data()) : "invalid";
+}
+std::string GpuProtocolParser::formatTimestamp(uint64_t timestamp) const { return fmt_ts(timestamp); }
+
+// ParserBuilder (:642-738)
+GpuParserBuilder& GpuParserBuilder::withValidation(bool e) { config_.enableValidation = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withChecksumValidation(bool e) { config_.enableChecksumValidation = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withFieldConstraints(bool e) { config_.enableFieldConstraints = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withCustomValidators(bool e) { config_.enableCustomValidators = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withPerformanceMetrics(bool e) { config_.enablePerformanceMetrics = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withFieldCaching(bool e) { config_.enableFieldCaching = e; return *this; }
+GpuParserBuilder& GpuParserBuilder::withMaxFieldCacheSize(size_t n) { config_.maxFieldCacheSize = n; return *this; }
+GpuParserBuilder& GpuParserBuilder::withMaxValidationErrors(size_t n) { config_.maxValidationErrors = n; return *this; }
+GpuParserBuilder& GpuParserBuilder::withMaxParseTime(std::chrono::microseconds t) { config_.maxParseTime = t; return *this; }
+GpuParserBuilder& GpuParserBuilder::withErrorCallback(std::function<void(const std::string&)> cb) {
+    config_.errorCallback = std::move(cb);
+    return *this;
+}
+GpuParserBuilder& GpuParserBuilder::withWarningCallback(std::function<void(const std::string&)> cb) {
+    config_.warningCallback = std::move(cb);
+    return *this;
+}
+GpuParserBuilder& GpuParserBuilder::withInfoCallback(std::function<void(const std::string&)> cb) {
+    config_.infoCallback = std::move(cb);
+    return *this;
+}
+GpuParserBuilder& GpuParserBuilder::withProtocol(const parser::ProtocolDefinition& p) {
+    protocols_.push_back(p);
+    return *this;
+}
+GpuParserBuilder& GpuParserBuilder::withProtocols(const std::vector<parser::ProtocolDefinition>& ps) {
+    protocols_.insert(protocols_.end(), ps.begin(), ps.end());
+    return *this;
+}
+std::unique_ptr<GpuProtocolParser> GpuParserBuilder::build(int device, const bt_opts* opts) {
+    auto p = std::make_unique<GpuProtocolParser>(config_, device, opts);
+    for (const auto& proto : protocols_) p->registerProtocol(proto);   // duplicates: the first stays
+    return p;
 }
 
 }  // namespace gpu

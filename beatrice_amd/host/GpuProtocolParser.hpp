@@ -31,8 +31,11 @@
 // raise SIGFPE in the stats (the reference divides by successfulParses).
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -130,6 +133,25 @@ public:
     GpuProtocolParser(const GpuProtocolParser&) = delete;
     GpuProtocolParser& operator=(const GpuProtocolParser&) = delete;
 
+    // ---- factories (ProtocolParser.hpp:56-58, ProtocolParser.cpp:10-29) ----
+    static std::unique_ptr<GpuProtocolParser> create(
+        const parser::ProtocolParser::ParserConfig& config = parser::ProtocolParser::ParserConfig{}, int device = 0,
+        const bt_opts* opts = nullptr);
+    // Registers each named protocol the registry holds, skipping the others, as the
+    // reference does with its ProtocolRegistry singleton: pass
+    // parser::ProtocolRegistry::getInstance() (or anything with hasProtocol / getProtocol).
+    template <class Registry>
+    static std::unique_ptr<GpuProtocolParser> createWithProtocols(const std::vector<std::string>& protocolNames,
+                                                                  const parser::ProtocolParser::ParserConfig& config,
+                                                                  Registry& registry, int device = 0,
+                                                                  const bt_opts* opts = nullptr) {
+        auto p = create(config, device, opts);
+        for (const auto& name : protocolNames)
+            if (registry.hasProtocol(name))
+                if (const parser::ProtocolDefinition* def = registry.getProtocol(name)) p->registerProtocol(*def);
+        return p;
+    }
+
     // ---- builtin layer walk (Ethernet / VLAN / IPv4 / IPv6 / TCP / UDP / ICMP) ----
     GpuParsedBatch parseBatch(const std::vector<Packet>& packets);
     // borrows `base` for the lifetime of the returned batch
@@ -147,6 +169,28 @@ public:
     bool validatePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol);
     void setConfig(const parser::ProtocolParser::ParserConfig& config);
     const parser::ProtocolParser::ParserConfig& getConfig() const { return config_; }
+
+    // ---- text and bytes of a ParseResult (ProtocolParser.hpp:74-75, 84-89) ----
+    // formatPacket: the reference's ParseResult::toJsonString / toXmlString / toCsvString /
+    // toHumanReadableString for "json" / "xml" / "csv" / "human", json for anything else,
+    // for any ParseResult (a GpuParsedBatch layer, a GpuFieldBatch result, one of the
+    // caller's). serializePacket: its rawData.
+    std::string formatPacket(const parser::ParseResult& result, const std::string& format = "json");
+    std::vector<uint8_t> serializePacket(const parser::ParseResult& result);
+    std::vector<std::string> getSupportedFormats() const;
+    // false unless the protocol is registered; kept, and (as in the reference) not called
+    bool addCustomValidator(const std::string& protocolName,
+                            std::function<bool(const std::vector<uint8_t>&, const parser::ParseResult&)> validator);
+    bool addCustomFormatter(const std::string& protocolName,
+                            std::function<std::string(const parser::ParseResult&)> formatter);
+    void clearCache() {}   // the GPU path keeps no field cache
+    void enableProfiling(bool enable) { profiling_ = enable; }
+    bool isProfilingEnabled() const { return profiling_; }
+    std::string bytesToHex(const std::vector<uint8_t>& bytes) const;
+    std::string formatMacAddress(const std::vector<uint8_t>& bytes) const;
+    std::string formatIPv4Address(const std::vector<uint8_t>& bytes) const;
+    std::string formatIPv6Address(const std::vector<uint8_t>& bytes) const;
+    std::string formatTimestamp(uint64_t timestamp) const;
 
     // batch forms: one GPU pass per protocol over the whole batch
     GpuFieldBatch parseBatch(const std::vector<Packet>& packets, const parser::ProtocolDefinition& protocol);
@@ -172,10 +216,46 @@ private:
     bt_ctx* ctx_ = nullptr;
     parser::ProtocolParser::ParserConfig config_;
     std::unordered_map<std::string, parser::ProtocolDefinition> protocols_;   // as the reference's protocols_
+    std::unordered_map<std::string, std::function<bool(const std::vector<uint8_t>&, const parser::ParseResult&)>>
+        customValidators_;
+    std::unordered_map<std::string, std::function<std::string(const parser::ParseResult&)>> customFormatters_;
+    std::atomic<bool> profiling_{false};
     mutable std::shared_mutex protocols_mu_;
     mutable std::mutex stats_mu_;
     parser::ProtocolParser::ParserStats stats_;
     double time_carry_us_ = 0.0;   // sub-microsecond remainder of the amortised time
+};
+
+// ParserBuilder (include/parser/ProtocolParser.hpp:141-166) building a GpuProtocolParser.
+class GpuParserBuilder {
+public:
+    GpuParserBuilder& withValidation(bool enable);
+    GpuParserBuilder& withChecksumValidation(bool enable);
+    GpuParserBuilder& withFieldConstraints(bool enable);
+    GpuParserBuilder& withCustomValidators(bool enable);
+    GpuParserBuilder& withPerformanceMetrics(bool enable);
+    GpuParserBuilder& withFieldCaching(bool enable);
+    GpuParserBuilder& withMaxFieldCacheSize(size_t size);
+    GpuParserBuilder& withMaxValidationErrors(size_t max);
+    GpuParserBuilder& withMaxParseTime(std::chrono::microseconds time);
+    GpuParserBuilder& withErrorCallback(std::function<void(const std::string&)> callback);
+    GpuParserBuilder& withWarningCallback(std::function<void(const std::string&)> callback);
+    GpuParserBuilder& withInfoCallback(std::function<void(const std::string&)> callback);
+    GpuParserBuilder& withProtocol(const parser::ProtocolDefinition& protocol);
+    GpuParserBuilder& withProtocols(const std::vector<parser::ProtocolDefinition>& protocols);
+    // every protocol the registry holds, in its iteration order (ProtocolParser.cpp:716-728):
+    // pass parser::ProtocolRegistry::getInstance()
+    template <class Registry>
+    GpuParserBuilder& withBuiltinProtocols(Registry& registry) {
+        for (const auto& name : registry.getRegisteredProtocols())
+            if (const parser::ProtocolDefinition* def = registry.getProtocol(name)) protocols_.push_back(*def);
+        return *this;
+    }
+    std::unique_ptr<GpuProtocolParser> build(int device = 0, const bt_opts* opts = nullptr);
+
+private:
+    parser::ProtocolParser::ParserConfig config_;
+    std::vector<parser::ProtocolDefinition> protocols_;
 };
 
 }  // namespace gpu

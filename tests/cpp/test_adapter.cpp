@@ -9,6 +9,10 @@
 //   parser   GpuProtocolParser::layer(i, k) vs ProtocolParser::parsePacket(slice, name)
 //            for every walked layer: every ParseResult member but the wall-clock times,
 //            field iteration order included.
+//   surface  formatPacket (every format, builtin and user-table results, validation results),
+//            serializePacket, getSupportedFormats, addCustomFormatter / Validator, the
+//            address / hex / timestamp utilities, create / createWithProtocols / ParserBuilder
+//            over the reference's own ProtocolRegistry singleton.
 //   plugin   dlopen of libgpu_parse_filter_plugin.so through createPlugin(), the
 //            IPacketPlugin lifecycle, pass count vs the reference.
 // Prints one line per check; exit status 0 = all passed.
@@ -420,6 +424,142 @@ static bool user_proto_case(const char* label, const Capture& cap) {
     return true;
 }
 
+// ---- the rest of ProtocolParser's surface: formatPacket / serializePacket /
+// getSupportedFormats / addCustom* / utilities / create / createWithProtocols / ParserBuilder
+static bool surface_case(const char* label, const Capture& cap) {
+    using namespace beatrice::parser;
+    using beatrice::gpu::GpuProtocolParser;
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    ProtocolParser ref(cfg);
+    GpuProtocolParser gpu(cfg, 0);
+    for (auto p : {BuiltinProtocols::createEthernetProtocol(), BuiltinProtocols::createVLANProtocol(),
+                   BuiltinProtocols::createIPv4Protocol(), BuiltinProtocols::createIPv6Protocol(),
+                   BuiltinProtocols::createTCPProtocol(), BuiltinProtocols::createUDPProtocol(),
+                   BuiltinProtocols::createICMPProtocol()})
+        ref.registerProtocol(p);
+    const char* formats[] = {"json", "xml", "csv", "human", "yaml"};   // unknown: json
+    CHECK(ref.getSupportedFormats() == gpu.getSupportedFormats(), "%s: getSupportedFormats", label);
+    size_t ntext = 0;
+    // builtin walk: the GPU layer's text == the reference's text of its own result
+    auto batch = gpu.parseBatch(cap.packets);
+    for (size_t i = 0; i < cap.packets.size() && i < 3000; ++i) {
+        const uint8_t* f = cap.packets[i].data();
+        const size_t len = cap.packets[i].length();
+        const auto ls = batch.layers(i);
+        for (size_t k = 0; k < ls.size(); ++k) {
+            ParseResult want = ref.parsePacket(std::vector<uint8_t>(f + ls[k].offset, f + len), ls[k].name);
+            const ParseResult got = batch.layer(i, k);
+            for (const char* fm : formats) {
+                // the formatter restated over the reference's own result (wall-clock times included)
+                CHECK(ref.formatPacket(want, fm) == gpu.formatPacket(want, fm), "%s: packet %zu %s: formatPacket(%s) of "
+                      "the reference's result differs", label, i, ls[k].name.c_str(), fm);
+            }
+            for (auto& kv : want.fields) kv.second.parseTime = std::chrono::microseconds(0);
+            for (const char* fm : formats) {
+                CHECK(ref.formatPacket(want, fm) == gpu.formatPacket(got, fm), "%s: packet %zu %s: formatPacket(%s) "
+                      "of the GPU's result differs", label, i, ls[k].name.c_str(), fm);
+                ++ntext;
+            }
+            CHECK(ref.serializePacket(want) == gpu.serializePacket(got), "%s: packet %zu serializePacket", label, i);
+        }
+    }
+    // user tables with constraints (validation results and their messages in the text)
+    std::mt19937 rng(0x5FAC);
+    std::vector<ProtocolDefinition> defs{parser_example_protocol()};
+    for (int k = 0; k < 8; ++k) defs.push_back(random_protocol(rng, 100 + k));
+    ProtocolParser vref;   // validation and constraints on (the default config), metrics on
+    GpuProtocolParser vgpu(ProtocolParser::ParserConfig{}, 0);
+    for (const auto& d : defs) {
+        vref.registerProtocol(d);
+        vgpu.registerProtocol(d);
+        auto b = vgpu.parseBatch(cap.packets, d);
+        for (size_t i = 0; i < cap.packets.size() && i < 500; ++i) {
+            const std::vector<uint8_t> v(cap.packets[i].data(), cap.packets[i].data() + cap.packets[i].length());
+            ParseResult want = vref.parsePacket(v, d);
+            const ParseResult got = b.result(i);
+            for (const char* fm : formats)
+                CHECK(vref.formatPacket(want, fm) == vgpu.formatPacket(want, fm), "%s: %s packet %zu: formatPacket(%s) "
+                      "of the reference's result differs", label, d.name.c_str(), i, fm);
+            want.totalParseTime = want.totalValidationTime = std::chrono::microseconds(0);
+            for (auto& kv : want.fields) kv.second.parseTime = std::chrono::microseconds(0);
+            for (auto& vr : want.validationResults) vr.validationTime = std::chrono::microseconds(0);
+            for (const char* fm : formats) {
+                CHECK(vref.formatPacket(want, fm) == vgpu.formatPacket(got, fm), "%s: %s packet %zu: formatPacket(%s) "
+                      "of the GPU's result differs", label, d.name.c_str(), i, fm);
+                ++ntext;
+            }
+            CHECK(vref.serializePacket(want) == vgpu.serializePacket(got), "%s: %s serializePacket", label,
+                  d.name.c_str());
+        }
+    }
+    // custom validators / formatters: registered protocols only (neither is ever called)
+    auto fmt_cb = [](const ParseResult& r) { return r.protocolName; };
+    auto val_cb = [](const std::vector<uint8_t>&, const ParseResult&) { return false; };
+    CHECK(vref.addCustomFormatter("NOPE", fmt_cb) == vgpu.addCustomFormatter("NOPE", fmt_cb) &&
+              vref.addCustomFormatter(defs[1].name, fmt_cb) == vgpu.addCustomFormatter(defs[1].name, fmt_cb) &&
+              vref.addCustomValidator("NOPE", val_cb) == vgpu.addCustomValidator("NOPE", val_cb) &&
+              vref.addCustomValidator(defs[2].name, val_cb) == vgpu.addCustomValidator(defs[2].name, val_cb),
+          "%s: addCustomFormatter / addCustomValidator", label);
+    CHECK(vref.isProfilingEnabled() == vgpu.isProfilingEnabled() && ref.isProfilingEnabled() == gpu.isProfilingEnabled(),
+          "%s: isProfilingEnabled", label);
+    vref.enableProfiling(false);
+    vgpu.enableProfiling(false);
+    CHECK(vref.isProfilingEnabled() == vgpu.isProfilingEnabled(), "%s: enableProfiling", label);
+    // the utility methods
+    for (size_t len : {0, 4, 5, 6, 16, 17}) {
+        std::vector<uint8_t> b(len);
+        for (auto& x : b) x = (uint8_t)rng();
+        CHECK(ref.bytesToHex(b) == gpu.bytesToHex(b) && ref.formatMacAddress(b) == gpu.formatMacAddress(b) &&
+                  ref.formatIPv4Address(b) == gpu.formatIPv4Address(b) &&
+                  ref.formatIPv6Address(b) == gpu.formatIPv6Address(b),
+              "%s: address/hex utilities, %zu bytes", label, len);
+    }
+    for (uint64_t ts : {0ull, 1ull, 1700000000ull, 4102444800ull})
+        CHECK(ref.formatTimestamp(ts) == gpu.formatTimestamp(ts), "%s: formatTimestamp(%llu)", label,
+              (unsigned long long)ts);
+    // factories and the builder, over the reference's registry singleton
+    auto& registry = ProtocolRegistry::getInstance();
+    registry.loadBuiltinProtocols();
+    registry.registerProtocol(parser_example_protocol());
+    const std::vector<std::string> names = {"ethernet", "ipv4", "no_such", "udp", "CUSTOM_PROTO"};
+    auto r1 = ProtocolParser::createWithProtocols(names, cfg);
+    auto g1 = GpuProtocolParser::createWithProtocols(names, cfg, registry, 0);
+    CHECK(r1->getSupportedProtocols() == g1->getSupportedProtocols(), "%s: createWithProtocols protocols", label);
+    auto r2 = ProtocolParser::create(cfg);
+    auto g2 = GpuProtocolParser::create(cfg, 0);
+    CHECK(r2->getSupportedProtocols().empty() && g2->getSupportedProtocols().empty() &&
+              r2->isProfilingEnabled() == g2->isProfilingEnabled() &&
+              r2->getConfig().enablePerformanceMetrics == g2->getConfig().enablePerformanceMetrics,
+          "%s: create", label);
+    auto r3 = ParserBuilder().withValidation(false).withPerformanceMetrics(false).withMaxFieldCacheSize(7)
+                  .withProtocol(random_protocol(rng, 200)).withBuiltinProtocols().build();
+    CHECK(r3->getConfig().maxFieldCacheSize == 7, "builder config");
+    auto g3 = beatrice::gpu::GpuParserBuilder().withValidation(false).withPerformanceMetrics(false)
+                  .withMaxFieldCacheSize(7).withProtocols(std::vector<ProtocolDefinition>{})
+                  .withBuiltinProtocols(registry).build(0);
+    // the builder's protocols: the same registry walk (r3 also holds the random table)
+    std::vector<std::string> pr = r3->getSupportedProtocols(), pg = g3->getSupportedProtocols();
+    for (const auto& n : pg) CHECK(r3->hasProtocol(n), "%s: builder protocol %s", label, n.c_str());
+    CHECK(pr.size() == pg.size() + 1 && g3->getConfig().maxFieldCacheSize == 7 &&
+              g3->getConfig().enableValidation == r3->getConfig().enableValidation &&
+              g3->isProfilingEnabled() == r3->isProfilingEnabled(),
+          "%s: ParserBuilder (%zu / %zu protocols)", label, pr.size(), pg.size());
+    size_t nparse = 0;
+    for (size_t i = 0; i < cap.packets.size() && i < 200; ++i) {
+        const std::vector<uint8_t> v(cap.packets[i].data(), cap.packets[i].data() + cap.packets[i].length());
+        for (const char* n : {"ethernet", "ipv4", "udp", "CUSTOM_PROTO", "no_such"}) {
+            if (!same_result(label, i, r1->parsePacket(v, n), g1->parsePacket(v, n))) return false;
+            if (!same_result(label, i, r3->parsePacket(v, n), g3->parsePacket(v, n))) return false;
+            nparse += 2;
+        }
+    }
+    std::printf("ok   surface %-22s formatPacket x5 formats (%zu texts, builtin + user tables with validation), "
+                "serializePacket, formats, addCustom*, utilities, create / createWithProtocols / ParserBuilder "
+                "(%zu ParseResults)\n", label, ntext, nparse);
+    return true;
+}
+
 static bool plugin_case(const Capture& cap, const char* so) {
     setenv("BEATRICE_GPU_FILTERS", "proto|PROTOCOL|3|udp;net|IP_RANGE|2|10.0.0.0/8;ports|PORT_RANGE|1|1000-2000", 1);
     setenv("BEATRICE_GPU_BATCH", "4096", 1);
@@ -505,6 +645,8 @@ int main(int argc, char** argv) {
     ok &= parser_case("fuzz", fz);
     ok &= user_proto_case("fuzz", fz);
     ok &= user_proto_case("c3", c3);
+    ok &= surface_case("c4", c4);
+    ok &= surface_case("fuzz", fz);
     ok &= plugin_case(c3, plugin_so);
     std::printf("%s (%d failures)\n", ok && !g_fail ? "ALL OK" : "FAILED", g_fail);
     return ok && !g_fail ? 0 : 1;
