@@ -148,7 +148,7 @@ EXPORTS = [
     "bt_parse_filter_device_async",
     "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_host_parallel", "bt_stream_create", "bt_stream_synchronize", "bt_stream_destroy", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
-    "bt_ring_walk_tpv3", "bt_ring_release_tpv3",
+    "bt_ring_walk_tpv3", "bt_ring_release_tpv3", "bt_ring_walk_tpv3_gpu",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3",
@@ -213,6 +213,8 @@ def lib() -> ctypes.CDLL:
         "bt_ring_walk_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, u32,
                                              ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_ring_release_tpv3": (ctypes.c_int, [ctypes.POINTER(Tpv3Ring), u32, u32]),
+        "bt_ring_walk_tpv3_gpu": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), vp, u32, u32, vp, u32,
+                                                 ctypes.POINTER(u32), ctypes.POINTER(u32), vp, vp]),
         "bt_ring_gather_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
                                                ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
@@ -586,6 +588,21 @@ def ring_gather_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, slots: np
                                      slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base,
                                      cap, ctypes.byref(nd), ctypes.byref(nb)))
     return out[slot_base:slot_base + nd.value], nb.value
+
+
+def ring_walk_tpv3_gpu(ctx: "Context", ring: np.ndarray, ring_dev: int, block_size: int, n_blocks: int,
+                       desc_dev: int, cap: int, first: int = 0, max_blocks: int | None = None,
+                       bad_dev: int | None = None, stream=None):
+    """bt_ring_walk_tpv3_gpu: the host reads the ready blocks' headers, a kernel walks
+    their frame chains through ring_dev (the ring's registered alias) and writes the
+    descriptors into desc_dev (device memory). Returns (descriptors, blocks taken); the
+    descriptors are ready once the context stream (or `stream`) has run the walk."""
+    r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
+    nd, nb = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().bt_ring_walk_tpv3_gpu(ctx.h, ctypes.byref(r), ring_dev, first,
+                                       n_blocks if max_blocks is None else max_blocks, desc_dev, cap,
+                                       ctypes.byref(nd), ctypes.byref(nb), bad_dev, stream))
+    return nd.value, nb.value
 
 
 def ring_release_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int, count: int):

@@ -52,7 +52,14 @@ struct MainArgs {
     const uint8_t* dfa;        // PAYLOAD DFA pool (device), copied to dynamic LDS per block
     uint32_t dfa_bytes;        // 0: the program has no BT_K_PAYLOAD slot
     uint32_t prefixes;         // BT_BATCH_PREFIXES: base holds header prefixes only
+    uint32_t lean;             // descriptor mode: bytes of a frame round A reads at most (0xFFFF:
+                               // its first 64-B window); 46 for host-resident frames (kLeanPcie)
 };
+// Frames read over PCIe (registered host memory): round A reads the first 46 B of a
+// frame (Eth + IPv4 + UDP, and every filter gate), not the whole 64-B window; round B
+// fetches what a longer header needs. PCIe moves 64-B lines, and a frame at 2 mod 16 in
+// a TPACKET_V3 slot then touches 1.5 lines on average instead of 2.
+constexpr uint32_t kLeanPcie = 46;
 
 constexpr uint32_t kDfaPoolMax = 16384;   // bytes of DFA tables per program (LDS budget)
 
@@ -91,6 +98,25 @@ inline uint64_t read_limit(const void* base, uint64_t bytes) {
 // first one). Release builds return 0 without touching the device.
 uint32_t bounds_take_main(void* stream, BoundsLog* first);
 uint32_t bounds_take_extract(void* stream, BoundsLog* first);
+
+// ---- TPACKET_V3 frame-chain walk on the GPU (bt_ring_walk.hip) ----
+struct RingBlock {                    // one taken block, from its header (read by the host)
+    uint32_t block;                   // ring block index
+    uint32_t n;                       // num_pkts
+    uint32_t start;                   // index of its first descriptor
+    uint32_t first_off;               // offset_to_first_pkt
+};
+struct RingWalkArgs {
+    const uint8_t* ring;              // device-visible ring (bt_host_register alias)
+    uint64_t block_size;
+    const RingBlock* blocks;          // pinned host memory, read by the kernel
+    uint32_t count;
+    bt_pkt_desc* desc;                // device memory, cap entries
+    uint32_t cap;
+    uint32_t* bad;                    // optional: max(block + 1) of the malformed blocks
+};
+int launch_ring_walk(const RingWalkArgs& a, void* stream);
+uint32_t bounds_take_ring(void* stream, BoundsLog* first);
 
 // ---- user-defined protocol extraction (bt_extract.hip) ----
 constexpr uint32_t kExWindow = 256;   // bytes of each packet staged in LDS; fields past it read memory

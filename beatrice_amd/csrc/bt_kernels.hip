@@ -582,7 +582,7 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
             const bool live_q = p0 + q < a.n;
             // bytes from a0 this round may read: the frame; when wide, only up to the end
             // of a0's 128-B line (round B takes the next line, and only what is needed)
-            const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
+            const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + min(ql, a.lean);
             const bool ok = live_q && (16u * c < a_end) && (addr + 16u <= a.bytes);
             st.v[j] = ok ? ld16(a.base + addr, ntl) : make_uint4(0, 0, 0, 0);
             if (wide) {   // chunks 4..7 of the same line
@@ -690,7 +690,7 @@ __device__ __forceinline__ bool round_b(const MainArgs& a, uint32_t t, uint32_t 
                                        uint32_t* w0) {
     // bytes from a0 that round A read, and whether they hold what header_end reads
     const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s, my_len, need_max)
-                                     : min(64u, s + my_len);
+                                     : min(64u, s + min(my_len, a.lean));
     const bool cov = a_end >= s + min(my_len, 28u);
     const uint32_t end = !live ? 0u
                        : cov ? s + header_end(w0, my_len, kNeedFilter)
@@ -1006,7 +1006,7 @@ __device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t l
         const uint32_t sq = (uint32_t)qo & 15u;
         st.qa0[j] = a0;
         // bitwise & keeps the conditions branch-free (&& made exec-mask branches)
-        const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + ql;
+        const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + min(ql, a.lean);
         const bool ok = (16u * c < a_end) & (addr + 16u <= a.bytes);
         st.v[j] = ld16(ok ? a.base + addr : zero, ntl);
         if (wide) {

@@ -188,6 +188,8 @@ struct bt_ctx {
     bt_outputs tg_out{};
     uint32_t tg_iters = 0;
     int spin_rc = -1;                  // hipSetDeviceFlags(hipDeviceScheduleSpin) result
+    const void* last_base = nullptr;   // host_resident's one-entry cache
+    bool last_base_host = false;
     unsigned device_flags = 0;
 
     // bt_memcpy_h2d / bt_memcpy_d2h: two pinned chunks, so no copy of the caller's
@@ -196,6 +198,16 @@ struct bt_ctx {
     uint8_t* xfer_h[2] = {nullptr, nullptr};
     hipEvent_t xfer_ev[2] = {nullptr, nullptr};
     hipEvent_t xfer_after = nullptr;   // the compaction stream's tail (after_cstream)
+
+    // bt_ring_walk_tpv3_gpu: the taken blocks' headers, in pinned memory the kernel reads;
+    // two buffers, each reused once the walk that read it has run
+    struct WalkStage {
+        RingBlock* h = nullptr;
+        uint32_t cap = 0;
+        hipEvent_t done = nullptr;
+        bool used = false;
+    } walk[2];
+    int walk_next = 0;
 
     // bt_extract (host lists): pinned + device staging, grown on demand
     uint8_t* ex_h = nullptr;
@@ -295,6 +307,19 @@ int ensure_cstream(bt_ctx* c) {
     return BT_OK;
 }
 
+// Whether a batch's frames sit in host memory the device reads over PCIe (registered or
+// pinned). One pointer query per new base (a capture ring or UMEM is one base for its life).
+bool host_resident(bt_ctx* c, const void* base) {
+    if (base == c->last_base) return c->last_base_host;
+    hipPointerAttribute_t attr{};
+    bool host = false;
+    if (hipPointerGetAttributes(&attr, base) == hipSuccess) host = attr.type == hipMemoryTypeHost;
+    else (void)hipGetLastError();
+    c->last_base = base;
+    c->last_base_host = host;
+    return host;
+}
+
 // BT_DEBUG_BOUNDS builds: after a launch, wait and read the kernels' bounds logs
 // (bt_bounds.h); a failed check becomes BT_E_INTERNAL naming the first one.
 int check_bounds(hipStream_t st, hipStream_t cst, const char* what) {
@@ -375,6 +400,8 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (w ? w->verdict : nullptr);
     if (w && !o->verdict) { int rc = ws_touch(c, w, st); if (rc) return rc; }   // the main kernel writes w->verdict
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
+    a.lean = 0xFFFFu;
+    const bool lean = b->desc && !(c->opts.flags & BT_OPT_NO_LEAN_PCIE) && host_resident(c, b->base);
     a.dfa = c->dfa_dev[c->dfa_cur];
     a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
     // Cache policy (measured): non-temporal record stores everywhere (C2 +3..9 %,
@@ -388,6 +415,10 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
     if (c->opts.flags & BT_OPT_WIDE_ALWAYS) a.nt |= 8u;
+    if (lean && !(a.nt & 8u)) {   // frames over PCIe: lean round A, never the wide 128-B mode
+        a.lean = kLeanPcie;
+        a.nt |= 4u;
+    }
     int rec = kRecNone;
     if (o->records) {
         if (aos || (c->opts.flags & BT_OPT_RECORDS_AOS)) rec = kRecAoS;
@@ -576,6 +607,10 @@ void bt_destroy(bt_ctx* c) {
         if (c->xfer_ev[k]) (void)hipEventDestroy(c->xfer_ev[k]);
     }
     if (c->xfer_after) (void)hipEventDestroy(c->xfer_after);
+    for (auto& w : c->walk) {
+        if (w.h) (void)hipHostFree(w.h);
+        if (w.done) (void)hipEventDestroy(w.done);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1135,6 +1170,69 @@ int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
     if (int rc = after_cstream(c)) return rc;
     HIP_TRY(hipMemsetAsync(dst, value, bytes, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return BT_OK;
+}
+
+int bt_ring_walk_tpv3_gpu(bt_ctx* c, const bt_tpv3_ring* ring, const void* ring_dev, uint32_t first_block,
+                          uint32_t max_blocks, bt_pkt_desc* desc_dev, uint32_t cap, uint32_t* n_desc,
+                          uint32_t* n_blocks_taken, uint32_t* bad_dev, void* stream) {
+    if (!c || !ring || !ring->base || !ring_dev || !n_desc || !n_blocks_taken || (cap && !desc_dev))
+        return fail(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3_gpu: null argument");
+    if (!ring->n_blocks || ring->block_size < 48 || first_block >= ring->n_blocks)
+        return fail(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3_gpu: bad ring geometry");
+    *n_desc = 0;
+    *n_blocks_taken = 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    auto& w = c->walk[c->walk_next];
+    const uint32_t lim = std::min(max_blocks, ring->n_blocks);
+    if (w.used) HIP_TRY(hipEventSynchronize(w.done));   // the walk that last read this buffer has run
+    if (w.cap < lim) {
+        if (w.h) HIP_TRY(hipHostFree(w.h));
+        w.h = nullptr;
+        HIP_TRY(hipHostMalloc(&w.h, sizeof(RingBlock) * std::max(lim, 64u), hipHostMallocDefault));
+        w.cap = std::max(lim, 64u);
+    }
+    if (!w.done) HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+    // the ready blocks and where each one's descriptors go (bt_ring.cpp's first phase)
+    uint64_t total = 0;
+    uint32_t nb = 0;
+    for (uint32_t k = 0; k < lim; ++k) {
+        const uint32_t b = (first_block + k) % ring->n_blocks;
+        const uint8_t* bd = static_cast<const uint8_t*>(ring->base) + (uint64_t)b * ring->block_size;
+        // tpacket_block_desc: version, offset_to_priv, then bh1 { block_status, num_pkts,
+        // offset_to_first_pkt, ... } (linux/if_packet.h)
+        const uint32_t status = __atomic_load_n(reinterpret_cast<const uint32_t*>(bd + 8), __ATOMIC_ACQUIRE);
+        if (!(status & 1u)) break;   // TP_STATUS_USER
+        const uint32_t np = *reinterpret_cast<const uint32_t*>(bd + 12);
+        const uint32_t first = *reinterpret_cast<const uint32_t*>(bd + 16);
+        if (total + np > cap) break;
+        if (np && first >= ring->block_size)
+            return fail(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3_gpu: block %u: first frame outside block", b);
+        w.h[nb++] = RingBlock{b, np, (uint32_t)total, first};
+        total += np;
+    }
+    RingWalkArgs a{};
+    a.ring = static_cast<const uint8_t*>(ring_dev);
+    a.block_size = ring->block_size;
+    a.blocks = w.h;
+    a.count = nb;
+    a.desc = desc_dev;
+    a.cap = cap;
+    a.bad = bad_dev;
+    if (int rc = launch_ring_walk(a, st)) return fail(rc, "ring walk launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipEventRecord(w.done, st));
+    w.used = true;
+    c->walk_next ^= 1;
+    *n_desc = (uint32_t)total;
+    *n_blocks_taken = nb;
+#ifdef BT_DEBUG_BOUNDS
+    BoundsLog f{};
+    if (const uint32_t k = bounds_take_ring(st, &f))
+        return fail(BT_E_INTERNAL, "BT_DEBUG_BOUNDS: ring walk: %u failed checks, first %s index %llu limit %llu", k,
+                    bounds_site_name(f.site), (unsigned long long)f.index, (unsigned long long)f.limit);
+#endif
     return BT_OK;
 }
 

@@ -293,6 +293,7 @@ typedef struct bt_opts {
 #define BT_OPT_WIDE_ALWAYS 0x800u  /* descriptor mode: always wide round A (A/B only)      */
 #define BT_OPT_PIPELINE 0x2000u    /* bt_time_device: steps as bt_parse_filter_device_async */
 #define BT_OPT_GROUP_SHARED_DEVICE 0x4000u /* bt_group_create: allow a device listed twice (tests) */
+#define BT_OPT_NO_LEAN_PCIE 0x8000u /* frames in host memory: read whole 64-B windows (A/B only) */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
@@ -448,6 +449,18 @@ int  bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_blo
 int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                          uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
                          uint32_t* n_blocks_taken);
+/* The walk with the frame chains followed on the GPU. The host reads only the taken blocks'
+ * headers (block_status, num_pkts, offset_to_first_pkt: one line per block) and a kernel on
+ * `stream` walks every chain through ring_dev (the ring's device-visible alias, e.g. from
+ * bt_host_register), one lane per block, writing the descriptors (as bt_ring_walk_tpv3
+ * does) into desc_dev, device memory of cap entries. *n_desc and *n_blocks_taken are known
+ * on return, the descriptors once the stream has run the kernel; batches on the same
+ * stream that read desc_dev follow it in order. A chain that leaves its block makes that
+ * block's remaining descriptors empty (length 0: nothing of them is read) and stores
+ * block + 1 into *bad_dev (device memory, optional; the largest such block wins). */
+int  bt_ring_walk_tpv3_gpu(bt_ctx* ctx, const bt_tpv3_ring* ring, const void* ring_dev, uint32_t first_block,
+                           uint32_t max_blocks, bt_pkt_desc* desc_dev, uint32_t cap, uint32_t* n_desc,
+                           uint32_t* n_blocks_taken, uint32_t* bad_dev, void* stream);
 /* Hands `count` blocks starting at first_block back to the kernel (TP_STATUS_KERNEL,
  * release-ordered). Call it once the device has finished reading them. */
 int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);

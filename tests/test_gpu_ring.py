@@ -158,3 +158,89 @@ def test_gathered_prefixes_1m_match_oracle(gpu_ctx, cfg):
 C3_SET = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
           {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
           {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+
+
+# ---- the frame chains walked on the GPU (bt_ring_walk_tpv3_gpu) -------------------------
+
+def _gpu_walk(ctx, ring, bs, nb, first=0, max_blocks=None):
+    """Registered ring -> GPU walk into device descriptors -> (descriptors, taken, bad)."""
+    import struct as _s
+    d_ring = ctx.register(ring)
+    cap = int(ring.nbytes // 64) + 64
+    d_desc = ctx.alloc(8 * cap)
+    d_bad = ctx.alloc(16)
+    try:
+        d_bad.zero()
+        n, taken = abi.ring_walk_tpv3_gpu(ctx, ring, d_ring, bs, nb, d_desc.ptr, cap, first=first,
+                                          max_blocks=max_blocks, bad_dev=d_bad.ptr)
+        ctx.synchronize()
+        desc = d_desc.download(np.zeros(max(n, 1), np.uint64))[:n]
+        bad = int(_s.unpack("<I", d_bad.download(np.zeros(4, np.uint8)).tobytes())[0])
+    finally:
+        d_desc.free()
+        d_bad.free()
+        ctx.unregister(ring)
+    return desc, taken, bad
+
+
+def test_gpu_walk_of_kernel_written_ring_matches_reference(gpu_ctx):
+    """The kernel-written ring (994 frames in 4 blocks, real stack traffic + edge frames):
+    the GPU-walked descriptors equal the fixture's, and parse + filter over them in device
+    memory gives the reference's records and decisions."""
+    g = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    bs, nb = (int(x) for x in g["geometry"])
+    ring = g["ring"].copy()
+    desc, taken, bad = _gpu_walk(gpu_ctx, ring, bs, nb)
+    assert taken == nb and bad == 0
+    assert np.array_equal(desc, g["desc"])
+    s = man["rings"]["ring_lo"]["filter_sets"][0]
+    filters = man["filter_sets"][s]
+    gpu_ctx.compile(filters)
+    r = abi.DeviceRun(gpu_ctx, ring, desc, len(desc))
+    try:
+        r.run()
+        out = r.fetch()
+    finally:
+        r.free()
+    assert np.array_equal(out["records"], g["rec"])
+    compare_decisions(out["decide"], g[f"code__{s}"], g[f"src__{s}"], filters, where="ring_lo gpu walk")
+
+
+@pytest.mark.parametrize("cfg", [synth.C2, synth.C3, synth.C4, synth.FUZZ])
+def test_gpu_walk_equals_host_walk(gpu_ctx, cfg):
+    data, desc0 = synth.capture(cfg, 1 << 18, seed=33)
+    ring, rdesc, used = synth.tpv3_ring(data, desc0, block_size=1 << 18)
+    host, taken_h = abi.ring_walk_tpv3(ring, 1 << 18, used, ctx=gpu_ctx)
+    dev, taken, bad = _gpu_walk(gpu_ctx, ring, 1 << 18, used)
+    assert taken == taken_h == used and bad == 0
+    assert np.array_equal(dev, host) and np.array_equal(dev, rdesc)
+    # a window of blocks that wraps past the ring's end, stopping at a block the kernel owns
+    rng = np.random.default_rng(cfg)
+    first = int(rng.integers(1, used))
+    ring2 = ring.copy()
+    owned = (first + 3) % used
+    ring2[owned * (1 << 18) + 8:owned * (1 << 18) + 12] = 0        # TP_STATUS_KERNEL
+    host, th = abi.ring_walk_tpv3(ring2, 1 << 18, used, first=first, ctx=gpu_ctx)
+    dev, td, bad = _gpu_walk(gpu_ctx, ring2, 1 << 18, used, first=first)
+    assert th == td == 3 and bad == 0 and np.array_equal(dev, host)
+
+
+def test_gpu_walk_reports_a_malformed_block(gpu_ctx):
+    import struct as _s
+    import ring_util as ru
+    data, desc = synth.capture(synth.C2, 3000, seed=3)
+    bs = 1 << 16
+    ring, rdesc, used = synth.tpv3_ring(data, desc, block_size=bs)
+    _, _, _, frames = next(ru.frame_headers(ring, bs, used))
+    bad_ring = ring.copy()
+    off = bs + frames[5][0]                                      # frame 5 of block 1 leaves the block
+    bad_ring[off:off + 4] = np.frombuffer(_s.pack("<I", bs), np.uint8)
+    dev, taken, bad = _gpu_walk(gpu_ctx, bad_ring, bs, used)
+    assert taken == used and bad == 2                            # block 1, reported as block + 1
+    host_ok, _ = abi.ring_walk_tpv3(ring, bs, used)
+    n0 = int(np.frombuffer(ring[12:16].tobytes(), np.uint32)[0])                   # block 0's frames
+    n1 = int(np.frombuffer(ring[bs + 12:bs + 16].tobytes(), np.uint32)[0])
+    assert np.array_equal(dev[:n0 + 6], host_ok[:n0 + 6])        # up to and including frame 5
+    assert not dev[n0 + 6:n0 + n1].any()                         # the rest of block 1: empty
+    assert np.array_equal(dev[n0 + n1:], host_ok[n0 + n1:])      # later blocks unaffected

@@ -28,6 +28,9 @@ ap.add_argument("--tpacket", action="store_true",
 ap.add_argument("--gather", action="store_true",
                 help="with --tpacket: the walker also copies each frame's header prefix into 128-B pinned "
                      "slots (bt_ring_gather_tpv3) and the kernels read the slots (BT_BATCH_PREFIXES)")
+ap.add_argument("--gpu-walk", action="store_true",
+                help="with --tpacket: the frame chains are walked on the GPU (bt_ring_walk_tpv3_gpu: the host "
+                     "reads only the block headers), descriptors in device memory")
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
 ap.add_argument("--host-threads", type=int, default=0)
 a = ap.parse_args()
@@ -50,6 +53,8 @@ if a.tpacket:
     if a.gather:
         slots = np.zeros((n + 64) * abi.PREFIX_SLOT, np.uint8)
         d_slots = ctx.register(slots)
+    if a.gpu_walk:
+        g_desc = ctx.alloc(8 * (n + 64))
     for mode in ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
         tiles = (n + 63) // 64 + nbat + 1          # each batch starts its outputs on a fresh tile
@@ -70,6 +75,11 @@ if a.tpacket:
                     cnt = len(got)
                     if len(counts) < nbat:
                         counts.append(cnt)
+                elif walk and a.gpu_walk:
+                    cnt, taken = abi.ring_walk_tpv3_gpu(ctx, ring, d_ring, bs, used, g_desc.ptr + 8 * start,
+                                                        n + 64 - start, first=k * B, max_blocks=min(B, used - k * B))
+                    if len(counts) < nbat:
+                        counts.append(cnt)
                 elif walk:
                     got, taken = abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B),
                                                     ctx=ctx, out=h_desc[start:])
@@ -82,7 +92,8 @@ if a.tpacket:
                     batch = abi.Batch(d_slots + abi.PREFIX_SLOT * start, d_desc + 8 * start, 0, cnt,
                                       abi.PREFIX_SLOT * cnt, abi.DESC_PACKED, abi.BATCH_PREFIXES)
                 else:
-                    batch = abi.Batch(d_ring, d_desc + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
+                    dd = g_desc.ptr if a.gpu_walk else d_desc
+                    batch = abi.Batch(d_ring, dd + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
                 outs = abi.Outputs(d_rec + 6144 * tile if rec else None, cnt, d_ver + 8 * tile, d_dec + 64 * tile,
                                    None, None)
                 ctx.run_device(batch, outs)      # async: the next walk overlaps this batch
@@ -104,17 +115,22 @@ if a.tpacket:
             kbest = min(kbest, time.perf_counter() - t0)
         t0 = time.perf_counter()
         for k in range(nbat):
+            if a.gpu_walk:
+                abi.ring_walk_tpv3_gpu(ctx, ring, d_ring, bs, used, g_desc.ptr, n + 64, first=k * B,
+                                       max_blocks=min(B, used - k * B))
+                continue
             if a.gather:
                 abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B, max_blocks=min(B, used - k * B),
                                      ctx=ctx)
             else:
                 abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
                                    out=h_desc[:])
+        ctx.synchronize()
         walk = time.perf_counter() - t0
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
         how = "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
-            "tpacket_v3 ring, zero-copy, "
+            "tpacket_v3 ring, chains walked on the GPU, zero-copy, " if a.gpu_walk else "tpacket_v3 ring, zero-copy, "
         print(json.dumps({"config": a.config, "mode": how + mode, "packets": n,
                           "ring_blocks": used, "block_bytes": bs, "batch_blocks": B, "seconds": round(best, 4),
                           "mpps": round(n / best / 1e6, 1), "walk_only_mpps": round(n / walk / 1e6, 1),
@@ -125,6 +141,8 @@ if a.tpacket:
             ctx.unregister(h)
     ctx.unregister(h_desc)
     ctx.unregister(ring)
+    if a.gpu_walk:
+        g_desc.free()
     if a.gather:
         ctx.unregister(slots)
     sys.exit(0)

@@ -55,8 +55,10 @@ for step in $STEPS; do
       cat "$OUT/sq.txt" ;;
     e2e)
       rm -f "$OUT/e2e.jsonl"
-      for cfg in c2 c3 c4; do
-        for mode in "" "--zero-copy" "--tpacket" ${E2E_EXTRA:-}; do
+      # E2E_MODES: ';'-separated e2e.py option sets (default: host gather, zero-copy, ring)
+      IFS=';' read -r -a modes <<< "${E2E_MODES:- ;--zero-copy;--tpacket}"
+      for cfg in ${E2E_CFGS:-c2 c3 c4}; do
+        for mode in "${modes[@]}"; do
           timeout -k 10 400 python tools/e2e.py --config $cfg $mode --reps 2 >> "$OUT/e2e.jsonl" 2> "$OUT/e2e.err" \
             || fail "e2e $cfg $mode" $? "$OUT/e2e.err"
         done
