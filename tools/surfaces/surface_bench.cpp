@@ -166,6 +166,42 @@ void bench_gpu_filter(const Capture& c, double seconds, const char* which) {
     (void)passed;
 }
 
+// The floor of any applyFilters(vector) -> vector<FilterResult>: constructing n results,
+// filling them from per-slot strings (on T threads) and destroying them, with no filtering.
+void bench_result_floor(const Capture& c, int threads, double seconds) {
+    const std::string pass = "Packet passed all filters", rej = "Filter proto rejected packet", name = "ports";
+    uint64_t done = 0;
+    double build_s = 0, fill_s = 0, free_s = 0;
+    const auto t0 = Clock::now();
+    while (secs(t0, Clock::now()) < seconds) {
+        const auto a = Clock::now();
+        std::vector<PacketFilter::FilterResult> r(c.packets.size());
+        const auto b = Clock::now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                for (size_t i = r.size() * t / threads; i < r.size() * (t + 1) / threads; ++i) {
+                    r[i].passed = i & 1;
+                    r[i].filterName = name;
+                    r[i].reason = (i & 1) ? pass : rej;
+                }
+            });
+        for (auto& x : th) x.join();
+        const auto d = Clock::now();
+        { std::vector<PacketFilter::FilterResult> gone; gone.swap(r); }
+        const auto e = Clock::now();
+        build_s += secs(a, b);
+        fill_s += secs(b, d);
+        free_s += secs(d, e);
+        done += c.packets.size();
+    }
+    const double el = secs(t0, Clock::now());
+    char extra[200];
+    std::snprintf(extra, sizeof(extra), "\"construct_s\": %.4f, \"fill_s\": %.4f, \"destroy_s\": %.4f, \"seconds\": %.3f",
+                  build_s, fill_s, free_s, el);
+    line("floor: vector<FilterResult>(n) + fill + destroy (no filtering)", c, threads, done / el, extra);
+}
+
 void bench_plugin(const Capture& c, int threads, const char* so) {
     void* h = dlopen(so, RTLD_LAZY);
     if (!h) {
@@ -234,6 +270,7 @@ int main(int argc, char** argv) {
             bench_ref(c, threads, seconds);
         }
         if (what == "all" || what == "filter") {
+            bench_result_floor(c, std::min(threads, 8), seconds);
             bench_gpu_filter(c, seconds, "apply");
             bench_gpu_filter(c, seconds, "classify");
         }
