@@ -32,11 +32,12 @@ ap.add_argument("--gpu-walk", action="store_true",
                 help="with --tpacket: the frame chains are walked on the GPU (bt_ring_walk_tpv3_gpu: the host "
                      "reads only the block headers), descriptors in device memory")
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
+ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="bt_opts.flags (A/B, e.g. 0x8000 no lean PCIe round A)")
 ap.add_argument("--host-threads", type=int, default=0)
 a = ap.parse_args()
 cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4}[a.config]
 data, desc = synth.capture(cfg, a.packets)
-ctx = abi.Context(0, host_chunk_packets=a.chunk, host_threads=a.host_threads)
+ctx = abi.Context(0, host_chunk_packets=a.chunk, host_threads=a.host_threads, flags=a.flags)
 ctx.compile([{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
              {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
              {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}])
@@ -131,7 +132,7 @@ if a.tpacket:
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
         how = "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
             "tpacket_v3 ring, chains walked on the GPU, zero-copy, " if a.gpu_walk else "tpacket_v3 ring, zero-copy, "
-        print(json.dumps({"config": a.config, "mode": how + mode, "packets": n,
+        print(json.dumps({"config": a.config, "flags": a.flags, "mode": how + mode, "packets": n,
                           "ring_blocks": used, "block_bytes": bs, "batch_blocks": B, "seconds": round(best, 4),
                           "mpps": round(n / best / 1e6, 1), "walk_only_mpps": round(n / walk / 1e6, 1),
                           "kernels_only_mpps": round(n / kbest / 1e6, 1),
@@ -171,7 +172,7 @@ if a.zero_copy:
             best = min(best, time.perf_counter() - t0)
         lens = synth.desc_len(desc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
-        print(json.dumps({"config": a.config, "mode": "zero-copy in, D2H copy out, " + mode, "packets": n,
+        print(json.dumps({"config": a.config, "flags": a.flags, "mode": "zero-copy in, D2H copy out, " + mode, "packets": n,
                           "seconds": round(best, 4), "mpps": round(n / best / 1e6, 1),
                           "pcie_read_GBps": round(pcie / best / 1e9, 2),
                           "d2h_GBps": round(n * (1.125 + (96 if rec else 0)) / best / 1e9, 2)}), flush=True)
@@ -185,7 +186,7 @@ if a.zero_copy:
             ctx.run_device(run.batch, outs)
             ctx.synchronize()
             best = min(best, time.perf_counter() - t0)
-        print(json.dumps({"config": a.config, "mode": "zero-copy in and out, " + mode, "packets": n,
+        print(json.dumps({"config": a.config, "flags": a.flags, "mode": "zero-copy in and out, " + mode, "packets": n,
                           "seconds": round(best, 4), "mpps": round(n / best / 1e6, 1),
                           "pcie_read_GBps": round(pcie / best / 1e9, 2),
                           "pcie_write_GBps": round(n * (1.125 + (96 if rec else 0)) / best / 1e9, 2)}), flush=True)
@@ -209,6 +210,6 @@ for mode in ("verdicts", "records+verdicts"):
     lens = synth.desc_len(desc)
     h2d = float((((lens.clip(max=112) + 15) // 16) * 16).sum() + 8 * a.packets)
     d2h = a.packets * (1 + 1 / 8 + (96 if rec else 0))
-    print(json.dumps({"config": a.config, "mode": mode, "packets": a.packets, "seconds": round(best, 4),
+    print(json.dumps({"config": a.config, "flags": a.flags, "mode": mode, "packets": a.packets, "seconds": round(best, 4),
                       "mpps": round(a.packets / best / 1e6, 1), "h2d_GBps": round(h2d / best / 1e9, 2),
                       "d2h_GBps": round(d2h / best / 1e9, 2), "n_pass": out["n_pass"]}), flush=True)
