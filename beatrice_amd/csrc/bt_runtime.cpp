@@ -317,6 +317,8 @@ bool host_resident(bt_ctx* c, const void* base) {
     else (void)hipGetLastError();
     c->last_base = base;
     c->last_base_host = host;
+    static const bool dbg = getenv("BT_DEBUG_LEAN") != nullptr;
+    if (dbg) fprintf(stderr, "[bt] batch base %p: %s memory (type %d)\n", base, host ? "host" : "device", (int)attr.type);
     return host;
 }
 
