@@ -55,10 +55,9 @@ struct MainArgs {
     uint32_t lean;             // descriptor mode: bytes of a frame round A reads at most (0xFFFF:
                                // its first 64-B window); 46 for host-resident frames (kLeanPcie)
 };
-// Frames read over PCIe (registered host memory): round A reads the first 46 B of a
-// frame (Eth + IPv4 + UDP, and every filter gate), not the whole 64-B window; round B
-// fetches what a longer header needs. PCIe moves 64-B lines, and a frame at 2 mod 16 in
-// a TPACKET_V3 slot then touches 1.5 lines on average instead of 2.
+// Frames read over PCIe (registered host memory) by a filter-only call: round A reads
+// the first 46 B of a frame (every filter gate and the detector's 38 B) instead of the
+// whole 64-B window (DESIGN.md §9.2 has the A/B).
 constexpr uint32_t kLeanPcie = 46;
 
 constexpr uint32_t kDfaPoolMax = 16384;   // bytes of DFA tables per program (LDS budget)

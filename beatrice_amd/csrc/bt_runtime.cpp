@@ -402,8 +402,13 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.verdict = o->verdict ? o->verdict : (w ? w->verdict : nullptr);
     if (w && !o->verdict) { int rc = ws_touch(c, w, st); if (rc) return rc; }   // the main kernel writes w->verdict
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
+    // Lean round A for frames read over PCIe, filter-only calls: the filters and the
+    // detector read <= 38 B, so a 46-B first round reads 25 % fewer bytes per frame (A/B,
+    // profiles/r03/e2e/lean_ab.jsonl: zero-copy verdicts C3 +17 %, C4 +4..10 %, C2 +2..4 %;
+    // TPACKET_V3 ring C2 / C4 level, C3 -8 %). Calls that also parse would need a second
+    // round for almost every tile (the walk reads to L3 + 40 B) and lost 28-39 %: not lean.
     a.lean = 0xFFFFu;
-    const bool lean = b->desc && !(c->opts.flags & BT_OPT_NO_LEAN_PCIE) && host_resident(c, b->base);
+    const bool lean = b->desc && !o->records && !(c->opts.flags & BT_OPT_NO_LEAN_PCIE) && host_resident(c, b->base);
     a.dfa = c->dfa_dev[c->dfa_cur];
     a.dfa_bytes = filter ? (uint32_t)c->dfa_pool.size() : 0u;
     // Cache policy (measured): non-temporal record stores everywhere (C2 +3..9 %,
