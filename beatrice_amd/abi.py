@@ -151,7 +151,7 @@ EXPORTS = [
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3", "bt_ring_walk_tpv3_gpu",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records",
-    "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3",
+    "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3", "bt_ring_gather_dense_tpv3",
     "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
 ]
@@ -217,6 +217,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(u32), ctypes.POINTER(u32), vp, vp]),
         "bt_ring_gather_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
                                                ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+        "bt_ring_gather_dense_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
+                                                     ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
         "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
@@ -574,19 +576,20 @@ BATCH_PREFIXES = 0x1
 
 def ring_gather_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, slots: np.ndarray, out: np.ndarray,
                      first: int = 0, max_blocks: int | None = None, ctx: "Context | None" = None,
-                     slot_base: int = 0):
+                     slot_base: int = 0, dense: bool = False):
     """bt_ring_gather_tpv3: the walk of ring_walk_tpv3, plus every frame's header prefix
     copied into slots[(slot_base + i) * PREFIX_SLOT ...]; descriptors (written to
-    out[slot_base:]) point into `slots`. Returns (desc view, blocks taken)."""
+    out[slot_base:]) point into `slots`. dense=True: bt_ring_gather_dense_tpv3 (each block's
+    prefixes back to back from its first slot). Returns (desc view, blocks taken)."""
     if slots.dtype != np.uint8 or not slots.flags.c_contiguous or out.dtype != np.uint64:
         raise ValueError("slots must be contiguous uint8, out uint64")
+    fn = lib().bt_ring_gather_dense_tpv3 if dense else lib().bt_ring_gather_tpv3
     cap = min(len(out) - slot_base, len(slots) // PREFIX_SLOT - slot_base)
     r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
     nd, nb = ctypes.c_uint32(), ctypes.c_uint32()
-    _check(lib().bt_ring_gather_tpv3(ctx.h if ctx else None, ctypes.byref(r), first,
-                                     n_blocks if max_blocks is None else max_blocks,
-                                     slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base,
-                                     cap, ctypes.byref(nd), ctypes.byref(nb)))
+    _check(fn(ctx.h if ctx else None, ctypes.byref(r), first, n_blocks if max_blocks is None else max_blocks,
+              slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base,
+              cap, ctypes.byref(nd), ctypes.byref(nb)))
     return out[slot_base:slot_base + nd.value], nb.value
 
 

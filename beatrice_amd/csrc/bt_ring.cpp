@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -59,7 +60,34 @@ struct Chain {
     const uint8_t* pend;       // gather: frame whose prefix is copied on the next visit
     uint32_t pend_len;
     uint8_t* pend_slot;
+    uint8_t* line;             // dense gather: the 64-B line being filled, and its
+    uint32_t fill;             //   16-B chunks so far (staged in `stage`)
+    __m128i stage[4];
 };
+
+// What the walk does with each frame besides its descriptor. Dense, staged: each chain
+// fills whole 64-B lines in `stage` and streams them (non-temporal, full lines); plain:
+// ordinary stores (A/B: BT_GATHER_PLAIN=1).
+enum WalkMode { kWalkOnly, kGatherSlots, kGatherDense, kGatherDensePlain, kGatherDenseLine };
+
+inline uint8_t* dense_at(const Chain& ch) { return ch.line + 16u * ch.fill; }
+
+inline void push16(Chain& ch, __m128i v) {
+    ch.stage[ch.fill++] = v;
+    if (ch.fill == 4) {
+        __m128i* d = reinterpret_cast<__m128i*>(ch.line);
+        _mm_stream_si128(d, ch.stage[0]);
+        _mm_stream_si128(d + 1, ch.stage[1]);
+        _mm_stream_si128(d + 2, ch.stage[2]);
+        _mm_stream_si128(d + 3, ch.stage[3]);
+        ch.line += 64;
+        ch.fill = 0;
+    }
+}
+
+inline void flush_stage(Chain& ch) {
+    for (uint32_t i = 0; i < ch.fill; ++i) _mm_stream_si128(reinterpret_cast<__m128i*>(ch.line) + i, ch.stage[i]);
+}
 
 inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 
@@ -88,10 +116,60 @@ inline uint32_t prefix_len(const uint8_t* f, uint32_t len) {
     return end < len ? end : len;
 }
 
-// Non-temporal 16-B stores into the (16-B-aligned) slot: the slot lines are not read
-// for ownership first, and they do not evict the ring lines the chains still walk.
-inline void copy_prefix(Chain& ch) {
+// Slots: non-temporal 16-B stores into the (16-B-aligned) slot: the slot lines are not
+// read for ownership first, and they do not evict the ring lines the chains still walk.
+// Dense: each chain writes its block's prefixes back to back; 16 chains per thread are more
+// open lines than the write-combining buffers hold, so the chunks are staged per chain and
+// streamed as whole lines.
+template <WalkMode MODE>
+inline uint32_t copy_prefix(Chain& ch) {
     const uint32_t m = prefix_len(ch.pend, ch.pend_len);
+    if (MODE == kGatherDense) {
+        const uint32_t full = m & ~15u;
+        uint32_t k = 0;
+        for (; k < full; k += 16) push16(ch, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k)));
+        if (k < m) {
+            alignas(16) uint8_t tail[16] = {};
+            std::memcpy(tail, ch.pend + k, m - k);
+            push16(ch, _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
+            k += 16;
+        }
+        ch.pend = nullptr;
+        return k;
+    }
+    if (MODE == kGatherDenseLine) {
+        // whole 64-B lines straight from the frame: one line for prefixes up to 64 B, two
+        // for longer ones; chunks past the prefix are zero
+        const uint32_t lines = m > 64u ? 2u : 1u, full = m & ~15u;
+        __m128i* d = reinterpret_cast<__m128i*>(ch.pend_slot);
+        uint32_t k = 0;
+        for (; k < full; k += 16) _mm_stream_si128(d + k / 16, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k)));
+        if (k < m) {
+            alignas(16) uint8_t tail[16] = {};
+            std::memcpy(tail, ch.pend + k, m - k);
+            _mm_stream_si128(d + k / 16, _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
+            k += 16;
+        }
+        for (; k < 64u * lines; k += 16) _mm_stream_si128(d + k / 16, _mm_setzero_si128());
+        ch.pend = nullptr;
+        return 64u * lines;
+    }
+    if (MODE == kGatherDensePlain) {
+        const uint32_t full = m & ~15u;
+        uint32_t k = 0;
+        for (; k < full; k += 16)
+            _mm_store_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k),
+                            _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k)));
+        if (k < m) {
+            alignas(16) uint8_t tail[16] = {};
+            std::memcpy(tail, ch.pend + k, m - k);
+            _mm_store_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k),
+                            _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
+            k += 16;
+        }
+        ch.pend = nullptr;
+        return k;
+    }
     if (((uintptr_t)ch.pend_slot & 15u) == 0) {
         // whole 16-B chunks of the frame with vector loads; the last partial chunk with
         // memcpy into a zeroed chunk, so no load reads past the frame (whose end may be
@@ -112,9 +190,10 @@ inline void copy_prefix(Chain& ch) {
         std::memcpy(ch.pend_slot, ch.pend, m);
     }
     ch.pend = nullptr;
+    return m;
 }
 
-template <bool GATHER>
+template <WalkMode MODE>
 int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_t* start, uint32_t count,
                     bt_pkt_desc* desc, uint8_t* slots) {
     const uint64_t bs = r->block_size;
@@ -134,6 +213,8 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
             ch.block = b;
             ch.first = start[k];
             ch.pend = nullptr;
+            ch.line = slots ? slots + (uint64_t)start[k] * BT_PREFIX_SLOT : nullptr;
+            ch.fill = 0;
             if (ch.n) {
                 __builtin_prefetch(ch.blk + ch.off);
                 ++live;
@@ -148,25 +229,31 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                     ++g;
                     continue;
                 }
-                if (GATHER && ch.pend) copy_prefix(ch);   // its lines were prefetched a round ago
+                if (MODE != kWalkOnly && ch.pend) {   // its lines were prefetched a round ago
+                    const uint32_t took = copy_prefix<MODE>(ch);
+                    if (MODE == kGatherDensePlain || MODE == kGatherDenseLine) ch.line += took;
+                }
                 if (ch.off + sizeof(tpacket3_hdr) > bs) return ch.block;
                 const tpacket3_hdr* h = reinterpret_cast<const tpacket3_hdr*>(ch.blk + ch.off);
                 const uint64_t mac = ch.off + h->tp_mac;
                 const uint32_t snap = h->tp_snaplen, next = h->tp_next_offset;
                 if (mac + snap > bs) return ch.block;
-                if (GATHER) {
+                if (MODE != kWalkOnly) {
                     const uint64_t i = ch.first + ch.j;
-                    ch.out[ch.j] = BT_DESC(i * BT_PREFIX_SLOT, std::min<uint32_t>(snap, kDescLenMax));
+                    ch.pend_slot = MODE == kGatherDense ? dense_at(ch)
+                                   : MODE == kGatherDensePlain || MODE == kGatherDenseLine ? ch.line
+                                   : slots + i * BT_PREFIX_SLOT;
+                    ch.out[ch.j] = BT_DESC((uint64_t)(ch.pend_slot - slots), std::min<uint32_t>(snap, kDescLenMax));
                     ch.pend = ch.blk + mac;
                     ch.pend_len = snap;
-                    ch.pend_slot = slots + i * BT_PREFIX_SLOT;
                     __builtin_prefetch(ch.pend);
                     __builtin_prefetch(ch.pend + 63);
                 } else {
                     ch.out[ch.j] = BT_DESC(ch.base_off + mac, std::min<uint32_t>(snap, kDescLenMax));
                 }
                 if (++ch.j == ch.n) {          // chain done: swap in the last live one
-                    if (GATHER && ch.pend) copy_prefix(ch);
+                    if (MODE != kWalkOnly && ch.pend) copy_prefix<MODE>(ch);
+                    if (MODE == kGatherDense) flush_stage(ch);
                     c[g] = c[--live];
                     continue;
                 }
@@ -186,8 +273,16 @@ extern "C" {
 
 namespace {
 
+// The dense gather's store kind (A/B switch, read per call): BT_GATHER_MODE = staged
+// (default), plain, line.
+int gather_kind() {
+    const char* e = std::getenv("BT_GATHER_MODE");
+    if (!e) return 0;
+    return std::strcmp(e, "plain") == 0 ? 1 : std::strcmp(e, "line") == 0 ? 2 : 0;
+}
+
 int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks, uint8_t* slots,
-              bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
+              bool dense, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
     if (!ring || !ring->base || !n_desc || !n_blocks_taken || (cap && !desc))
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3: null argument");
     if (!ring->n_blocks || ring->block_size < sizeof(tpacket_block_desc) || first_block >= ring->n_blocks)
@@ -214,11 +309,16 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
     //    worker interleaving up to kChains block chains
     const uint32_t nb = (uint32_t)blocks.size();
     std::atomic<int64_t> bad{-1};
+    const int kind = slots && dense ? gather_kind() : 0;
     auto work = [&](unsigned w, unsigned T) {
         const uint32_t a = (uint32_t)((uint64_t)nb * w / T), b = (uint32_t)((uint64_t)nb * (w + 1) / T);
         if (a >= b) return;
-        const int64_t e = slots ? walk_blocks<true>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
-                                : walk_blocks<false>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr);
+        const int64_t e =
+            !slots ? walk_blocks<kWalkOnly>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr)
+            : dense ? (kind == 1 ? walk_blocks<kGatherDensePlain>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
+                       : kind == 2 ? walk_blocks<kGatherDenseLine>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
+                                   : walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots))
+                    : walk_blocks<kGatherSlots>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots);
         if (slots) _mm_sfence();   // this worker's streaming stores land before the join
         if (e >= 0) bad.store(e);
     };
@@ -236,14 +336,23 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
 
 int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                       bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
-    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, false, desc, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                         uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
                         uint32_t* n_blocks_taken) {
     if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_tpv3: null slots");
-    return ring_walk(ctx, ring, first_block, max_blocks, slots, desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, false, desc, cap, n_desc, n_blocks_taken);
+}
+
+int bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                              uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
+                              uint32_t* n_blocks_taken) {
+    if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: null slots");
+    if ((uintptr_t)slots & 15u)
+        return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: slots not 16-B aligned");
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, true, desc, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count) {

@@ -97,14 +97,14 @@ def test_cpp_stage_synthetic_ring():
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
 
 
-def _run_gathered(ctx, ring, bs, nb, filters):
-    """bt_ring_gather_tpv3 -> device run over the 128-B prefix slots (BT_BATCH_PREFIXES),
-    slots and outputs in registered host memory."""
+def _run_gathered(ctx, ring, bs, nb, filters, dense=False):
+    """bt_ring_gather_tpv3 (dense: bt_ring_gather_dense_tpv3) -> device run over the prefix
+    slots (BT_BATCH_PREFIXES), slots and outputs in registered host memory."""
     wdesc, _ = abi.ring_walk_tpv3(ring, bs, nb, ctx=ctx)
     n = len(wdesc)
     slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)   # poison past each prefix
     gd = np.zeros(n, np.uint64)
-    desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx)
+    desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx, dense=dense)
     assert taken == nb and len(desc) == n
     tiles = (n + 63) // 64
     h_rec = np.zeros(tiles * 6144, np.uint8)
@@ -123,7 +123,8 @@ def _run_gathered(ctx, ring, bs, nb, filters):
     return wdesc, abi.untile_records(h_rec, n), h_dec[:n]
 
 
-def test_gathered_prefixes_match_reference(gpu_ctx):
+@pytest.mark.parametrize("dense", [False, True])
+def test_gathered_prefixes_match_reference(gpu_ctx, dense):
     """Header prefixes gathered by the walker give the kernels the reference's records
     and decisions on the kernel-written ring; a PAYLOAD slot is left to the host."""
     g = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
@@ -133,23 +134,24 @@ def test_gathered_prefixes_match_reference(gpu_ctx):
         filters = man["filter_sets"][s]
         if any(f["type"] == abi.PAYLOAD for f in filters):
             continue
-        desc, rec, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, filters)
+        desc, rec, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, filters, dense)
         assert np.array_equal(desc, g["desc"])
         assert np.array_equal(rec, g["rec"])
         compare_decisions(dec, g[f"code__{s}"], g[f"src__{s}"], filters, where=f"ring_lo/{s} gathered")
     pay = [{"type": abi.PROTOCOL, "expr": "tcp", "priority": 3}, {"type": abi.PAYLOAD, "expr": "GET", "priority": 2}]
-    _, _, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, pay)
+    _, _, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, pay, dense)
     _, _, dref, _ = _run_ring(gpu_ctx, g["ring"].copy(), bs, nb, pay, records=False)
     code, slot = dec >> 6, dec & 63
     reached = ((dref >> 6) != 1) | ((dref & 63) == 1)   # packets the PAYLOAD slot decides
     assert np.all(code[reached] == 3) and np.array_equal(dec[~reached], dref[~reached])
 
 
+@pytest.mark.parametrize("dense", [False, True])
 @pytest.mark.parametrize("cfg", [synth.C3, synth.C4, synth.FUZZ])
-def test_gathered_prefixes_1m_match_oracle(gpu_ctx, cfg):
+def test_gathered_prefixes_1m_match_oracle(gpu_ctx, cfg, dense):
     data, desc0 = synth.capture(cfg, 1 << 20, seed=23)
     ring, _, used = synth.tpv3_ring(data, desc0)
-    desc, rec, dec = _run_gathered(gpu_ctx, ring, synth.TPV3_BLOCK, used, C3_SET)
+    desc, rec, dec = _run_gathered(gpu_ctx, ring, synth.TPV3_BLOCK, used, C3_SET, dense)
     orec, odec, _ = ol.oracle_run(ring, desc, len(desc), C3_SET)
     assert np.array_equal(rec, orec)
     assert np.array_equal(dec, odec)

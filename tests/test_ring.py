@@ -191,6 +191,11 @@ def test_gather_prefixes_hold_every_byte_the_walk_reads(which):
     assert gtaken == taken and len(gdesc) == n
     assert np.array_equal(synth.desc_len(gdesc), synth.desc_len(wdesc))
     assert np.array_equal(synth.desc_off(gdesc), np.arange(n, dtype=np.uint64) * abi.PREFIX_SLOT)
+    _same_as_ring(ring, wdesc, slots, gdesc, man)
+
+
+def _same_as_ring(ring, wdesc, slots, gdesc, man):
+    n = len(wdesc)
     rec_w, _, _ = ol.oracle_run(ring, wdesc, n, None, parse=True)
     rec_g, _, _ = ol.oracle_run(slots, gdesc, n, None, parse=True)
     assert np.array_equal(rec_g, rec_w)
@@ -199,3 +204,43 @@ def test_gather_prefixes_hold_every_byte_the_walk_reads(which):
         _, dw, _ = ol.oracle_run(ring, wdesc, n, filters, parse=False)
         _, dg, _ = ol.oracle_run(slots, gdesc, n, filters, parse=False)
         assert np.array_equal(dg, dw), s
+
+
+@pytest.mark.parametrize("which", ["kernel_ring", "c2", "c3", "c4", "fuzz"])
+def test_dense_gather_packs_each_block(which):
+    """bt_ring_gather_dense_tpv3: each block's prefixes back to back from its first slot,
+    16-B aligned, each holding the frame's first bytes (the walk's prefix), and the oracle
+    gives the same records and decisions over them as over the ring."""
+    import json
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    if which == "kernel_ring":
+        g, bs, nb = _fixture()
+        ring, used = g["ring"].copy(), nb
+    else:
+        cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4, "fuzz": synth.FUZZ}[which]
+        data, desc = synth.capture(cfg, 6000, seed=12)
+        bs = 1 << 16
+        ring, _, used = synth.tpv3_ring(data, desc, block_size=bs)
+    wdesc, taken = abi.ring_walk_tpv3(ring, bs, used)
+    n = len(wdesc)
+    slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)
+    out = np.zeros(n, np.uint64)
+    gdesc, gtaken = abi.ring_gather_tpv3(ring, bs, used, slots, out, dense=True)
+    assert gtaken == taken and len(gdesc) == n
+    lens = synth.desc_len(wdesc).astype(np.int64)
+    assert np.array_equal(synth.desc_len(gdesc), synth.desc_len(wdesc))
+    goff = synth.desc_off(gdesc).astype(np.int64)
+    woff = synth.desc_off(wdesc).astype(np.int64)
+    blk = woff // bs
+    first = np.r_[True, blk[1:] != blk[:-1]]
+    assert np.all(goff % 16 == 0)
+    assert np.array_equal(goff[first], np.flatnonzero(first) * abi.PREFIX_SLOT)   # block k at j_k * slot
+    step = np.diff(goff)[~first[1:]]
+    assert np.all((step >= 0) & (step <= abi.PREFIX_SLOT) & (step % 16 == 0))
+    # each prefix holds the frame's first bytes: up to the next prefix within the block
+    nxt = np.r_[goff[1:], goff[-1] + abi.PREFIX_SLOT]
+    room = np.where(np.r_[~first[1:], False], nxt - goff, abi.PREFIX_SLOT)
+    for i in range(n):
+        k = int(min(room[i], lens[i], 38))
+        assert np.array_equal(slots[goff[i]:goff[i] + k], ring[woff[i]:woff[i] + k]), i
+    _same_as_ring(ring, wdesc, slots, gdesc, man)

@@ -28,6 +28,8 @@ ap.add_argument("--tpacket", action="store_true",
 ap.add_argument("--gather", action="store_true",
                 help="with --tpacket: the walker also copies each frame's header prefix into 128-B pinned "
                      "slots (bt_ring_gather_tpv3) and the kernels read the slots (BT_BATCH_PREFIXES)")
+ap.add_argument("--dense", action="store_true",
+                help="with --gather: each block's prefixes packed back to back (bt_ring_gather_dense_tpv3)")
 ap.add_argument("--gpu-walk", action="store_true",
                 help="with --tpacket: the frame chains are walked on the GPU (bt_ring_walk_tpv3_gpu: the host "
                      "reads only the block headers), descriptors in device memory")
@@ -72,7 +74,8 @@ if a.tpacket:
             for k in range(nbat):
                 if walk and a.gather:
                     got, taken = abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B,
-                                                      max_blocks=min(B, used - k * B), ctx=ctx, slot_base=start)
+                                                      max_blocks=min(B, used - k * B), ctx=ctx, slot_base=start,
+                                                      dense=a.dense)
                     cnt = len(got)
                     if len(counts) < nbat:
                         counts.append(cnt)
@@ -122,7 +125,7 @@ if a.tpacket:
                 continue
             if a.gather:
                 abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B, max_blocks=min(B, used - k * B),
-                                     ctx=ctx)
+                                     ctx=ctx, dense=a.dense)
             else:
                 abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
                                    out=h_desc[:])
@@ -130,7 +133,8 @@ if a.tpacket:
         walk = time.perf_counter() - t0
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
-        how = "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
+        how = "tpacket_v3 ring, header gather packed per block, zero-copy, " if a.gather and a.dense else \
+            "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
             "tpacket_v3 ring, chains walked on the GPU, zero-copy, " if a.gpu_walk else "tpacket_v3 ring, zero-copy, "
         print(json.dumps({"config": a.config, "flags": a.flags, "mode": how + mode, "packets": n,
                           "ring_blocks": used, "block_bytes": bs, "batch_blocks": B, "seconds": round(best, 4),

@@ -3,6 +3,7 @@
 //   walk_scaling <cfg 2|3|4> <frames> <block_bytes> <max_threads> [reg|pool]
 // reg:  the ring is page-locked + mapped with bt_host_register first (GPU needed)
 // pool: the walk runs through a context's host pool (bt_create host_threads = T)
+// gather: walk vs the three header gathers through a pool of max_threads threads
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -20,7 +21,7 @@ extern "C" uint64_t bt_synth_tpv3_pack(const uint8_t* data, const uint64_t* desc
 int main(int argc, char** argv) {
     const int cfg = atoi(argv[1]);
     const uint64_t n = strtoull(argv[2], nullptr, 0), bs = strtoull(argv[3], nullptr, 0);
-    const unsigned maxT = (unsigned)atoi(argv[4]);
+    unsigned maxT = (unsigned)atoi(argv[4]);
     const std::string mode = argc > 5 ? argv[5] : "";
     std::vector<uint64_t> desc(n);
     std::vector<uint8_t> data(bt_synth_layout(cfg, n, 1, desc.data()));
@@ -45,6 +46,46 @@ int main(int argc, char** argv) {
             return 1;
         }
         printf("ring registered with the GPU\n");
+    }
+    if (mode == "gather") {
+        // walk / gather into 128-B slots / dense staged / dense plain, interleaved, through a
+        // pool of maxT threads, 128 blocks per call; best of 5 rounds each
+        bt_opts o{};
+        o.host_threads = maxT;
+        bt_ctx* c = nullptr;
+        if (bt_create(0, &o, &c) != BT_OK) {
+            printf("bt_create failed (%s): one thread, no pool\n", bt_last_error());
+            c = nullptr;
+            maxT = 1;
+        }
+        std::vector<uint8_t> slots((n + 64) * BT_PREFIX_SLOT + 64);
+        uint8_t* sl = slots.data() + ((64 - ((uintptr_t)slots.data() & 63)) & 63);
+        for (auto& x : slots) x = 0;
+        const char* names[5] = {"walk", "gather 128-B slots", "gather dense, staged lines", "gather dense, plain stores",
+                                "gather dense, 64-B lines"};
+        const char* kinds[5] = {"staged", "staged", "staged", "plain", "line"};
+        double best[5] = {1e9, 1e9, 1e9, 1e9, 1e9};
+        for (int rep = 0; rep < 5; ++rep)
+            for (int m = 0; m < 5; ++m) {
+                setenv("BT_GATHER_MODE", kinds[m], 1);
+                const auto t0 = std::chrono::steady_clock::now();
+                for (uint64_t b0 = 0; b0 < used; b0 += 128) {
+                    uint32_t nd = 0, nb = 0;
+                    const uint32_t cap = (uint32_t)(n + 64 - first[b0]);
+                    if (m == 0)
+                        bt_ring_walk_tpv3(c, &r, (uint32_t)b0, 128, out.data() + first[b0], cap, &nd, &nb);
+                    else if (m == 1)
+                        bt_ring_gather_tpv3(c, &r, (uint32_t)b0, 128, sl + first[b0] * BT_PREFIX_SLOT, out.data() + first[b0],
+                                            cap, &nd, &nb);
+                    else
+                        bt_ring_gather_dense_tpv3(c, &r, (uint32_t)b0, 128, sl + first[b0] * BT_PREFIX_SLOT,
+                                                  out.data() + first[b0], cap, &nd, &nb);
+                }
+                best[m] = std::min(best[m], std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+            }
+        for (int m = 0; m < 5; ++m) printf("cfg %d threads %u  %-28s %.1f Mpps\n", cfg, maxT, names[m], n / best[m] / 1e6);
+        if (c) bt_destroy(c);
+        return 0;
     }
     if (mode == "pool") {
         for (unsigned T = 1; T <= maxT; T *= 2) {
