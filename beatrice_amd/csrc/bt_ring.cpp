@@ -20,7 +20,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -65,10 +64,8 @@ struct Chain {
     __m128i stage[4];
 };
 
-// What the walk does with each frame besides its descriptor. Dense, staged: each chain
-// fills whole 64-B lines in `stage` and streams them (non-temporal, full lines); plain:
-// ordinary stores (A/B: BT_GATHER_PLAIN=1).
-enum WalkMode { kWalkOnly, kGatherSlots, kGatherDense, kGatherDensePlain, kGatherDenseLine };
+// What the walk does with each frame besides its descriptor.
+enum WalkMode { kWalkOnly, kGatherSlots, kGatherDense };
 
 inline uint8_t* dense_at(const Chain& ch) { return ch.line + 16u * ch.fill; }
 
@@ -122,7 +119,7 @@ inline uint32_t prefix_len(const uint8_t* f, uint32_t len) {
 // open lines than the write-combining buffers hold, so the chunks are staged per chain and
 // streamed as whole lines.
 template <WalkMode MODE>
-inline uint32_t copy_prefix(Chain& ch) {
+inline void copy_prefix(Chain& ch) {
     const uint32_t m = prefix_len(ch.pend, ch.pend_len);
     if (MODE == kGatherDense) {
         const uint32_t full = m & ~15u;
@@ -132,43 +129,9 @@ inline uint32_t copy_prefix(Chain& ch) {
             alignas(16) uint8_t tail[16] = {};
             std::memcpy(tail, ch.pend + k, m - k);
             push16(ch, _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
-            k += 16;
         }
         ch.pend = nullptr;
-        return k;
-    }
-    if (MODE == kGatherDenseLine) {
-        // whole 64-B lines straight from the frame: one line for prefixes up to 64 B, two
-        // for longer ones; chunks past the prefix are zero
-        const uint32_t lines = m > 64u ? 2u : 1u, full = m & ~15u;
-        __m128i* d = reinterpret_cast<__m128i*>(ch.pend_slot);
-        uint32_t k = 0;
-        for (; k < full; k += 16) _mm_stream_si128(d + k / 16, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k)));
-        if (k < m) {
-            alignas(16) uint8_t tail[16] = {};
-            std::memcpy(tail, ch.pend + k, m - k);
-            _mm_stream_si128(d + k / 16, _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
-            k += 16;
-        }
-        for (; k < 64u * lines; k += 16) _mm_stream_si128(d + k / 16, _mm_setzero_si128());
-        ch.pend = nullptr;
-        return 64u * lines;
-    }
-    if (MODE == kGatherDensePlain) {
-        const uint32_t full = m & ~15u;
-        uint32_t k = 0;
-        for (; k < full; k += 16)
-            _mm_store_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k),
-                            _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + k)));
-        if (k < m) {
-            alignas(16) uint8_t tail[16] = {};
-            std::memcpy(tail, ch.pend + k, m - k);
-            _mm_store_si128(reinterpret_cast<__m128i*>(ch.pend_slot + k),
-                            _mm_load_si128(reinterpret_cast<const __m128i*>(tail)));
-            k += 16;
-        }
-        ch.pend = nullptr;
-        return k;
+        return;
     }
     if (((uintptr_t)ch.pend_slot & 15u) == 0) {
         // whole 16-B chunks of the frame with vector loads; the last partial chunk with
@@ -190,7 +153,6 @@ inline uint32_t copy_prefix(Chain& ch) {
         std::memcpy(ch.pend_slot, ch.pend, m);
     }
     ch.pend = nullptr;
-    return m;
 }
 
 template <WalkMode MODE>
@@ -229,10 +191,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                     ++g;
                     continue;
                 }
-                if (MODE != kWalkOnly && ch.pend) {   // its lines were prefetched a round ago
-                    const uint32_t took = copy_prefix<MODE>(ch);
-                    if (MODE == kGatherDensePlain || MODE == kGatherDenseLine) ch.line += took;
-                }
+                if (MODE != kWalkOnly && ch.pend) copy_prefix<MODE>(ch);   // its lines were prefetched a round ago
                 if (ch.off + sizeof(tpacket3_hdr) > bs) return ch.block;
                 const tpacket3_hdr* h = reinterpret_cast<const tpacket3_hdr*>(ch.blk + ch.off);
                 const uint64_t mac = ch.off + h->tp_mac;
@@ -240,9 +199,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                 if (mac + snap > bs) return ch.block;
                 if (MODE != kWalkOnly) {
                     const uint64_t i = ch.first + ch.j;
-                    ch.pend_slot = MODE == kGatherDense ? dense_at(ch)
-                                   : MODE == kGatherDensePlain || MODE == kGatherDenseLine ? ch.line
-                                   : slots + i * BT_PREFIX_SLOT;
+                    ch.pend_slot = MODE == kGatherDense ? dense_at(ch) : slots + i * BT_PREFIX_SLOT;
                     ch.out[ch.j] = BT_DESC((uint64_t)(ch.pend_slot - slots), std::min<uint32_t>(snap, kDescLenMax));
                     ch.pend = ch.blk + mac;
                     ch.pend_len = snap;
@@ -273,14 +230,6 @@ extern "C" {
 
 namespace {
 
-// The dense gather's store kind (A/B switch, read per call): BT_GATHER_MODE = staged
-// (default), plain, line.
-int gather_kind() {
-    const char* e = std::getenv("BT_GATHER_MODE");
-    if (!e) return 0;
-    return std::strcmp(e, "plain") == 0 ? 1 : std::strcmp(e, "line") == 0 ? 2 : 0;
-}
-
 int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks, uint8_t* slots,
               bool dense, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
     if (!ring || !ring->base || !n_desc || !n_blocks_taken || (cap && !desc))
@@ -309,15 +258,12 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
     //    worker interleaving up to kChains block chains
     const uint32_t nb = (uint32_t)blocks.size();
     std::atomic<int64_t> bad{-1};
-    const int kind = slots && dense ? gather_kind() : 0;
     auto work = [&](unsigned w, unsigned T) {
         const uint32_t a = (uint32_t)((uint64_t)nb * w / T), b = (uint32_t)((uint64_t)nb * (w + 1) / T);
         if (a >= b) return;
         const int64_t e =
             !slots ? walk_blocks<kWalkOnly>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr)
-            : dense ? (kind == 1 ? walk_blocks<kGatherDensePlain>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
-                       : kind == 2 ? walk_blocks<kGatherDenseLine>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
-                                   : walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots))
+            : dense ? walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
                     : walk_blocks<kGatherSlots>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots);
         if (slots) _mm_sfence();   // this worker's streaming stores land before the join
         if (e >= 0) bad.store(e);

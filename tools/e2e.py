@@ -30,6 +30,9 @@ ap.add_argument("--gather", action="store_true",
                      "slots (bt_ring_gather_tpv3) and the kernels read the slots (BT_BATCH_PREFIXES)")
 ap.add_argument("--dense", action="store_true",
                 help="with --gather: each block's prefixes packed back to back (bt_ring_gather_dense_tpv3)")
+ap.add_argument("--mix", type=int, default=0,
+                help="with --gather: every N-th batch is walked and read in place instead (the host "
+                     "gathers, the GPU reads the other batches' frames over PCIe itself)")
 ap.add_argument("--gpu-walk", action="store_true",
                 help="with --tpacket: the frame chains are walked on the GPU (bt_ring_walk_tpv3_gpu: the host "
                      "reads only the block headers), descriptors in device memory")
@@ -72,7 +75,8 @@ if a.tpacket:
         def one_pass(walk=True):
             start, tile = 0, 0
             for k in range(nbat):
-                if walk and a.gather:
+                gathered = a.gather and not (a.mix and k % a.mix == a.mix - 1)
+                if walk and gathered:
                     got, taken = abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B,
                                                       max_blocks=min(B, used - k * B), ctx=ctx, slot_base=start,
                                                       dense=a.dense)
@@ -92,7 +96,7 @@ if a.tpacket:
                         counts.append(cnt)
                 else:
                     cnt = counts[k]
-                if a.gather:
+                if gathered:
                     batch = abi.Batch(d_slots + abi.PREFIX_SLOT * start, d_desc + 8 * start, 0, cnt,
                                       abi.PREFIX_SLOT * cnt, abi.DESC_PACKED, abi.BATCH_PREFIXES)
                 else:
@@ -123,7 +127,7 @@ if a.tpacket:
                 abi.ring_walk_tpv3_gpu(ctx, ring, d_ring, bs, used, g_desc.ptr, n + 64, first=k * B,
                                        max_blocks=min(B, used - k * B))
                 continue
-            if a.gather:
+            if a.gather and not (a.mix and k % a.mix == a.mix - 1):
                 abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B, max_blocks=min(B, used - k * B),
                                      ctx=ctx, dense=a.dense)
             else:
@@ -133,7 +137,9 @@ if a.tpacket:
         walk = time.perf_counter() - t0
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
-        how = "tpacket_v3 ring, header gather packed per block, zero-copy, " if a.gather and a.dense else \
+        how = f"tpacket_v3 ring, header gather packed per block, every {a.mix}th batch in place, zero-copy, " \
+            if a.gather and a.dense and a.mix else \
+            "tpacket_v3 ring, header gather packed per block, zero-copy, " if a.gather and a.dense else \
             "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
             "tpacket_v3 ring, chains walked on the GPU, zero-copy, " if a.gpu_walk else "tpacket_v3 ring, zero-copy, "
         print(json.dumps({"config": a.config, "flags": a.flags, "mode": how + mode, "packets": n,

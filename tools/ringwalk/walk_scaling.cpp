@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
         printf("ring registered with the GPU\n");
     }
     if (mode == "gather") {
-        // walk / gather into 128-B slots / dense staged / dense plain, interleaved, through a
+        // walk / gather into 128-B slots / dense gather, interleaved, through a
         // pool of maxT threads, 128 blocks per call; best of 5 rounds each
         bt_opts o{};
         o.host_threads = maxT;
@@ -61,13 +61,10 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> slots((n + 64) * BT_PREFIX_SLOT + 64);
         uint8_t* sl = slots.data() + ((64 - ((uintptr_t)slots.data() & 63)) & 63);
         for (auto& x : slots) x = 0;
-        const char* names[5] = {"walk", "gather 128-B slots", "gather dense, staged lines", "gather dense, plain stores",
-                                "gather dense, 64-B lines"};
-        const char* kinds[5] = {"staged", "staged", "staged", "plain", "line"};
-        double best[5] = {1e9, 1e9, 1e9, 1e9, 1e9};
+        const char* names[3] = {"walk", "gather 128-B slots", "gather dense"};
+        double best[3] = {1e9, 1e9, 1e9};
         for (int rep = 0; rep < 5; ++rep)
-            for (int m = 0; m < 5; ++m) {
-                setenv("BT_GATHER_MODE", kinds[m], 1);
+            for (int m = 0; m < 3; ++m) {
                 const auto t0 = std::chrono::steady_clock::now();
                 for (uint64_t b0 = 0; b0 < used; b0 += 128) {
                     uint32_t nd = 0, nb = 0;
@@ -83,7 +80,7 @@ int main(int argc, char** argv) {
                 }
                 best[m] = std::min(best[m], std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
             }
-        for (int m = 0; m < 5; ++m) printf("cfg %d threads %u  %-28s %.1f Mpps\n", cfg, maxT, names[m], n / best[m] / 1e6);
+        for (int m = 0; m < 3; ++m) printf("cfg %d threads %u  %-28s %.1f Mpps\n", cfg, maxT, names[m], n / best[m] / 1e6);
         if (c) bt_destroy(c);
         return 0;
     }
