@@ -217,7 +217,7 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(u32), ctypes.POINTER(u32), vp, vp]),
         "bt_ring_gather_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
                                                ctypes.POINTER(u32), ctypes.POINTER(u32)]),
-        "bt_ring_gather_dense_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
+        "bt_ring_gather_dense_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, vp, u32,
                                                      ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
@@ -576,20 +576,27 @@ BATCH_PREFIXES = 0x1
 
 def ring_gather_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, slots: np.ndarray, out: np.ndarray,
                      first: int = 0, max_blocks: int | None = None, ctx: "Context | None" = None,
-                     slot_base: int = 0, dense: bool = False):
+                     slot_base: int = 0, dense: bool = False, ring_out: np.ndarray | None = None):
     """bt_ring_gather_tpv3: the walk of ring_walk_tpv3, plus every frame's header prefix
     copied into slots[(slot_base + i) * PREFIX_SLOT ...]; descriptors (written to
     out[slot_base:]) point into `slots`. dense=True: bt_ring_gather_dense_tpv3 (each block's
-    prefixes back to back from its first slot). Returns (desc view, blocks taken)."""
+    prefixes back to back from its first slot; ring_out[slot_base:] gets the ring descriptors).
+    Returns (desc view, blocks taken)."""
     if slots.dtype != np.uint8 or not slots.flags.c_contiguous or out.dtype != np.uint64:
         raise ValueError("slots must be contiguous uint8, out uint64")
-    fn = lib().bt_ring_gather_dense_tpv3 if dense else lib().bt_ring_gather_tpv3
+    if ring_out is not None and (not dense or ring_out.dtype != np.uint64 or len(ring_out) < len(out)):
+        raise ValueError("ring_out: uint64, as long as out, dense gather only")
     cap = min(len(out) - slot_base, len(slots) // PREFIX_SLOT - slot_base)
     r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
     nd, nb = ctypes.c_uint32(), ctypes.c_uint32()
-    _check(fn(ctx.h if ctx else None, ctypes.byref(r), first, n_blocks if max_blocks is None else max_blocks,
-              slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base,
-              cap, ctypes.byref(nd), ctypes.byref(nb)))
+    args = (ctx.h if ctx else None, ctypes.byref(r), first, n_blocks if max_blocks is None else max_blocks,
+            slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base)
+    tail = (cap, ctypes.byref(nd), ctypes.byref(nb))
+    if dense:
+        rd = None if ring_out is None else ring_out.ctypes.data + 8 * slot_base
+        _check(lib().bt_ring_gather_dense_tpv3(*args, rd, *tail))
+    else:
+        _check(lib().bt_ring_gather_tpv3(*args, *tail))
     return out[slot_base:slot_base + nd.value], nb.value
 
 

@@ -54,6 +54,7 @@ struct Chain {
     uint64_t base_off, off;
     uint32_t j, n, delay;
     bt_pkt_desc* out;
+    bt_pkt_desc* rout;         // dense gather: the frames' ring descriptors too (optional)
     int64_t block;
     uint64_t first;            // global index of the block's first frame (slot numbering)
     const uint8_t* pend;       // gather: frame whose prefix is copied on the next visit
@@ -157,7 +158,7 @@ inline void copy_prefix(Chain& ch) {
 
 template <WalkMode MODE>
 int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_t* start, uint32_t count,
-                    bt_pkt_desc* desc, uint8_t* slots) {
+                    bt_pkt_desc* desc, uint8_t* slots, bt_pkt_desc* ring_desc) {
     const uint64_t bs = r->block_size;
     for (uint32_t g0 = 0; g0 < count; g0 += kChains) {
         Chain c[kChains];
@@ -172,6 +173,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
             ch.n = bd->hdr.bh1.num_pkts;
             ch.j = 0;
             ch.out = desc + start[k];
+            ch.rout = ring_desc ? ring_desc + start[k] : nullptr;
             ch.block = b;
             ch.first = start[k];
             ch.pend = nullptr;
@@ -201,6 +203,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                     const uint64_t i = ch.first + ch.j;
                     ch.pend_slot = MODE == kGatherDense ? dense_at(ch) : slots + i * BT_PREFIX_SLOT;
                     ch.out[ch.j] = BT_DESC((uint64_t)(ch.pend_slot - slots), std::min<uint32_t>(snap, kDescLenMax));
+                    if (ch.rout) ch.rout[ch.j] = BT_DESC(ch.base_off + mac, std::min<uint32_t>(snap, kDescLenMax));
                     ch.pend = ch.blk + mac;
                     ch.pend_len = snap;
                     __builtin_prefetch(ch.pend);
@@ -231,7 +234,8 @@ extern "C" {
 namespace {
 
 int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks, uint8_t* slots,
-              bool dense, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
+              bool dense, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap, uint32_t* n_desc,
+              uint32_t* n_blocks_taken) {
     if (!ring || !ring->base || !n_desc || !n_blocks_taken || (cap && !desc))
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3: null argument");
     if (!ring->n_blocks || ring->block_size < sizeof(tpacket_block_desc) || first_block >= ring->n_blocks)
@@ -262,9 +266,9 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
         const uint32_t a = (uint32_t)((uint64_t)nb * w / T), b = (uint32_t)((uint64_t)nb * (w + 1) / T);
         if (a >= b) return;
         const int64_t e =
-            !slots ? walk_blocks<kWalkOnly>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr)
-            : dense ? walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots)
-                    : walk_blocks<kGatherSlots>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots);
+            !slots ? walk_blocks<kWalkOnly>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr, nullptr)
+            : dense ? walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots, ring_desc)
+                    : walk_blocks<kGatherSlots>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots, nullptr);
         if (slots) _mm_sfence();   // this worker's streaming stores land before the join
         if (e >= 0) bad.store(e);
     };
@@ -282,23 +286,23 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
 
 int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                       bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
-    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, false, desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, false, desc, nullptr, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                         uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
                         uint32_t* n_blocks_taken) {
     if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_tpv3: null slots");
-    return ring_walk(ctx, ring, first_block, max_blocks, slots, false, desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, false, desc, nullptr, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
-                              uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
-                              uint32_t* n_blocks_taken) {
+                              uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
+                              uint32_t* n_desc, uint32_t* n_blocks_taken) {
     if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: null slots");
     if ((uintptr_t)slots & 15u)
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: slots not 16-B aligned");
-    return ring_walk(ctx, ring, first_block, max_blocks, slots, true, desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, true, desc, ring_desc, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count) {

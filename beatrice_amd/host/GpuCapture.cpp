@@ -263,21 +263,31 @@ GpuTpacketStage::GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring, O
     reg(decide_.data(), decide_.size(), &decideDev_);
     reg(verdict_.data(), verdict_.size() * 8, &verdictDev_);
     if (opts_.records) reg(records_.data(), records_.size(), &recordsDev_);
+    if (opts_.gather) {
+        slots_.resize((size_t)cap * BT_PREFIX_SLOT + 64);
+        slotDesc_.resize(cap);
+        reg(slots_.data(), slots_.size(), &slotsDev_);
+        reg(slotDesc_.data(), slotDesc_.size() * sizeof(bt_pkt_desc), &slotDescDev_);
+    }
 }
 
 GpuTpacketStage::~GpuTpacketStage() {
     bt_ctx* ctx = filter_.context();
     (void)bt_synchronize(ctx);
     for (void* p : {(void*)ringBase_, (void*)desc_.data(), (void*)decide_.data(), (void*)verdict_.data(),
-                    (void*)records_.data()})
-        if (p && (p != records_.data() || opts_.records)) (void)bt_host_unregister(ctx, p);
+                    (void*)records_.data(), (void*)slots_.data(), (void*)slotDesc_.data()})
+        if (p) (void)bt_host_unregister(ctx, p);
 }
 
 const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds timeout) {
     batch_ = Batch{};
     if (!ring_.waitReady(timeout)) return batch_;
     uint32_t n = 0;
-    auto taken = ring_.take(filter_.context(), opts_.maxBlocks, desc_.data(), opts_.maxPackets, &n);
+    const bool gathered = opts_.gather && !(opts_.inPlaceEvery && polls_ % opts_.inPlaceEvery == opts_.inPlaceEvery - 1);
+    ++polls_;
+    auto taken = gathered ? ring_.takeGathered(filter_.context(), opts_.maxBlocks, slots_.data(), slotDesc_.data(),
+                                               desc_.data(), opts_.maxPackets, &n)
+                          : ring_.take(filter_.context(), opts_.maxBlocks, desc_.data(), opts_.maxPackets, &n);
     if (taken.isError()) throw std::runtime_error("GpuTpacketStage: " + taken.getErrorMessage());
     batch_.blocks = taken.getValue();
     if (batch_.blocks == 0)   // a single ready block with more frames than maxPackets
@@ -287,12 +297,14 @@ const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds ti
     batch_.decide = decide_.data();
     batch_.verdict = verdict_.data();
     batch_.records = opts_.records ? records_.data() : nullptr;
+    batch_.gathered = gathered;
     bt_batch b{};
-    b.base = static_cast<const uint8_t*>(ringDev_);
-    b.desc = descDev_;
+    b.base = static_cast<const uint8_t*>(gathered ? slotsDev_ : ringDev_);
+    b.desc = gathered ? slotDescDev_ : descDev_;
     b.n = n;
-    b.bytes = ring_.bytes();
+    b.bytes = gathered ? slots_.size() : ring_.bytes();
     b.desc_format = BT_DESC_PACKED;
+    b.flags = gathered ? BT_BATCH_PREFIXES : 0u;   // PAYLOAD slots: resolved on the host from the frame
     bt_outputs o{};
     o.records = recordsDev_;
     o.n_cap = opts_.maxPackets;

@@ -104,6 +104,12 @@ public:
                                         // frame chains walked in parallel)
         uint32_t maxPackets = 1u << 20; // descriptors per batch (upper bound)
         bool records = false;           // also write bt_rec records (device tiled layout)
+        // Header gather (bt_ring_gather_dense_tpv3): the walker packs each frame's header
+        // prefix into registered slots and the kernels read those instead of the ring over
+        // PCIe. inPlaceEvery = k > 0: every k-th batch is still read in
+        // place, sharing the work between the host's copy and the GPU's PCIe reads.
+        bool gather = false;
+        uint32_t inPlaceEvery = 0;
     };
     // One batch of ring blocks, owned by the caller until release().
     struct Batch {
@@ -113,6 +119,7 @@ public:
         const uint64_t* verdict = nullptr;   // bit i = packet i passed
         const void* records = nullptr;       // tiled (include/beatrice_gpu.h); records == true only
         std::vector<uint32_t> pass;          // ascending
+        bool gathered = false;               // the kernels read packed header prefixes
     };
 
     // The filter supplies the context (device, stream) and the compiled program; the
@@ -147,6 +154,11 @@ private:
     std::vector<uint64_t> verdict_;
     std::vector<uint8_t> records_;
     void *descDev_ = nullptr, *decideDev_ = nullptr, *verdictDev_ = nullptr, *recordsDev_ = nullptr;
+    // header gather: packed prefixes and their descriptors (registered)
+    std::vector<uint8_t> slots_;
+    std::vector<bt_pkt_desc> slotDesc_;
+    void *slotsDev_ = nullptr, *slotDescDev_ = nullptr;
+    uint64_t polls_ = 0;
     Batch batch_;
 };
 

@@ -61,6 +61,10 @@ public:
     // walks up to maxBlocks ready blocks from the cursor (bt_ring_walk_tpv3 on ctx's
     // host pool; ctx may be null); desc receives ring-relative descriptors
     Result<uint32_t> take(bt_ctx* ctx, uint32_t maxBlocks, bt_pkt_desc* desc, uint32_t cap, uint32_t* n);
+    // the same walk, with each frame's header prefix packed into `slots` (bt_ring_gather_dense_tpv3:
+    // slotDesc points into slots, ringDesc at the frames)
+    Result<uint32_t> takeGathered(bt_ctx* ctx, uint32_t maxBlocks, uint8_t* slots, bt_pkt_desc* slotDesc,
+                                  bt_pkt_desc* ringDesc, uint32_t cap, uint32_t* n);
     // hands `blocks` blocks back to the kernel starting at the cursor and advances it
     void release(uint32_t blocks);
     Stats statistics();

@@ -452,14 +452,16 @@ int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_b
 /* The same gather with the prefixes packed: the frames of the k-th taken block (whose first
  * descriptor is j_k) go back to back, each 16-B aligned and taking its prefix length rounded
  * up to 16, from byte j_k * BT_PREFIX_SLOT of `slots` (16-B aligned, BT_PREFIX_SLOT * cap
- * bytes, as above); desc[i] = BT_DESC(offset of frame i's prefix, min(tp_snaplen, 65535)).
+ * bytes, as above); desc[i] = BT_DESC(offset of frame i's prefix, min(tp_snaplen, 65535)),
+ * and ring_desc[i] (optional, cap entries) = frame i's ring descriptor as bt_ring_walk_tpv3
+ * writes it, for what reads the whole frame (PAYLOAD / CUSTOM slots, forwarding).
  * A block's packets then sit in consecutive bytes (a 42-B UDP header in 48 B), so the
  * kernels' reads of a tile are one contiguous run over PCIe instead of one 128-B slot per
  * packet. Bytes past a prefix belong to the next frame: the batch flag BT_BATCH_PREFIXES
  * (PAYLOAD slots decided on the host) is required as for the slots. */
 int  bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
-                               uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
-                               uint32_t* n_blocks_taken);
+                               uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
+                               uint32_t* n_desc, uint32_t* n_blocks_taken);
 /* The walk with the frame chains followed on the GPU. The host reads only the taken blocks'
  * headers (block_status, num_pkts, offset_to_first_pkt: one line per block) and a kernel on
  * `stream` walks every chain through ring_dev (the ring's device-visible alias, e.g. from

@@ -171,7 +171,7 @@ static std::string kind_of(const std::exception_ptr& e) {
 }
 
 static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32_t nb, const std::vector<Spec>& specs,
-                       uint32_t maxBlocks, bool records) {
+                       uint32_t maxBlocks, bool records, bool gather = false, uint32_t inPlaceEvery = 0) {
     // fresh copy of the image: the stage hands blocks back (status -> kernel)
     std::vector<uint8_t> mem(ring_mem, ring_mem + (size_t)bs * nb);
     TpacketV3Ring ring;
@@ -185,9 +185,11 @@ static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32
     o.maxBlocks = maxBlocks;
     o.maxPackets = 1u << 20;
     o.records = records;
+    o.gather = gather;
+    o.inPlaceEvery = inPlaceEvery;
     GpuTpacketStage stage(gpu, ring, o);
     uint64_t total = 0, passed = 0;
-    uint32_t batches = 0;
+    uint32_t batches = 0, gathered = 0;
     for (;;) {
         std::vector<Packet> pk;
         std::exception_ptr eg, er;
@@ -215,6 +217,9 @@ static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32
         }
         if (b->n == 0 && b->blocks == 0) break;
         ++batches;
+        gathered += b->gathered;
+        CHECK(b->gathered == (gather && !(inPlaceEvery && batches % inPlaceEvery == 0)), "%s: batch %u gathered=%d",
+              label, batches, b->gathered);
         for (uint32_t i = 0; i < b->n; ++i)
             pk.emplace_back(std::shared_ptr<const uint8_t[]>(stage.frame(i), [](const uint8_t*) {}),
                             (size_t)stage.length(i));
@@ -265,8 +270,9 @@ static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32
           "%s: stats differ (processed %lu/%lu passed %lu/%lu)", label, (unsigned long)sa.packetsProcessed,
           (unsigned long)sb.packetsProcessed, (unsigned long)sa.packetsPassed, (unsigned long)sb.packetsPassed);
     CHECK(total > 0, "%s: nothing drained", label);
-    std::printf("ok   stage %-20s %lu frames in %u batches, %lu passed%s\n", label, (unsigned long)total, batches,
-                (unsigned long)passed, records ? ", records equal" : "");
+    CHECK(!gather || gathered > 0, "%s: no batch was gathered", label);
+    std::printf("ok   stage %-20s %lu frames in %u batches (%u gathered), %lu passed%s\n", label, (unsigned long)total,
+                batches, gathered, (unsigned long)passed, records ? ", records equal" : "");
     return true;
 }
 
@@ -301,6 +307,9 @@ int main(int argc, char** argv) {
         stage_case("lo/host-slots", img.data(), bs, nb, kHost, 16, false);
         stage_case("lo/throws", img.data(), bs, nb, kThrow, 1, false);
         stage_case("lo/no-filters", img.data(), bs, nb, {}, 3, false);
+        stage_case("lo/headline gathered", img.data(), bs, nb, kHeadline, 1, true, true);
+        stage_case("lo/payload+custom g", img.data(), bs, nb, kLoopback, 2, false, true, 2);
+        stage_case("lo/throws gathered", img.data(), bs, nb, kThrow, 1, false, true);
     } else if (mode == "stage-synth") {
         const uint32_t n = 300000, bs = 1u << 20;
         std::vector<uint64_t> desc(n);
@@ -316,6 +325,8 @@ int main(int argc, char** argv) {
         }
         stage_case("c3/headline", ring.data(), bs, (uint32_t)used, kHeadline, 8, true);
         stage_case("c3/host-slots", ring.data(), bs, (uint32_t)used, kHost, 32, false);
+        stage_case("c3/headline gathered", ring.data(), bs, (uint32_t)used, kHeadline, 8, true, true);
+        stage_case("c3/host-slots mixed", ring.data(), bs, (uint32_t)used, kHost, 8, false, true, 3);
     } else {
         std::printf("usage: test_capture backend | stage <ring.bin> <block_size> <n_blocks> | stage-synth\n");
         return 2;

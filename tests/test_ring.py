@@ -224,9 +224,10 @@ def test_dense_gather_packs_each_block(which):
     wdesc, taken = abi.ring_walk_tpv3(ring, bs, used)
     n = len(wdesc)
     slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)
-    out = np.zeros(n, np.uint64)
-    gdesc, gtaken = abi.ring_gather_tpv3(ring, bs, used, slots, out, dense=True)
+    out, rout = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    gdesc, gtaken = abi.ring_gather_tpv3(ring, bs, used, slots, out, dense=True, ring_out=rout)
     assert gtaken == taken and len(gdesc) == n
+    assert np.array_equal(rout, wdesc)   # the frames' own descriptors alongside
     lens = synth.desc_len(wdesc).astype(np.int64)
     assert np.array_equal(synth.desc_len(gdesc), synth.desc_len(wdesc))
     goff = synth.desc_off(gdesc).astype(np.int64)

@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
                                             cap, &nd, &nb);
                     else
                         bt_ring_gather_dense_tpv3(c, &r, (uint32_t)b0, 128, sl + first[b0] * BT_PREFIX_SLOT,
-                                                  out.data() + first[b0], cap, &nd, &nb);
+                                                  out.data() + first[b0], nullptr, cap, &nd, &nb);
                 }
                 best[m] = std::min(best[m], std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
             }
