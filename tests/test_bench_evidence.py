@@ -118,6 +118,7 @@ def test_rocprof_stats_agree_with_bench_events(cfg):
 
 
 R02 = os.path.join(ROOT, "profiles", "r02")
+ROUNDS = ["r02", "r03"]   # the closing files of each round since the bench took its current form
 
 
 def _check_entry(e, n_gpus=1):
@@ -137,8 +138,9 @@ def _check_entry(e, n_gpus=1):
         assert r["traffic_bytes_per_packet"] >= 0.97 * r["traffic_floor_bytes_per_packet"]
 
 
-def test_r02_default_line_covers_every_config():
-    d = _line(os.path.join(R02, "bench_default.json"))
+@pytest.mark.parametrize("rnd", ROUNDS)
+def test_default_line_covers_every_config(rnd):
+    d = _line(os.path.join(ROOT, "profiles", rnd, "bench_default.json"))
     assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
     assert d["n_gpus"] == 1 and "parse + PacketFilter" in d["config"]["workload"] and "64B" in d["config"]["workload"]
     _check_entry(d)
@@ -153,12 +155,13 @@ def test_r02_default_line_covers_every_config():
     assert d["value"] == pytest.approx(d["config"]["packets_total"] / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
 
 
-def test_r02_default_line_timing_form():
+@pytest.mark.parametrize("rnd", ROUNDS)
+def test_default_line_timing_form(rnd):
     """The committed line's timed region: pipelined compaction over two output sets for
     the entries with a filter, no per-kernel events inside it, and a kernel pass (events
     on every main kernel) whose mean is the roofline's kernel_ms and whose steps run as
     fast as the timed ones (the warm-up leads straight into the timed region)."""
-    d = _line(os.path.join(R02, "bench_default.json"))
+    d = _line(os.path.join(ROOT, "profiles", rnd, "bench_default.json"))
     entries = [("c2f", d)] + list(d["configs"].items())
     for k, e in entries:
         t, r = e["timing"], e["roofline"]
@@ -174,8 +177,9 @@ def test_r02_default_line_timing_form():
             assert t["pipelined"] == (k != "c2") and t["output_sets"] == (1 if k == "c2" else 2), k
 
 
-def test_r02_two_rank_line_has_per_rank_entries():
-    d = _line(os.path.join(R02, "bench_2rank_one_gpu.json"))
+@pytest.mark.parametrize("rnd", ROUNDS)
+def test_two_rank_line_has_per_rank_entries(rnd):
+    d = _line(os.path.join(ROOT, "profiles", rnd, "bench_2rank_one_gpu.json"))
     assert d["n_gpus"] == 2 and len(d["per_rank"]) == 2
     assert set(d["configs"]) == {"c3", "c3_strong"}
     assert d["configs"]["c3"]["scaling"] == "weak" and d["configs"]["c3_strong"]["scaling"] == "strong"
@@ -183,8 +187,9 @@ def test_r02_two_rank_line_has_per_rank_entries():
     assert sum(r["packets"] for r in s["per_rank"]) == s["packets_total"] == 1 << 24
 
 
-def test_r02_four_rank_line_splits_the_strong_batch():
-    d = _line(os.path.join(R02, "bench_4rank_one_gpu.json"))
+@pytest.mark.parametrize("rnd", ROUNDS)
+def test_four_rank_line_splits_the_strong_batch(rnd):
+    d = _line(os.path.join(ROOT, "profiles", rnd, "bench_4rank_one_gpu.json"))
     assert d["n_gpus"] == 4 and len(d["per_rank"]) == 4 and d["scaling"] == "weak"
     s = d["configs"]["c3_strong"]
     parts = [r["packets"] for r in s["per_rank"]]
@@ -192,10 +197,11 @@ def test_r02_four_rank_line_splits_the_strong_batch():
     assert max(parts) - min(parts) < 1 << 12   # byte-balanced shards of near-equal size here
 
 
+@pytest.mark.parametrize("rnd", ROUNDS)
 @pytest.mark.parametrize("cfg", ["c2f", "c2", "c3", "c4", "c1"])
-def test_r02_rocprof_stats_agree_with_bench_events(cfg):
-    under = _line(os.path.join(R02, "prof", f"{cfg}_bench_under_rocprof.json"))
-    with open(os.path.join(R02, "prof", f"{cfg}_kernel_stats.csv")) as fh:
+def test_round_rocprof_stats_agree_with_bench_events(rnd, cfg):
+    under = _line(os.path.join(ROOT, "profiles", rnd, "prof", f"{cfg}_bench_under_rocprof.json"))
+    with open(os.path.join(ROOT, "profiles", rnd, "prof", f"{cfg}_kernel_stats.csv")) as fh:
         rows = [x for x in csv.DictReader(fh) if "parse_filter_" in x["Name"] or "extract_tile" in x["Name"]]
     assert len(rows) == 1
     assert under["roofline"]["kernel"] in rows[0]["Name"]
@@ -207,3 +213,14 @@ def test_committed_traffic_is_keyed_to_these_kernels():
     assert set(d) >= {"c2f", "c2", "c3", "c4"}
     for k, v in d.items():
         assert v["kernel_src_sha"] == bench.kernel_source_sha(), f"{k}: PMC traffic measured on other kernel sources"
+
+
+def test_r03_rank_lines_come_from_the_self_spawning_launcher():
+    """Round 3's rehearsals ran `bench.py --gpus N` with no torchrun (the ranks spawned by
+    bench.py itself) on the one-GPU box: the device check reports the shared device."""
+    for n in (2, 4):
+        d = _line(os.path.join(ROOT, "profiles", "r03", f"bench_{n}rank_one_gpu.json"))
+        assert d["n_gpus"] == n and len(d["per_rank"]) == n
+        c = d["config"]
+        assert c["rehearsal_one_device"] is True and c["devices_distinct"] == 1   # distinct devices used
+        assert len(c["pci_bus_ids"]) == n and len(set(c["pci_bus_ids"])) == 1
