@@ -654,6 +654,8 @@ def main():
               flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        args.no_cpu = True   # the CPU baseline is a rank-0, N=1 figure: an N > 1 line carries none
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -44,7 +44,7 @@ for step in $STEPS; do
       python3 tools/summ.py "$OUT/bench_default.json" ;;
     multi)
       for n in 2 4; do
-        BT_BENCH_DEVICE=0 timeout -k 10 600 python bench.py --gpus $n --cpu-seconds 2 \
+        BT_BENCH_DEVICE=0 timeout -k 10 600 python bench.py --gpus $n \
           > "$OUT/bench_${n}rank_one_gpu.json" 2> "$OUT/bench_${n}rank.err" || fail multi$n $? "$OUT/bench_${n}rank.err"
         python3 tools/summ.py "$OUT/bench_${n}rank_one_gpu.json"
       done ;;
