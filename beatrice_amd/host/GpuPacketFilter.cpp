@@ -250,6 +250,17 @@ void advise_huge(void* p, size_t bytes) {
     if (e > a) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
 }
 
+// Faults the (still unconstructed) storage in on the host threads, one write per 4 KiB
+// page, so the serial default construction that follows runs on resident memory instead
+// of taking every page fault (and the zeroing behind it) on the calling thread.
+void prefault(bt_ctx* ctx, void* p, size_t bytes) {
+    if (bytes < (size_t(16) << 20)) return;
+    auto* b = static_cast<volatile uint8_t*>(p);
+    parallel_ranges(ctx, (bytes + 4095) / 4096, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) b[k * 4096] = 0;
+    });
+}
+
 }  // namespace
 
 void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
@@ -371,6 +382,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
     // result either way, its strings are copied rather than concatenated per packet.
     results.reserve(t.stop);
     advise_huge(results.data(), t.stop * sizeof(FilterResult));
+    prefault(ctx_, results.data(), t.stop * sizeof(FilterResult));
     results.resize(t.stop);
     parallel_ranges(ctx_, t.stop, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
