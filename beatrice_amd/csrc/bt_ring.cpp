@@ -46,7 +46,10 @@ inline uint32_t status_acquire(const tpacket_block_desc* bd) {
 // block_size-aligned, so chains that advance in phase sit at equal offsets in their
 // blocks and collide in the same cache sets (measured: C3 with 1 MiB blocks stopped
 // scaling past one thread without it). Returns the first malformed block, or -1.
-constexpr int kChains = 16;
+#ifndef BT_RING_CHAINS
+#define BT_RING_CHAINS 16   // a build knob for A/B
+#endif
+constexpr int kChains = BT_RING_CHAINS;
 constexpr uint32_t kStagger = 4;
 
 struct Chain {
