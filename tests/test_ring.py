@@ -117,6 +117,18 @@ def test_malformed_ring_is_rejected():
         abi.ring_walk_tpv3(bad, bs, used)
     with pytest.raises(abi.BtError):
         abi.ring_walk_tpv3(ring, bs, used, first=used)
+    # the gathers walk the same chains and refuse the same rings
+    n = len(desc) + 64
+    for dense in (False, True):
+        bad = ring.copy()
+        bad[off:off + 4] = np.frombuffer(struct.pack("<I", bs), np.uint8)
+        slots, out = np.zeros(n * abi.PREFIX_SLOT, np.uint8), np.zeros(n, np.uint64)
+        with pytest.raises(abi.BtError, match="frame chain leaves the block"):
+            abi.ring_gather_tpv3(bad, bs, used, slots, out, dense=dense)
+    with pytest.raises(abi.BtError, match="16-B aligned"):
+        abi.ring_gather_tpv3(ring, bs, used, np.zeros(n * abi.PREFIX_SLOT + 16, np.uint8)[1:], out, dense=True)
+    with pytest.raises(ValueError):   # ring descriptors come with the packed gather only
+        abi.ring_gather_tpv3(ring, bs, used, slots, out, dense=False, ring_out=np.zeros(n, np.uint64))
 
 
 def _can_raw():
