@@ -1070,6 +1070,8 @@ int bt_host_unregister(bt_ctx* c, void* host) {
     // compaction stream, callers' streams) has finished before its mapping goes away
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipHostUnregister(host));
+    std::lock_guard<std::mutex> lk(c->mu);   // host_resident's cache (read under mu): the
+    c->last_base = nullptr;                   // address may come back as another kind
     return BT_OK;
 }
 
@@ -1090,6 +1092,8 @@ int bt_dev_free(bt_ctx* c, void* p) {
     if (!p) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipFree(p));   // implicitly waits for the device: no queued kernel still uses p
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->last_base = nullptr;   // host_resident's cache (as bt_host_unregister)
     return BT_OK;
 }
 

@@ -96,7 +96,7 @@ void GpuPacketFilter::open(const std::vector<int>& devices, const bt_opts* opts)
 GpuPacketFilter::~GpuPacketFilter() { bt_group_destroy(group_); }
 
 Result<void> GpuPacketFilter::addFilter(const std::string& name, const FilterConfig& config) {
-    std::lock_guard<std::mutex> lock(filtersMutex_);   // :19-31
+    std::unique_lock<std::shared_mutex> lock(filtersMutex_);   // :19-31
     if (filters_.find(name) != filters_.end())
         return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter already exists: " + name);
     FilterEntry entry;
@@ -107,7 +107,7 @@ Result<void> GpuPacketFilter::addFilter(const std::string& name, const FilterCon
 }
 
 Result<void> GpuPacketFilter::removeFilter(const std::string& name) {
-    std::lock_guard<std::mutex> lock(filtersMutex_);   // :33-43
+    std::unique_lock<std::shared_mutex> lock(filtersMutex_);   // :33-43
     auto it = filters_.find(name);
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     filters_.erase(it);
@@ -116,7 +116,7 @@ Result<void> GpuPacketFilter::removeFilter(const std::string& name) {
 }
 
 Result<void> GpuPacketFilter::setFilterEnabled(const std::string& name, bool enabled) {
-    std::lock_guard<std::mutex> lock(filtersMutex_);   // :45-55
+    std::unique_lock<std::shared_mutex> lock(filtersMutex_);   // :45-55
     auto it = filters_.find(name);
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     it->second.config.enabled = enabled;
@@ -125,7 +125,7 @@ Result<void> GpuPacketFilter::setFilterEnabled(const std::string& name, bool ena
 }
 
 Result<void> GpuPacketFilter::setCustomFilter(const std::string& name, std::function<bool(const Packet&)> filterFunc) {
-    std::lock_guard<std::mutex> lock(filtersMutex_);   // :155-166
+    std::unique_lock<std::shared_mutex> lock(filtersMutex_);   // :155-166
     auto it = filters_.find(name);
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     it->second.customFunc = std::move(filterFunc);
@@ -134,7 +134,7 @@ Result<void> GpuPacketFilter::setCustomFilter(const std::string& name, std::func
 }
 
 std::vector<std::string> GpuPacketFilter::getActiveFilters() const {
-    std::lock_guard<std::mutex> lock(filtersMutex_);   // :132-143
+    std::shared_lock<std::shared_mutex> lock(filtersMutex_);   // :132-143
     std::vector<std::string> active;
     for (const auto& [name, entry] : filters_)
         if (entry.config.enabled) active.push_back(name);
@@ -183,9 +183,19 @@ void GpuPacketFilter::compileLocked() {
     dirty_ = false;
 }
 
+std::shared_lock<std::shared_mutex> GpuPacketFilter::lockProgram() {
+    for (;;) {
+        {
+            std::shared_lock<std::shared_mutex> rd(filtersMutex_);
+            if (!dirty_) return rd;
+        }
+        std::unique_lock<std::shared_mutex> wr(filtersMutex_);
+        if (dirty_) compileLocked();
+    }
+}
+
 std::vector<std::string> GpuPacketFilter::evaluationOrder() {
-    std::lock_guard<std::mutex> lock(filtersMutex_);
-    if (dirty_) compileLocked();
+    const auto lock = lockProgram();
     std::vector<std::string> names;
     for (const auto& s : program_) names.push_back(s.name);
     return names;
@@ -261,22 +271,50 @@ void prefault(bt_ctx* ctx, void* p, size_t bytes) {
     });
 }
 
+// Counts a batch call in flight for its duration.
+struct InFlight {
+    std::atomic<int>& n;
+    explicit InFlight(std::atomic<int>& c) : n(c) { n.fetch_add(1, std::memory_order_relaxed); }
+    ~InFlight() { n.fetch_sub(1, std::memory_order_relaxed); }
+};
+
 }  // namespace
+
+template <class Fn>
+void GpuPacketFilter::forRanges(size_t n, Fn&& fn) {
+    if (inFlight_.load(std::memory_order_relaxed) > 1) {
+        if (n) fn(size_t(0), n);
+    } else {
+        parallel_ranges(ctx_, n, [&](size_t lo, size_t hi) { fn(lo, hi); });
+    }
+}
+
+void GpuPacketFilter::setTiming(double device_s, double host_s) {
+    std::lock_guard<std::mutex> lock(statsMutex_);
+    timing_.device_s = device_s;
+    timing_.host_s = host_s;
+}
 
 void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
                                std::vector<bt_rec>* records) {
     const uint32_t n = (uint32_t)packets.size();
-    ptrs_.resize(n);
-    lens_.resize(n);
-    parallel_ranges(ctx_, n, [&](size_t lo, size_t hi) {
+    // the gather list, per calling thread and reused across its batches (written through
+    // plain pointers: a thread_local named inside the lambda would be the pool thread's own)
+    thread_local std::vector<const uint8_t*> ptrs;
+    thread_local std::vector<uint32_t> lens;
+    ptrs.resize(n);
+    lens.resize(n);
+    const uint8_t** P = ptrs.data();
+    uint32_t* L = lens.data();
+    forRanges(n, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
-            ptrs_[i] = packets[i].data();
-            lens_[i] = (uint32_t)packets[i].length();
+            P[i] = packets[i].data();
+            L[i] = (uint32_t)packets[i].length();
         }
     });
     decide.resize(n);
     if (records) records->resize(n);
-    if (bt_group_parse_filter_ptrs(group_, ptrs_.data(), lens_.data(), n, records ? records->data() : nullptr, nullptr,
+    if (bt_group_parse_filter_ptrs(group_, P, L, n, records ? records->data() : nullptr, nullptr,
                                    decide.data(), nullptr, nullptr) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
 }
@@ -306,9 +344,11 @@ GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets,
     Tally t;
     t.rejected.assign(program_.size() + 1, 0);
     const size_t n = packets.size();
+    std::unique_lock<std::mutex> host(hostMutex_, std::defer_lock);   // taken at the first host slot
     for (size_t i = 0; i < n; ++i) {
         uint32_t d = decide[i];
         if ((d >> 6) == BT_DECIDE_HOST) {
+            if (!host.owns_lock()) host.lock();
             if (error_idx) {
                 try {
                     d = resolveHost(packets[i], d & 63u);
@@ -366,8 +406,8 @@ void GpuPacketFilter::flushTally(const Tally& t, std::chrono::microseconds per) 
 
 std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const std::vector<Packet>& packets) {
     std::vector<FilterResult> results;
-    std::lock_guard<std::mutex> lock(filtersMutex_);
-    if (dirty_) compileLocked();
+    const auto lock = lockProgram();
+    const InFlight busy(inFlight_);
     if (packets.empty()) return results;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint8_t> decide;
@@ -375,16 +415,16 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
-    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
+    const double device_s = std::chrono::duration<double>(t1 - t0).count();
     const Tally t = scan(packets, decide, nullptr, nullptr);
     // The FilterResults of the packets before any throw (:102-111), built on the host
     // threads from per-slot strings made once per program: the reference's vector is the
     // result either way, its strings are copied rather than concatenated per packet.
     results.reserve(t.stop);
     advise_huge(results.data(), t.stop * sizeof(FilterResult));
-    prefault(ctx_, results.data(), t.stop * sizeof(FilterResult));
+    if (inFlight_.load(std::memory_order_relaxed) == 1) prefault(ctx_, results.data(), t.stop * sizeof(FilterResult));
     results.resize(t.stop);
-    parallel_ranges(ctx_, t.stop, [&](size_t lo, size_t hi) {
+    forRanges(t.stop, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
             FilterResult& r = results[i];
             const uint32_t code = decide[i] >> 6, slot = decide[i] & 63u;
@@ -403,7 +443,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
     });
     flushTally(t, per);
     t.rethrowIfAny(*this, decide);   // earlier packets are counted
-    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return results;
 }
 
@@ -413,36 +453,36 @@ GpuPacketFilter::FilterResult GpuPacketFilter::applyFilters(const Packet& packet
 
 GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& packets) {
     Verdicts v;
-    std::lock_guard<std::mutex> lock(filtersMutex_);
-    if (dirty_) compileLocked();
+    const auto lock = lockProgram();
+    const InFlight busy(inFlight_);
     if (packets.empty()) return v;
     const auto t0 = std::chrono::steady_clock::now();
     runBatch(packets, v.decide);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
-    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
+    const double device_s = std::chrono::duration<double>(t1 - t0).count();
     const Tally t = scan(packets, v.decide, &v.pass_idx, nullptr);
     flushTally(t, per);
     t.rethrowIfAny(*this, v.decide);
-    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;
 }
 
 GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<Packet>& packets, bool withRecords) {
     Verdicts v;
-    std::lock_guard<std::mutex> lock(filtersMutex_);
-    if (dirty_) compileLocked();
+    const auto lock = lockProgram();
+    const InFlight busy(inFlight_);
     if (packets.empty()) return v;
     const auto t0 = std::chrono::steady_clock::now();
     runBatch(packets, v.decide, withRecords ? &v.records : nullptr);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
-    timing_.device_s = std::chrono::duration<double>(t1 - t0).count();
+    const double device_s = std::chrono::duration<double>(t1 - t0).count();
     const Tally t = scan(packets, v.decide, &v.pass_idx, &v.error_idx);
     flushTally(t, per);
-    timing_.host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;
 }
 
@@ -450,8 +490,7 @@ std::vector<uint32_t> GpuPacketFilter::classifyMapped(const bt_batch& batch, con
                                                      uint8_t* decideHost, uint64_t* verdictHost,
                                                      const std::function<Packet(uint32_t)>& packetOf) {
     std::vector<uint32_t> pass;
-    std::lock_guard<std::mutex> lock(filtersMutex_);
-    if (dirty_) compileLocked();
+    const auto lock = lockProgram();
     if (!batch.n) return pass;
     if (!out.decide || !decideHost) throw std::invalid_argument("GpuPacketFilter::classifyMapped: decide required");
     const auto t0 = std::chrono::steady_clock::now();
@@ -476,9 +515,11 @@ std::vector<uint32_t> GpuPacketFilter::classifyMapped(const bt_batch& batch, con
         for (size_t s = 0; s < program_.size(); ++s)
             if (rejected[s]) stats_.filterCounts[program_[s].name] += rejected[s];
     };
+    std::unique_lock<std::mutex> host(hostMutex_, std::defer_lock);   // taken at the first host slot
     for (uint32_t i = 0; i < batch.n; ++i) {
         uint32_t d = decideHost[i];
         if ((d >> 6) == BT_DECIDE_HOST) {
+            if (!host.owns_lock()) host.lock();
             decideHost[i] = (uint8_t)(d = resolveHost(packetOf(i), d & 63u));
             if (verdictHost && (d >> 6) == BT_DECIDE_PASS) verdictHost[i / 64] |= 1ull << (i % 64);
         }

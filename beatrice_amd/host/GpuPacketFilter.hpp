@@ -14,6 +14,12 @@
 //   * PAYLOAD (std::regex) and CUSTOM (std::function) filters are evaluated here on
 //     the host, with the reference's semantics, for the packets that reach them.
 // processingTime is the amortised batch time (the reference's value is a wall clock).
+// Threads: batch calls from several threads run concurrently on one filter (the compiled
+// program is shared and immutable while they run; the device pass is serialised per
+// device, each caller builds its own results); addFilter / removeFilter / setFilterEnabled
+// / setCustomFilter wait for the calls in flight, as the reference's filtersMutex_ makes
+// them (src/PacketFilter.cpp:19-61), and CUSTOM / PAYLOAD host resumption stays serial,
+// as in the reference, which holds that mutex around every callback.
 // Several devices: a device list (or BEATRICE_GPU_DEVICES=0,1,... for the default
 // constructor) makes the filter drive a bt_group — the program compiled once, every batch
 // split across the devices (include/beatrice_gpu.h, "several devices in one process").
@@ -21,7 +27,9 @@
 
 #include <cstdint>
 #include <functional>
+#include <atomic>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -87,13 +95,16 @@ public:
     std::vector<uint32_t> classifyMapped(const bt_batch& batch, const bt_outputs& out, uint8_t* decideHost,
                                          uint64_t* verdictHost, const std::function<Packet(uint32_t)>& packetOf);
 
-    // Where the last batch call's time went: the device pass (host gather, H2D, kernels,
+    // Where the last batch call's time went (the latest to finish, when several threads call): the device pass (host gather, H2D, kernels,
     // D2H over every device of the group) and the host's work after it (PAYLOAD / CUSTOM
     // resumption, FilterResults, stats).
     struct BatchTiming {
         double device_s = 0, host_s = 0;
     };
-    BatchTiming lastBatchTiming() const { return timing_; }
+    BatchTiming lastBatchTiming() const {
+        std::lock_guard<std::mutex> lock(statsMutex_);
+        return timing_;
+    }
 
     // Evaluation order of the enabled filters (names), as applyFilters uses it.
     std::vector<std::string> evaluationOrder();
@@ -115,6 +126,14 @@ private:
     };
 
     void compileLocked();
+    // A shared hold on the compiled program (compiling it first if a mutator changed it).
+    std::shared_lock<std::shared_mutex> lockProgram();
+    // fn(lo, hi) over [0, n): on the context's host threads when this is the only batch
+    // call in flight, else on the calling thread (concurrent callers are the parallelism,
+    // and results freed by the caller are then allocated on its own thread)
+    template <class Fn>
+    void forRanges(size_t n, Fn&& fn);
+    void setTiming(double device_s, double host_s);
     // host continuation for packets the device left at a PAYLOAD/CUSTOM slot
     uint32_t resolveHost(const Packet& p, uint32_t first_slot);
     [[noreturn]] void rethrow(const Slot& s) const;
@@ -129,14 +148,14 @@ private:
     bt_group* group_ = nullptr;
     bt_ctx* ctx_ = nullptr;
     std::unordered_map<std::string, FilterEntry> filters_;
-    mutable std::mutex filtersMutex_;
+    mutable std::shared_mutex filtersMutex_;   // unique: mutators and compile; shared: batch calls
+    std::mutex hostMutex_;                      // CUSTOM / PAYLOAD host resumption, one caller at a time
+    std::atomic<int> inFlight_{0};              // batch calls running
     FilterStats stats_;
     mutable std::mutex statsMutex_;
     bool dirty_ = true;
     std::vector<Slot> program_;
     std::vector<std::string> rejectReason_;   // per slot: "Filter <name> rejected packet"
-    std::vector<const uint8_t*> ptrs_;        // runBatch's gather list, reused across batches
-    std::vector<uint32_t> lens_;
     BatchTiming timing_;
 };
 

@@ -58,7 +58,7 @@ public:
             batch_ = (size_t)std::max(1, env_int("BEATRICE_GPU_BATCH", 65536));
             records_ = env_int("BEATRICE_GPU_RECORDS", 0) != 0;
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
-            filter_ = std::make_unique<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
+            filter_ = std::make_shared<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
         }
         {
@@ -243,22 +243,37 @@ private:
         }
     }
 
-    // Batches reach the device and the sink in sequence order, whichever thread took them.
+    // Batches are classified concurrently by the threads that took them (GpuPacketFilter
+    // serialises only the device pass; each caller resumes host slots and builds its own
+    // verdicts) and reach the sink in sequence order. With the whole call under one lock,
+    // the onPacket threads whose shards filled queued behind each other's host work.
     void classifyBatch(const std::vector<Packet>& batch, uint64_t seq) {
-        std::unique_lock<std::mutex> g(gpu_mu_);
-        order_cv_.wait(g, [&] { return done_seq_ == seq; });
-        struct Advance {   // the next batch may go even if this one throws
+        std::shared_ptr<GpuPacketFilter> f;
+        {
+            std::lock_guard<std::mutex> g(gpu_mu_);
+            f = filter_;
+        }
+        struct Advance {   // waits for this batch's turn, then lets the next one go (also on a throw)
             GpuParseFilterPlugin* p;
+            uint64_t seq;
+            std::unique_lock<std::mutex> g;
+            void turn() {
+                if (g.owns_lock()) return;
+                g = std::unique_lock<std::mutex>(p->gpu_mu_);
+                p->order_cv_.wait(g, [&] { return p->done_seq_ == seq; });
+            }
             ~Advance() {
+                turn();
                 ++p->done_seq_;
                 p->order_cv_.notify_all();
             }
-        } advance{this};
-        if (!filter_) return;
-        const auto v = filter_->classifyPerPacket(batch, records_);
+        } advance{this, seq, {}};
+        if (!f) return;
+        const auto v = f->classifyPerPacket(batch, records_);
         processed_ += batch.size();
         passed_ += v.pass_idx.size();
         errors_ += v.error_idx.size();
+        advance.turn();
         if (sink_) sink_(seq, batch, v);
     }
 
@@ -266,9 +281,9 @@ private:
     std::mutex flush_mu_;              // stop_, armed_ (the flush thread's wake-ups)
     std::condition_variable cv_;
     uint64_t armed_ = 0;               // shards that went from empty to pending
-    std::mutex gpu_mu_;                // filter_, sink_, done_seq_ (one batch on the device at a time)
+    std::mutex gpu_mu_;                // filter_, sink_, done_seq_ (the sink's turn)
     std::condition_variable order_cv_;
-    std::unique_ptr<GpuPacketFilter> filter_;
+    std::shared_ptr<GpuPacketFilter> filter_;   // a batch in flight holds its own reference
     size_t batch_ = 65536;
     int flush_us_ = 2000;
     bool records_ = false;

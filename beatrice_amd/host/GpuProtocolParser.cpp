@@ -281,13 +281,38 @@ void GpuProtocolParser::run(GpuParsedBatch& b) {
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     // updateStats (src/parser/ProtocolParser.cpp:482-506) for every walked layer
     static const char* kName[8] = {"ethernet", "vlan", "vlan", "ipv4", "ipv6", "tcp", "udp", "icmp"};
-    uint64_t ok = 0, bad = 0, per[8] = {};
-    for (const bt_rec& r : b.recs_) {
-        for (int k = 0; k < 8; ++k) {
-            if (!(r.present & (1u << k))) continue;
-            ++per[k];
-            if (r.ok & (1u << k)) ++ok; else ++bad;
+    // per-layer counts of the batch, tallied on the host threads (a 96-B record per packet)
+    struct Tally {
+        uint64_t ok = 0, bad = 0, per[8] = {};
+        char pad[64];   // one cache line apart
+    };
+    std::vector<Tally> parts(n >= 65536 ? 16 : 1);
+    struct U {
+        const bt_rec* recs;
+        size_t n;
+        std::vector<Tally>* parts;
+    } u{b.recs_.data(), n, &parts};
+    auto tally = [](void* x, uint32_t w, uint32_t T) {
+        auto* u = static_cast<U*>(x);
+        const uint32_t P = (uint32_t)u->parts->size();
+        for (uint32_t part = w; part < P; part += T) {
+            Tally& t = (*u->parts)[part];
+            for (size_t i = u->n * part / P; i < u->n * (part + 1) / P; ++i) {
+                const bt_rec& r = u->recs[i];
+                for (int k = 0; k < 8; ++k) {
+                    if (!(r.present & (1u << k))) continue;
+                    ++t.per[k];
+                    if (r.ok & (1u << k)) ++t.ok; else ++t.bad;
+                }
+            }
         }
+    };
+    if (parts.size() == 1 || bt_host_parallel(ctx_, tally, &u) != BT_OK) tally(&u, 0, 1);
+    uint64_t ok = 0, bad = 0, per[8] = {};
+    for (const Tally& t : parts) {
+        ok += t.ok;
+        bad += t.bad;
+        for (int k = 0; k < 8; ++k) per[k] += t.per[k];
     }
     std::lock_guard<std::mutex> lk(stats_mu_);
     const uint64_t layers = ok + bad;
@@ -320,13 +345,36 @@ void GpuProtocolParser::resetStats() {
     time_carry_us_ = 0.0;
 }
 
+// A batch keeps each packet's bytes alive through a reference to them (Packet::getData, 16 B)
+// rather than a copy of the Packet (216 B, its Metadata strings included, which cost more to
+// copy and destroy than the GPU pass took), and lists frames and lengths; large batches are
+// filled on the context's host threads.
+template <class Batch>
+void GpuProtocolParser::adopt(bt_ctx* ctx, const std::vector<Packet>& packets, Batch& b) {
+    const size_t n = packets.size();
+    b.keep_.resize(n);
+    b.frames_.resize(n);
+    b.lens_.resize(n);
+    struct U {
+        const std::vector<Packet>* packets;
+        Batch* b;
+        size_t n;
+    } u{&packets, &b, n};
+    auto fill = [](void* x, uint32_t w, uint32_t T) {
+        auto* u = static_cast<U*>(x);
+        for (size_t i = u->n * w / T; i < u->n * (w + 1) / T; ++i) {
+            const Packet& p = (*u->packets)[i];
+            u->b->keep_[i] = p.getData();
+            u->b->frames_[i] = p.data();
+            u->b->lens_[i] = (uint32_t)p.length();
+        }
+    };
+    if (n < 8192 || bt_host_parallel(ctx, fill, &u) != BT_OK) fill(&u, 0, 1);
+}
+
 GpuParsedBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets) {
     GpuParsedBatch b;
-    b.keep_ = packets;
-    for (const auto& p : b.keep_) {
-        b.frames_.push_back(p.data());
-        b.lens_.push_back((uint32_t)p.length());
-    }
+    adopt(ctx_, packets, b);
     run(b);
     return b;
 }
@@ -738,11 +786,7 @@ GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets,
                                            const parser::ProtocolDefinition& protocol) {
     GpuFieldBatch b;
     b.def_ = protocol;
-    b.keep_ = packets;
-    for (const auto& p : b.keep_) {
-        b.frames_.push_back(p.data());
-        b.lens_.push_back((uint32_t)p.length());
-    }
+    adopt(ctx_, packets, b);
     extract(b);
     return b;
 }

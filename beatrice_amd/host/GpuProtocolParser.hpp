@@ -37,6 +37,8 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <type_traits>
+#include <utility>
 #include <shared_mutex>
 #include <string>
 #include <unordered_map>
@@ -50,6 +52,28 @@
 
 namespace beatrice {
 namespace gpu {
+
+// std::allocator that leaves trivially constructible elements uninitialised on resize():
+// the records are written by the device pass right after, so zeroing them first only
+// doubled the host's memory traffic.
+template <class T>
+struct UninitAllocator : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = UninitAllocator<U>;
+    };
+    UninitAllocator() = default;
+    template <class U>
+    UninitAllocator(const UninitAllocator<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible_v<U>) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... Args>
+    void construct(U* p, Args&&... args) {
+        ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+    }
+};
 
 struct WalkedLayer {
     std::string name;   // "ethernet", "vlan", "ipv4", "ipv6", "tcp", "udp", "icmp"
@@ -82,10 +106,10 @@ public:
 
 private:
     friend class GpuProtocolParser;
-    std::vector<bt_rec> recs_;
+    std::vector<bt_rec, UninitAllocator<bt_rec>> recs_;
     std::vector<const uint8_t*> frames_;
     std::vector<uint32_t> lens_;
-    std::vector<Packet> keep_;   // owns the frames of a vector<Packet> batch
+    std::vector<std::shared_ptr<const uint8_t[]>> keep_;   // the frames of a vector<Packet> batch
     bt_ctx* ctx_ = nullptr;      // host pool for format(); owned by the GpuProtocolParser
 };
 
@@ -121,7 +145,7 @@ private:
     std::vector<uint8_t> image_;       // size() x span_
     std::vector<const uint8_t*> frames_;
     std::vector<uint32_t> lens_;
-    std::vector<Packet> keep_;
+    std::vector<std::shared_ptr<const uint8_t[]>> keep_;
 };
 
 class GpuProtocolParser {
@@ -210,6 +234,8 @@ public:
     void resetStats();
 
 private:
+    template <class Batch>
+    static void adopt(bt_ctx* ctx, const std::vector<Packet>& packets, Batch& b);
     void run(GpuParsedBatch& b);
     void extract(GpuFieldBatch& b);
     void countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us);

@@ -17,7 +17,12 @@
 //            IPacketPlugin lifecycle, pass count vs the reference.
 // Prints one line per check; exit status 0 = all passed.
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -152,6 +157,74 @@ static bool filter_case(const char* label, const Capture& cap, const std::vector
           (unsigned long)sb.packetsProcessed, (unsigned long)sa.packetsPassed, (unsigned long)sb.packetsPassed);
     std::printf("ok   filters %-22s %zu packets, %lu passed%s\n", label, cap.packets.size(),
                 (unsigned long)sa.packetsPassed, ea ? (" (threw " + what_kind(ea) + ")").c_str() : "");
+    return true;
+}
+
+// Several threads calling one GpuPacketFilter at once (each on its own shard, in chunks),
+// while another thread keeps re-enabling a filter (a recompile between their calls): every
+// result and the summed stats equal the reference's over the whole capture.
+static bool concurrent_case(const char* label, const Capture& cap, const std::vector<Spec>& specs, int threads) {
+    PacketFilter ref;
+    GpuPacketFilter gpu(0);
+    install(ref, specs);
+    install(gpu, specs);
+    const std::vector<PacketFilter::FilterResult> want = ref.applyFilters(cap.packets);
+    std::vector<PacketFilter::FilterResult> got(cap.packets.size());
+    std::vector<uint8_t> classified(cap.packets.size(), 2);
+    std::atomic<bool> done{false};
+    std::atomic<int> errors{0};
+    std::thread mutator([&] {
+        while (!done.load()) {
+            gpu.setFilterEnabled(specs.front().name, true);
+            std::this_thread::sleep_for(std::chrono::microseconds(300));
+        }
+    });
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            const size_t lo = cap.packets.size() * t / threads, hi = cap.packets.size() * (t + 1) / threads;
+            size_t chunk = 700 + 311 * (size_t)t;
+            for (size_t at = lo; at < hi; at += chunk) {
+                const std::vector<Packet> part(cap.packets.begin() + at, cap.packets.begin() + std::min(hi, at + chunk));
+                try {
+                    if ((at / chunk) % 2) {   // half the chunks through classify
+                        const auto v = gpu.classify(part);
+                        for (size_t i = 0; i < part.size(); ++i) classified[at + i] = (v.decide[i] >> 6) == BT_DECIDE_PASS;
+                        std::vector<PacketFilter::FilterResult> r = gpu.applyFilters(part);
+                        for (size_t i = 0; i < r.size(); ++i) got[at + i] = std::move(r[i]);
+                    } else {
+                        std::vector<PacketFilter::FilterResult> r = gpu.applyFilters(part);
+                        for (size_t i = 0; i < r.size(); ++i) got[at + i] = std::move(r[i]);
+                    }
+                } catch (...) {
+                    ++errors;
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    done = true;
+    mutator.join();
+    CHECK(errors == 0, "%s: %d calls threw", label, errors.load());
+    for (size_t i = 0; i < want.size(); ++i) {
+        CHECK(want[i].passed == got[i].passed && want[i].filterName == got[i].filterName && want[i].reason == got[i].reason,
+              "%s: packet %zu ref=(%d,%s) gpu=(%d,%s)", label, i, want[i].passed, want[i].filterName.c_str(), got[i].passed,
+              got[i].filterName.c_str());
+        CHECK(classified[i] == 2 || classified[i] == (uint8_t)want[i].passed, "%s: classify packet %zu", label, i);
+    }
+    // classified chunks were counted twice (classify + applyFilters)
+    uint64_t twice = 0, twice_passed = 0;
+    for (size_t i = 0; i < want.size(); ++i)
+        if (classified[i] != 2) {
+            ++twice;
+            twice_passed += want[i].passed;
+        }
+    const auto sa = ref.getStats(), sb = gpu.getStats();
+    CHECK(sb.packetsProcessed == sa.packetsProcessed + twice && sb.packetsPassed == sa.packetsPassed + twice_passed,
+          "%s: stats processed %lu (want %lu) passed %lu (want %lu)", label, (unsigned long)sb.packetsProcessed,
+          (unsigned long)(sa.packetsProcessed + twice), (unsigned long)sb.packetsPassed,
+          (unsigned long)(sa.packetsPassed + twice_passed));
+    std::printf("ok   concurrent %-19s %zu packets on %d threads + a recompiling thread, %lu passed\n", label,
+                cap.packets.size(), threads, (unsigned long)sa.packetsPassed);
     return true;
 }
 
@@ -602,7 +675,19 @@ static bool plugin_case(const Capture& cap, const char* so) {
     return true;
 }
 
+// A crash names where it happened (the test's stdout is a pipe, so its buffered lines are lost).
+static void on_fatal(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    dprintf(2, "test_adapter: signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    _exit(128 + sig);
+}
+
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);
+    signal(SIGSEGV, on_fatal);
+    signal(SIGABRT, on_fatal);
     const char* plugin_so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
     using T = PacketFilter::FilterType;
     Capture c3 = capture(3, 20000, 0x5EED0003), c4 = capture(4, 12000, 0x5EED0004), fz = capture(9, 30000, 0x5EED0009);
@@ -640,6 +725,8 @@ int main(int argc, char** argv) {
     ok &= filter_case("c3/throw-late", c3, throws_late);
     ok &= filter_case("c4/custom-throw", c4, custom_throw);
     ok &= filter_case("c3/no-filters", c3, {});
+    ok &= concurrent_case("c3/headline", c3, headline, 8);
+    ok &= concurrent_case("fuzz/payload+custom", fz, host_side, 6);
     ok &= parser_case("c3", c3);
     ok &= parser_case("c4", c4);
     ok &= parser_case("fuzz", fz);

@@ -15,6 +15,7 @@
 #   sq      SQ counters of the main kernels (tools/gpu_sq.sh)        -> $OUT/sq.txt
 #   e2e     end-to-end (PCIe) table (tools/e2e.py)                   -> $OUT/e2e.jsonl
 #   surfaces  the drop-in C++ surfaces timed next to the reference  -> $OUT/surfaces.json
+#             (SURF_ARGS: surface_bench arguments, default "all")
 # CFGS (default "c2f c2 c3 c4 c1") selects the configs of prof / sq.
 set -o pipefail
 OUT=${OUT:-gpurun_out/round}
@@ -65,7 +66,7 @@ for step in $STEPS; do
       done
       cat "$OUT/e2e.jsonl" ;;
     surfaces)
-      timeout -k 10 900 tools/surfaces/surface_bench all > "$OUT/surfaces.json" 2> "$OUT/surfaces.err" || fail surfaces $? "$OUT/surfaces.err"
+      timeout -k 10 900 tools/surfaces/surface_bench ${SURF_ARGS:-all} > "$OUT/surfaces.json" 2> "$OUT/surfaces.err" || fail surfaces $? "$OUT/surfaces.err"
       cat "$OUT/surfaces.json" ;;
     *) echo "unknown step $step"; exit 8 ;;
   esac

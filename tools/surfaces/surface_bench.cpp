@@ -2,7 +2,8 @@
 // to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
 // integrator calls").
 //
-//   surface_bench [all|filter|ref|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
+//   surface_bench [all|filter|ref|mt|parser|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
+//                 [--chunks 16384,65536]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
 // (the reference's batch type, include/beatrice/Packet.hpp) and C3's 5-tuple filter set:
@@ -14,6 +15,10 @@
 //             whole capture per call, with the split of the call into the device pass
 //             (host gather -> H2D -> kernels -> D2H) and the host's FilterResult / stats work;
 //   classify  GpuPacketFilter::classify(const std::vector<Packet>&) (decisions + pass list);
+//   mt        the same two from T threads at once on ONE shared GpuPacketFilter, each thread
+//             on its own shard in chunks (the reference's pattern above, one instance);
+//   parser    ProtocolParser::parsePacket per walked layer against GpuProtocolParser::parseBatch
+//             (records, ParseResults on demand, JSON text): bench_parser below;
 //   plugin    libgpu_parse_filter_plugin.so through createPlugin(): onPacket from 1 and from
 //             T threads (PluginManager::processPacket's per-packet call), until the verdict
 //             sink has seen every packet.
@@ -34,6 +39,9 @@
 #include <vector>
 
 #include "../../beatrice_amd/host/GpuPacketFilter.hpp"
+#include "../../beatrice_amd/host/GpuProtocolParser.hpp"
+#include "parser/ProtocolParser.hpp"
+#include "parser/ProtocolRegistry.hpp"
 #include "beatrice/IPacketPlugin.hpp"
 #include "beatrice/PacketFilter.hpp"
 #include "beatrice_gpu_plugin.h"
@@ -166,6 +174,42 @@ void bench_gpu_filter(const Capture& c, double seconds, const char* which) {
     (void)passed;
 }
 
+// One GpuPacketFilter called from T threads at once, each on its own shard in chunks of
+// `chunk` packets: the reference's multi-threaded pattern (bench_ref) against one shared
+// filter instead of T private ones. Results are consumed and destroyed on the calling
+// thread, as a caller's would be.
+void bench_gpu_filter_mt(const Capture& c, int threads, size_t chunk, double seconds, const char* which) {
+    GpuPacketFilter f;
+    add_set(f);
+    const bool apply = std::strcmp(which, "apply") == 0;
+    (void)f.classify(std::vector<Packet>(c.packets.begin(), c.packets.begin() + std::min(c.packets.size(), chunk)));
+    std::atomic<uint64_t> done{0};
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    const auto t0 = Clock::now();
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            const size_t lo = c.packets.size() * t / threads, hi = c.packets.size() * (t + 1) / threads;
+            const std::vector<Packet> shard(c.packets.begin() + lo, c.packets.begin() + hi);
+            std::vector<Packet> part;
+            uint64_t mine = 0;
+            for (size_t at = 0; !stop.load(std::memory_order_relaxed); at = (at + chunk) % shard.size()) {
+                part.assign(shard.begin() + at, shard.begin() + std::min(shard.size(), at + chunk));
+                if (apply) mine += f.applyFilters(part).size();
+                else mine += f.classify(part).decide.size();
+                if (t == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+            }
+            done += mine;
+        });
+    for (auto& x : th) x.join();
+    const double el = secs(t0, Clock::now());
+    char extra[160];
+    std::snprintf(extra, sizeof(extra), "\"chunk\": %zu, \"shared_instance\": true, \"seconds\": %.3f", chunk, el);
+    line(apply ? "GpuPacketFilter::applyFilters(vector<Packet>) -> vector<FilterResult>, T callers"
+               : "GpuPacketFilter::classify(vector<Packet>), T callers",
+         c, threads, done / el, extra);
+}
+
 // The floor of any applyFilters(vector) -> vector<FilterResult>: constructing n results,
 // filling them from per-slot strings (on T threads) and destroying them, with no filtering.
 void bench_result_floor(const Capture& c, int threads, double seconds) {
@@ -200,6 +244,117 @@ void bench_result_floor(const Capture& c, int threads, double seconds) {
     std::snprintf(extra, sizeof(extra), "\"construct_s\": %.4f, \"fill_s\": %.4f, \"destroy_s\": %.4f, \"seconds\": %.3f",
                   build_s, fill_s, free_s, el);
     line("floor: vector<FilterResult>(n) + fill + destroy (no filtering)", c, threads, done / el, extra);
+}
+
+// The parser side. The reference's parse of a batch is ProtocolParser::parsePacket(slice,
+// name) per walked layer (the bench's cpu_baseline, oracle/ref_harness.cpp), on T threads
+// with a parser each; against it:
+//   parseBatch         GpuProtocolParser::parseBatch(vector<Packet>): every packet's layer
+//                      walk on the GPU, its bt_rec back on the host (records are the product)
+//   parseBatch+layer   the same, then layer(i, k) -> the reference's ParseResult for every
+//                      walked layer of every packet, on T threads (what a caller that wants
+//                      ParseResult objects pays)
+//   parseBatch+json    the same, then format(BT_FMT_JSON): the reference's toJsonString text
+//                      of every walked layer of the batch
+// The walk (layer names and offsets) the reference threads follow is taken from one GPU pass
+// before their timing starts: their time is the parsePacket calls alone.
+void bench_parser(const Capture& c, int threads, double seconds) {
+    using namespace beatrice::parser;
+    beatrice::gpu::GpuProtocolParser gp;
+    const size_t n = std::min<size_t>(c.packets.size(), 1u << 20);
+    const std::vector<Packet> pk(c.packets.begin(), c.packets.begin() + n);
+    (void)gp.parseBatch(pk);   // warm-up: device init, staging
+    struct Walk {
+        uint32_t off;
+        const char* name;
+    };
+    std::vector<std::vector<Walk>> walks(n);
+    {
+        const auto b = gp.parseBatch(pk);
+        static const char* names[] = {"ethernet", "vlan", "ipv4", "ipv6", "tcp", "udp", "icmp"};
+        for (size_t i = 0; i < n; ++i)
+            for (const auto& l : b.layers(i))
+                for (const char* nm : names)
+                    if (l.name == nm) walks[i].push_back({(uint32_t)l.offset, nm});
+    }
+    size_t n_layers = 0;
+    for (const auto& w : walks) n_layers += w.size();
+    {   // the reference, T threads, one ProtocolParser each (metrics off, as the harness)
+        std::atomic<uint64_t> done{0};
+        std::atomic<bool> stop{false};
+        std::vector<std::thread> th;
+        const auto t0 = Clock::now();
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                ProtocolParser::ParserConfig cfg;
+                cfg.enablePerformanceMetrics = false;
+                ProtocolParser rp(cfg);
+                rp.registerProtocol(BuiltinProtocols::createEthernetProtocol());
+                rp.registerProtocol(BuiltinProtocols::createVLANProtocol());
+                rp.registerProtocol(BuiltinProtocols::createIPv4Protocol());
+                rp.registerProtocol(BuiltinProtocols::createIPv6Protocol());
+                rp.registerProtocol(BuiltinProtocols::createTCPProtocol());
+                rp.registerProtocol(BuiltinProtocols::createUDPProtocol());
+                rp.registerProtocol(BuiltinProtocols::createICMPProtocol());
+                const size_t lo = n * t / threads, hi = n * (t + 1) / threads;
+                uint64_t mine = 0;
+                for (size_t i = lo; !stop.load(std::memory_order_relaxed); i = i + 1 < hi ? i + 1 : lo) {
+                    const uint8_t* f = pk[i].data();
+                    const size_t len = pk[i].length();
+                    for (const Walk& w : walks[i]) {
+                        const std::vector<uint8_t> slice(f + w.off, f + len);
+                        const ParseResult r = rp.parsePacket(slice, w.name);
+                        (void)r;
+                    }
+                    ++mine;
+                    if (t == 0 && (mine & 1023) == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+                }
+                done += mine;
+            });
+        for (auto& x : th) x.join();
+        const double el = secs(t0, Clock::now());
+        char extra[128];
+        std::snprintf(extra, sizeof(extra), "\"layers_per_packet\": %.3f, \"seconds\": %.3f", (double)n_layers / n, el);
+        line("ref ProtocolParser::parsePacket per walked layer", c, threads, done / el, extra);
+    }
+    auto timed = [&](const char* what, int mode) {
+        uint64_t done = 0;
+        double dev_s = 0, post_s = 0;
+        const auto t0 = Clock::now();
+        while (secs(t0, Clock::now()) < seconds) {
+            const auto a = Clock::now();
+            const auto b = gp.parseBatch(pk);
+            const auto m = Clock::now();
+            if (mode == 1) {
+                std::vector<std::thread> th;
+                for (int t = 0; t < threads; ++t)
+                    th.emplace_back([&, t] {
+                        for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+                            const size_t k = walks[i].size();
+                            for (size_t j = 0; j < k; ++j) {
+                                const ParseResult r = b.layer(i, j);
+                                (void)r;
+                            }
+                        }
+                    });
+                for (auto& x : th) x.join();
+            } else if (mode == 2) {
+                const std::string text = b.format(BT_FMT_JSON);
+                if (text.empty()) std::abort();
+            }
+            dev_s += secs(a, m);
+            post_s += secs(m, Clock::now());
+            done += n;
+        }
+        const double el = secs(t0, Clock::now());
+        char extra[160];
+        std::snprintf(extra, sizeof(extra), "\"parse_batch_s\": %.4f, \"host_post_s\": %.4f, \"seconds\": %.3f", dev_s,
+                      post_s, el);
+        line(what, c, mode == 1 ? threads : 0, done / el, extra);
+    };
+    timed("GpuProtocolParser::parseBatch(vector<Packet>) -> records", 0);
+    timed("GpuProtocolParser::parseBatch + layer(i,k) ParseResult for every walked layer", 1);
+    timed("GpuProtocolParser::parseBatch + format(BT_FMT_JSON) of the batch", 2);
 }
 
 void bench_plugin(const Capture& c, int threads, const char* so) {
@@ -256,11 +411,20 @@ int main(int argc, char** argv) {
     double seconds = 3.0;
     int threads = usable_cpus();
     const char* so = "beatrice_amd/libgpu_parse_filter_plugin.so";
+    std::vector<size_t> chunks = {16384, 65536};
     for (int i = 2; i + 1 < argc; i += 2) {
         if (!std::strcmp(argv[i], "--packets")) n2 = n3 = (uint32_t)std::atol(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--seconds")) seconds = std::atof(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--threads")) threads = std::atoi(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--plugin")) so = argv[i + 1];
+        else if (!std::strcmp(argv[i], "--chunks")) {   // comma-separated chunk sizes of the T-caller runs
+            chunks.clear();
+            for (const char* q = argv[i + 1]; *q;) {
+                chunks.push_back((size_t)std::atol(q));
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
     }
     std::fprintf(stderr, "surface_bench: %d usable CPUs\n", threads);
     const Capture caps[2] = {capture("c2", 2, n2, 0xC2), capture("c3", 3, n3, 0xC3)};
@@ -274,6 +438,13 @@ int main(int argc, char** argv) {
             bench_gpu_filter(c, seconds, "apply");
             bench_gpu_filter(c, seconds, "classify");
         }
+        if (what == "all" || what == "filter" || what == "mt") {
+            for (size_t ch : chunks) {
+                bench_gpu_filter_mt(c, threads, ch, seconds, "apply");
+                bench_gpu_filter_mt(c, threads, ch, seconds, "classify");
+            }
+        }
+        if (what == "all" || what == "parser") bench_parser(c, threads, seconds);
         if (what == "all" || what == "plugin") {
             bench_plugin(c, 1, so);
             bench_plugin(c, threads, so);
