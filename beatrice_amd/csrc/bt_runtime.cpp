@@ -5,6 +5,7 @@
 // device workspace for the ordered compaction. Nothing here throws across the ABI:
 // failures return a beatrice::ErrorCode value and set a thread-local message.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -227,10 +228,35 @@ int set_error(int code, const char* fmt, ...) {
     return code;
 }
 
+// CPUs this process may run on: the affinity set, bounded by the cgroup v2 CPU quota (a GPU
+// box's job sees every CPU of the machine in its affinity set but may use 16).
+unsigned usable_cpus() {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long period = 0;
+        if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period) {
+            const unsigned long long quota = strtoull(q, nullptr, 10) / period;
+            if (quota >= 1 && quota < n) n = (unsigned)quota;
+        }
+        fclose(f);
+    }
+    return n;
+}
+
 HostPool& pool_of(bt_ctx* c) {
     std::call_once(c->pool_once, [c] {
         unsigned nt = c->opts.host_threads;
-        if (!nt) nt = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (!nt) {   // auto: BT_HOST_THREADS, else 8 (at most the usable CPUs)
+            // 8, not every usable CPU: with callers on all 16 of a GPU box's CPUs (T callers of
+            // one GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool
+            // oversubscribes them: C2 applyFilters 136-142 against 163 Mpps, classify 161-163
+            // against 172-192 (tools/surfaces/ab_pool_threads.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
+            const char* e = getenv("BT_HOST_THREADS");
+            nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(8u, usable_cpus());
+        }
         c->pool = std::make_unique<HostPool>(std::min(nt, 16u));
     });
     return *c->pool;

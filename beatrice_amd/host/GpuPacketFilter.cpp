@@ -103,6 +103,7 @@ Result<void> GpuPacketFilter::addFilter(const std::string& name, const FilterCon
     entry.config = config;
     filters_[name] = entry;
     dirty_ = true;
+    updateNeedsPackets();
     return Result<void>::success();
 }
 
@@ -112,6 +113,7 @@ Result<void> GpuPacketFilter::removeFilter(const std::string& name) {
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     filters_.erase(it);
     dirty_ = true;
+    updateNeedsPackets();
     return Result<void>::success();
 }
 
@@ -121,6 +123,7 @@ Result<void> GpuPacketFilter::setFilterEnabled(const std::string& name, bool ena
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     it->second.config.enabled = enabled;
     dirty_ = true;
+    updateNeedsPackets();
     return Result<void>::success();
 }
 
@@ -130,7 +133,15 @@ Result<void> GpuPacketFilter::setCustomFilter(const std::string& name, std::func
     if (it == filters_.end()) return Result<void>::error(ErrorCode::INVALID_ARGUMENT, "Filter not found: " + name);
     it->second.customFunc = std::move(filterFunc);
     dirty_ = true;
+    updateNeedsPackets();
     return Result<void>::success();
+}
+
+void GpuPacketFilter::updateNeedsPackets() {
+    bool any = false;
+    for (const auto& [name, entry] : filters_)
+        if (entry.config.enabled && entry.config.type == FilterType::CUSTOM) any = true;
+    needsPackets_.store(any, std::memory_order_relaxed);
 }
 
 std::vector<std::string> GpuPacketFilter::getActiveFilters() const {
@@ -295,6 +306,15 @@ void GpuPacketFilter::setTiming(double device_s, double host_s) {
     timing_.host_s = host_s;
 }
 
+void GpuPacketFilter::runFrames(const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                                std::vector<uint8_t>& decide, std::vector<bt_rec>* records) {
+    decide.resize(n);
+    if (records) records->resize(n);
+    if (bt_group_parse_filter_ptrs(group_, frames, lens, n, records ? records->data() : nullptr, nullptr,
+                                   decide.data(), nullptr, nullptr) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+}
+
 void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
                                std::vector<bt_rec>* records) {
     const uint32_t n = (uint32_t)packets.size();
@@ -312,11 +332,7 @@ void GpuPacketFilter::runBatch(const std::vector<Packet>& packets, std::vector<u
             L[i] = (uint32_t)packets[i].length();
         }
     });
-    decide.resize(n);
-    if (records) records->resize(n);
-    if (bt_group_parse_filter_ptrs(group_, P, L, n, records ? records->data() : nullptr, nullptr,
-                                   decide.data(), nullptr, nullptr) != BT_OK)
-        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    runFrames(P, L, n, decide, records);
 }
 
 // The host's pass over a batch's decisions, in packet order: PAYLOAD / CUSTOM slots the
@@ -339,11 +355,11 @@ struct GpuPacketFilter::Tally {
     }
 };
 
-GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets, std::vector<uint8_t>& decide,
+template <class PacketAt>
+GpuPacketFilter::Tally GpuPacketFilter::scan(size_t n, PacketAt packet, std::vector<uint8_t>& decide,
                                             std::vector<uint32_t>* pass_idx, std::vector<uint32_t>* error_idx) {
     Tally t;
     t.rejected.assign(program_.size() + 1, 0);
-    const size_t n = packets.size();
     std::unique_lock<std::mutex> host(hostMutex_, std::defer_lock);   // taken at the first host slot
     for (size_t i = 0; i < n; ++i) {
         uint32_t d = decide[i];
@@ -351,13 +367,13 @@ GpuPacketFilter::Tally GpuPacketFilter::scan(const std::vector<Packet>& packets,
             if (!host.owns_lock()) host.lock();
             if (error_idx) {
                 try {
-                    d = resolveHost(packets[i], d & 63u);
+                    d = resolveHost(packet(i), d & 63u);
                 } catch (...) {   // a CUSTOM callback threw for this packet
                     d = (BT_DECIDE_THROW << 6) | (d & 63u);
                 }
             } else {
                 try {
-                    d = resolveHost(packets[i], d & 63u);
+                    d = resolveHost(packet(i), d & 63u);
                 } catch (...) {
                     t.stop = i;
                     t.ex = std::current_exception();
@@ -416,7 +432,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(packets, decide, nullptr, nullptr);
+    const Tally t = scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, decide, nullptr, nullptr);
     // The FilterResults of the packets before any throw (:102-111), built on the host
     // threads from per-slot strings made once per program: the reference's vector is the
     // result either way, its strings are copied rather than concatenated per packet.
@@ -462,7 +478,8 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(packets, v.decide, &v.pass_idx, nullptr);
+    const Tally t =
+        scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide, &v.pass_idx, nullptr);
     flushTally(t, per);
     t.rethrowIfAny(*this, v.decide);
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
@@ -480,7 +497,28 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<P
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(packets, v.decide, &v.pass_idx, &v.error_idx);
+    const Tally t = scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide, &v.pass_idx,
+                         &v.error_idx);
+    flushTally(t, per);
+    setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
+    return v;
+}
+
+GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const uint8_t* const* frames, const uint32_t* lens,
+                                                             size_t n, bool withRecords,
+                                                             const std::function<Packet(size_t)>& packetOf) {
+    Verdicts v;
+    const auto lock = lockProgram();
+    const InFlight busy(inFlight_);
+    if (!n) return v;
+    if (!frames || !lens || !packetOf) throw std::invalid_argument("GpuPacketFilter::classifyPerPacket: null argument");
+    const auto t0 = std::chrono::steady_clock::now();
+    runFrames(frames, lens, (uint32_t)n, v.decide, withRecords ? &v.records : nullptr);
+    const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
+                     (int64_t)n;
+    const auto t1 = std::chrono::steady_clock::now();
+    const double device_s = std::chrono::duration<double>(t1 - t0).count();
+    const Tally t = scan(n, [&](size_t i) { return packetOf(i); }, v.decide, &v.pass_idx, &v.error_idx);
     flushTally(t, per);
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;

@@ -86,6 +86,11 @@ public:
     // Never throws for a filter; throws std::runtime_error if the device fails.
     // withRecords: the same kernel pass also parses every packet (Verdicts::records).
     Verdicts classifyPerPacket(const std::vector<Packet>& packets, bool withRecords = false);
+    // The same over frames held by the caller (n pointers and lengths, e.g. a batch that keeps
+    // only each Packet's bytes alive); packetOf(i) gives packet i for the host-side filters
+    // (PAYLOAD regexes outside the GPU subset, CUSTOM callbacks), only for packets that reach one.
+    Verdicts classifyPerPacket(const uint8_t* const* frames, const uint32_t* lens, size_t n, bool withRecords,
+                               const std::function<Packet(size_t)>& packetOf);
 
     // Zero-copy form over frames the device already sees (a capture ring registered
     // with bt_host_register): runs parse+filter over `batch` into `out` (device-visible
@@ -105,6 +110,11 @@ public:
         std::lock_guard<std::mutex> lock(statsMutex_);
         return timing_;
     }
+
+    // Whether an enabled CUSTOM filter is installed (its callback gets the whole Packet: a
+    // caller that keeps only packets' bytes for classifyPerPacket(frames, ...) keeps the Packets
+    // too while this holds).
+    bool needsPackets() const { return needsPackets_.load(std::memory_order_relaxed); }
 
     // Evaluation order of the enabled filters (names), as applyFilters uses it.
     std::vector<std::string> evaluationOrder();
@@ -138,8 +148,12 @@ private:
     uint32_t resolveHost(const Packet& p, uint32_t first_slot);
     [[noreturn]] void rethrow(const Slot& s) const;
     void runBatch(const std::vector<Packet>& packets, std::vector<uint8_t>& decide, std::vector<bt_rec>* records = nullptr);
+    void runFrames(const uint8_t* const* frames, const uint32_t* lens, uint32_t n, std::vector<uint8_t>& decide,
+                   std::vector<bt_rec>* records);
     struct Tally;
-    Tally scan(const std::vector<Packet>& packets, std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
+    // packet(i) -> packet i (a reference or a value) for the host-side resumption
+    template <class PacketAt>
+    Tally scan(size_t n, PacketAt packet, std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
                std::vector<uint32_t>* error_idx);
     void flushTally(const Tally& t, std::chrono::microseconds per);
 
@@ -151,6 +165,8 @@ private:
     mutable std::shared_mutex filtersMutex_;   // unique: mutators and compile; shared: batch calls
     std::mutex hostMutex_;                      // CUSTOM / PAYLOAD host resumption, one caller at a time
     std::atomic<int> inFlight_{0};              // batch calls running
+    std::atomic<bool> needsPackets_{false};     // an enabled CUSTOM filter (updated by the mutators)
+    void updateNeedsPackets();                  // filtersMutex_ held
     FilterStats stats_;
     mutable std::mutex statsMutex_;
     bool dirty_ = true;

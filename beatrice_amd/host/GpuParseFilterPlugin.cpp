@@ -13,8 +13,15 @@
 //   BEATRICE_GPU_FLUSH_US  a partial batch is classified at the latest this many
 //                          microseconds after its first packet arrived, by the plugin's
 //                          flush thread when no further packet comes (default 2000)
+//   BEATRICE_GPU_WORKERS   classifier threads (default 2, at most 8)
+//   BEATRICE_GPU_DEBUG     1: onStop prints where the classifier threads' time went
 //   BEATRICE_GPU_FILTERS   ';'-separated  name|TYPE|priority|expression  entries, TYPE one of
 //                          BPF PROTOCOL IP_RANGE PORT_RANGE PAYLOAD CUSTOM
+//
+// Threads. onPacket appends to a per-thread shard of the pending batch; a full shard (or, from
+// the plugin's flush thread, a partial one past its deadline) is queued for the plugin's
+// classifier threads, which take the batches in order, run them through GpuPacketFilter and
+// call the sink in order; at most 4 batches wait in the queue (onPacket blocks beyond that).
 //
 // Results. Each packet is attributed on its own, as PluginManager::processPacket sees a
 // per-packet plugin (src/PluginManager.cpp:158-171: an exception is caught per packet and
@@ -28,7 +35,9 @@
 // (src/PluginManager.cpp:26-34).
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <functional>
 #include <memory>
@@ -45,32 +54,96 @@
 namespace beatrice {
 namespace gpu {
 
+// A batch of packets the plugin holds until it is classified: each packet's bytes kept alive
+// through a reference to them (Packet::getData) with the frame pointers and lengths the device
+// pass reads (28 B per packet instead of a 216-B Packet copy, whose copy and destruction were
+// most of onPacket's time), plus the whole Packets only while a CUSTOM filter (whose callback
+// gets the Packet, metadata included) is installed.
+struct HeldBatch {
+    std::vector<std::shared_ptr<const uint8_t[]>> keep;
+    std::vector<const uint8_t*> frames;
+    std::vector<uint32_t> lens;
+    std::vector<Packet> packets;   // empty unless the batch started with a CUSTOM filter installed
+    bool whole = false;
+
+    size_t size() const { return frames.size(); }
+    bool empty() const { return frames.empty(); }
+    void push(const Packet& p) {
+        keep.push_back(p.getData());
+        frames.push_back(p.data());
+        lens.push_back((uint32_t)p.length());
+        if (whole) packets.push_back(p);
+    }
+    void clear() {
+        keep.clear();
+        frames.clear();
+        lens.clear();
+        packets.clear();
+        whole = false;
+    }
+    void reserve(size_t n) {
+        keep.reserve(n);
+        frames.reserve(n);
+        lens.reserve(n);
+    }
+    size_t capacity() const { return frames.capacity(); }
+    void swap(HeldBatch& o) {
+        keep.swap(o.keep);
+        frames.swap(o.frames);
+        lens.swap(o.lens);
+        packets.swap(o.packets);
+        std::swap(whole, o.whole);
+    }
+    // packet i for the host-side filters: the held Packet, or one made from its bytes
+    Packet packet(size_t i) const { return whole ? packets[i] : Packet(keep[i], lens[i]); }
+};
+
 class GpuParseFilterPlugin : public IPacketPlugin {
 public:
-    using Sink = std::function<void(uint64_t seq, const std::vector<Packet>&, const GpuPacketFilter::Verdicts&)>;
+    using Sink = std::function<void(uint64_t seq, const HeldBatch&, const GpuPacketFilter::Verdicts&)>;
 
-    ~GpuParseFilterPlugin() override { stopFlusher(); }
+    ~GpuParseFilterPlugin() override {
+        stopFlusher();
+        stopWorker();
+    }
 
     void onStart() override {
         stopFlusher();
+        stopWorker();
         {
             std::lock_guard<std::mutex> g(gpu_mu_);
             batch_ = (size_t)std::max(1, env_int("BEATRICE_GPU_BATCH", 65536));
             records_ = env_int("BEATRICE_GPU_RECORDS", 0) != 0;
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
+            workers_ = std::min(8, std::max(1, env_int("BEATRICE_GPU_WORKERS", 2)));
             filter_ = std::make_shared<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
+            whole_ = filter_->needsPackets();
         }
         {
             std::lock_guard<std::mutex> lk(flush_mu_);
             stop_ = false;
         }
+        {
+            std::lock_guard<std::mutex> lk(q_mu_);
+            wstop_ = false;
+        }
+        for (int k = 0; k < workers_; ++k) classifiers_.emplace_back([this] { classifyLoop(); });
         flusher_ = std::thread([this] { flushLoop(); });
     }
 
     void onStop() override {
         stopFlusher();
         flush();
+        stopWorker();
+        if (env_int("BEATRICE_GPU_DEBUG", 0))   // where the classifier threads' time went
+            std::fprintf(stderr,
+                         "[gpu_parse_filter] %llu batches: classify %.1f ms (device pass %.1f), waiting for the "
+                         "sink's turn %.1f ms, "
+                         "sink %.1f ms (summed over %d classifier threads); onPacket blocked on a full queue %.1f ms\n",
+                         (unsigned long long)prof_.batches.load(), prof_.classify_ns / 1e6, prof_.device_ns / 1e6,
+                         prof_.turn_ns / 1e6,
+                         prof_.sink_ns / 1e6, workers_, prof_.blocked_ns / 1e6);
         std::lock_guard<std::mutex> g(gpu_mu_);
         filter_.reset();
     }
@@ -79,29 +152,32 @@ public:
     // Each thread appends to its own shard of the pending batch (its lock is contended only
     // by the flush thread), so the threads do not serialise on one lock per packet: with a
     // single pending vector, 16 threads ran at 1.1 Mpps against 8.6 Mpps for one
-    // (tools/surfaces, round 3). A full shard is classified outside its lock, by the thread
-    // that filled it, while the others keep appending.
+    // (tools/surfaces, round 3). A full shard goes to the classifier thread's queue and the
+    // thread goes on appending; it blocks only while kMaxQueued batches wait (backpressure).
     void onPacket(Packet& packet) override {
         if (!enabled_) return;
         Shard& sh = shards_[shardOfThisThread()];
-        std::vector<Packet> full;
-        uint64_t seq = 0;
+        HeldBatch full;
         bool armed = false;
         {
             std::lock_guard<std::mutex> lk(sh.mu);
             if (sh.pending.empty()) {
                 sh.first.store(Clock::now().time_since_epoch().count(), std::memory_order_relaxed);
+                sh.pending.whole = wholePackets();
                 armed = true;
             }
-            sh.pending.push_back(packet);        // shares the immutable bytes, no copy
-            if (sh.pending.size() >= batch_) seq = takeLocked(sh, full);
+            sh.pending.push(packet);             // shares the immutable bytes, no copy
+            if (sh.pending.size() >= batch_) takeLocked(sh, full);
         }
         if (armed && full.empty()) {             // the flush thread arms this shard's deadline
             std::lock_guard<std::mutex> lk(flush_mu_);
             ++armed_;
             cv_.notify_one();
         }
-        if (!full.empty()) classifyBatch(full, seq);
+        if (!full.empty()) {
+            enqueue(std::move(full));
+            recycleOne();
+        }
     }
 
     std::string getName() const override { return "gpu_parse_filter"; }
@@ -119,18 +195,20 @@ public:
         if (filter_) filter_->resetStats();
     }
 
-    // Classifies every partial shard now (the flush thread does this on its own after
-    // BEATRICE_GPU_FLUSH_US).
+    // Classifies every partial shard now and returns when every batch queued so far has
+    // reached the sink (the flush thread does the same on its own after BEATRICE_GPU_FLUSH_US).
     void flush() {
         for (Shard& sh : shards_) {
-            std::vector<Packet> full;
-            uint64_t seq = 0;
+            HeldBatch full;
             {
                 std::lock_guard<std::mutex> lk(sh.mu);
-                if (!sh.pending.empty()) seq = takeLocked(sh, full);
+                if (!sh.pending.empty()) takeLocked(sh, full);
             }
-            if (!full.empty()) classifyBatch(full, seq);
+            if (!full.empty()) enqueue(std::move(full));
         }
+        std::unique_lock<std::mutex> lk(q_mu_);
+        const uint64_t upto = next_seq_;
+        done_cv_.wait(lk, [&] { return done_seq_ >= upto || wstop_; });
     }
 
     void setVerdictSink(Sink s) {
@@ -145,7 +223,7 @@ private:
     static constexpr size_t kShards = 32;
     struct Shard {
         std::mutex mu;
-        std::vector<Packet> pending;
+        HeldBatch pending;
         std::atomic<int64_t> first{0};   // arrival of the pending batch's first packet (ticks)
     };
 
@@ -154,18 +232,139 @@ private:
         return v ? std::atoi(v) : d;
     }
 
+    // Whether new batches keep whole Packets: an enabled CUSTOM filter is installed. Read from
+    // the filter at onStart and after every classified batch (a CUSTOM filter installed later
+    // through filter() reaches the batches started after the next one; the packets of batches
+    // already pending reach its callback as Packet(bytes, length)).
+    bool wholePackets() const { return whole_.load(std::memory_order_relaxed); }
+
     static size_t shardOfThisThread() {
         static std::atomic<size_t> next{0};
         thread_local const size_t mine = next.fetch_add(1, std::memory_order_relaxed) % kShards;
         return mine;
     }
 
-    // Hands the shard's pending batch out with the next sequence number (sh.mu held).
-    uint64_t takeLocked(Shard& sh, std::vector<Packet>& out) {
+    // Hands the shard's pending batch out (sh.mu held); the shard continues in a cleared
+    // vector from the recycled ones when there is one (its capacity kept).
+    void takeLocked(Shard& sh, HeldBatch& out) {
         out.swap(sh.pending);
-        sh.pending.reserve(std::min<size_t>(batch_, 4096));
+        {
+            std::lock_guard<std::mutex> lk(q_mu_);
+            if (!clean_.empty()) {
+                sh.pending.swap(clean_.back());
+                clean_.pop_back();
+            }
+        }
+        if (sh.pending.capacity() < std::min<size_t>(batch_, 4096)) sh.pending.reserve(std::min<size_t>(batch_, 4096));
         sh.first.store(0, std::memory_order_relaxed);
-        return next_seq_.fetch_add(1);
+    }
+
+    // Queues a batch for the classifier thread under the next sequence number; waits while
+    // kMaxQueued batches are queued.
+    void enqueue(HeldBatch&& batch) {
+        const auto t0 = Clock::now();
+        std::unique_lock<std::mutex> lk(q_mu_);
+        space_cv_.wait(lk, [&] { return queue_.size() < kMaxQueued || wstop_; });
+        prof_.blocked_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+        if (wstop_) {   // stopped (onStop raced with onPacket): nobody will classify it
+            errors_ += batch.size();
+            return;
+        }
+        queue_.push_back({next_seq_++, std::move(batch)});
+        q_cv_.notify_one();
+    }
+
+    // The Packets of a classified batch are released by a producer thread, not by the
+    // classifier (whose time bounds the plugin): one used vector is cleared here and kept,
+    // with its capacity, for the next shard that fills.
+    void recycleOne() {
+        HeldBatch v;
+        {
+            std::lock_guard<std::mutex> lk(q_mu_);
+            if (used_.empty()) return;
+            v.swap(used_.back());
+            used_.pop_back();
+        }
+        v.clear();
+        std::lock_guard<std::mutex> lk(q_mu_);
+        if (clean_.size() < kShards) clean_.push_back(std::move(v));
+    }
+
+    // A classifier thread: takes the queued batches in sequence order and classifies them
+    // (with several classifier threads, one batch's device pass overlaps another's host
+    // work: GpuPacketFilter serialises only the device pass); the sink gets them in order.
+    void classifyLoop() {
+        std::unique_lock<std::mutex> lk(q_mu_);
+        for (;;) {
+            q_cv_.wait(lk, [&] { return wstop_ || !queue_.empty(); });
+            if (queue_.empty()) return;   // stopped and drained
+            Queued q = std::move(queue_.front());
+            queue_.pop_front();
+            space_cv_.notify_one();
+            lk.unlock();
+            std::shared_ptr<GpuPacketFilter> f;
+            {
+                std::lock_guard<std::mutex> g(gpu_mu_);
+                f = filter_;
+            }
+            GpuPacketFilter::Verdicts v;
+            bool ok = false;
+            const auto t0 = Clock::now();
+            if (f) {
+                try {
+                    const HeldBatch& b = q.batch;
+                    v = f->classifyPerPacket(b.frames.data(), b.lens.data(), b.size(), records_,
+                                             [&b](size_t i) { return b.packet(i); });
+                    whole_ = f->needsPackets();
+                    ok = true;
+                    prof_.device_ns += (uint64_t)(f->lastBatchTiming().device_s * 1e9);
+                } catch (const std::exception&) {   // the device failed: nobody to throw to here
+                    errors_ += q.batch.size();
+                }
+            }
+            const auto t1 = Clock::now();
+            lk.lock();
+            done_cv_.wait(lk, [&] { return done_seq_ == q.seq; });   // the sink's turn
+            lk.unlock();
+            const auto t2 = Clock::now();
+            if (ok) {
+                processed_ += q.batch.size();
+                passed_ += v.pass_idx.size();
+                errors_ += v.error_idx.size();
+                std::lock_guard<std::mutex> g(gpu_mu_);
+                if (sink_) sink_(q.seq, q.batch, v);
+            }
+            const auto t3 = Clock::now();
+            auto ns = [](Clock::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
+            prof_.classify_ns += ns(t1 - t0);
+            prof_.turn_ns += ns(t2 - t1);
+            prof_.sink_ns += ns(t3 - t2);
+            ++prof_.batches;
+            lk.lock();
+            done_seq_ = q.seq + 1;
+            if (used_.size() < kShards) used_.push_back(std::move(q.batch));
+            else {   // nobody is recycling (no full shards): release here
+                lk.unlock();
+                q.batch.clear();
+                lk.lock();
+            }
+            done_cv_.notify_all();
+        }
+    }
+
+    void stopWorker() {
+        {
+            std::lock_guard<std::mutex> lk(q_mu_);
+            wstop_ = true;
+        }
+        q_cv_.notify_all();
+        space_cv_.notify_all();
+        for (auto& w : classifiers_) w.join();
+        classifiers_.clear();
+        std::lock_guard<std::mutex> lk(q_mu_);
+        used_.clear();
+        clean_.clear();
+        done_cv_.notify_all();
     }
 
     // The flush thread: sleeps until the earliest deadline (first packet + flush_us) of any
@@ -193,18 +392,12 @@ private:
             for (Shard& sh : shards_) {
                 const int64_t f = sh.first.load(std::memory_order_relaxed);
                 if (!f || f > due) continue;
-                std::vector<Packet> full;
-                uint64_t seq = 0;
+                HeldBatch full;
                 {
                     std::lock_guard<std::mutex> sl(sh.mu);
-                    if (!sh.pending.empty()) seq = takeLocked(sh, full);
+                    if (!sh.pending.empty()) takeLocked(sh, full);
                 }
-                if (full.empty()) continue;
-                try {
-                    classifyBatch(full, seq);
-                } catch (const std::exception&) {   // the device failed: nobody to throw to here
-                    errors_ += full.size();
-                }
+                if (!full.empty()) enqueue(std::move(full));
             }
             lk.lock();
         }
@@ -243,52 +436,33 @@ private:
         }
     }
 
-    // Batches are classified concurrently by the threads that took them (GpuPacketFilter
-    // serialises only the device pass; each caller resumes host slots and builds its own
-    // verdicts) and reach the sink in sequence order. With the whole call under one lock,
-    // the onPacket threads whose shards filled queued behind each other's host work.
-    void classifyBatch(const std::vector<Packet>& batch, uint64_t seq) {
-        std::shared_ptr<GpuPacketFilter> f;
-        {
-            std::lock_guard<std::mutex> g(gpu_mu_);
-            f = filter_;
-        }
-        struct Advance {   // waits for this batch's turn, then lets the next one go (also on a throw)
-            GpuParseFilterPlugin* p;
-            uint64_t seq;
-            std::unique_lock<std::mutex> g;
-            void turn() {
-                if (g.owns_lock()) return;
-                g = std::unique_lock<std::mutex>(p->gpu_mu_);
-                p->order_cv_.wait(g, [&] { return p->done_seq_ == seq; });
-            }
-            ~Advance() {
-                turn();
-                ++p->done_seq_;
-                p->order_cv_.notify_all();
-            }
-        } advance{this, seq, {}};
-        if (!f) return;
-        const auto v = f->classifyPerPacket(batch, records_);
-        processed_ += batch.size();
-        passed_ += v.pass_idx.size();
-        errors_ += v.error_idx.size();
-        advance.turn();
-        if (sink_) sink_(seq, batch, v);
-    }
-
     Shard shards_[kShards];
     std::mutex flush_mu_;              // stop_, armed_ (the flush thread's wake-ups)
     std::condition_variable cv_;
     uint64_t armed_ = 0;               // shards that went from empty to pending
-    std::mutex gpu_mu_;                // filter_, sink_, done_seq_ (the sink's turn)
-    std::condition_variable order_cv_;
+    std::mutex gpu_mu_;                // filter_, sink_
     std::shared_ptr<GpuPacketFilter> filter_;   // a batch in flight holds its own reference
+    std::atomic<bool> whole_{false};            // wholePackets()
     size_t batch_ = 65536;
     int flush_us_ = 2000;
     bool records_ = false;
-    std::atomic<uint64_t> next_seq_{0};
-    uint64_t done_seq_ = 0;
+    // the classifier thread's queue and the vectors recycled through it (q_mu_)
+    static constexpr size_t kMaxQueued = 4;
+    struct Queued {
+        uint64_t seq;
+        HeldBatch batch;
+    };
+    std::mutex q_mu_;
+    std::condition_variable q_cv_, space_cv_, done_cv_;
+    std::deque<Queued> queue_;
+    std::vector<HeldBatch> used_, clean_;   // classified (bytes still held) / cleared
+    uint64_t next_seq_ = 0, done_seq_ = 0;
+    bool wstop_ = true;
+    struct {
+        std::atomic<uint64_t> batches{0}, classify_ns{0}, device_ns{0}, turn_ns{0}, sink_ns{0}, blocked_ns{0};
+    } prof_;
+    std::vector<std::thread> classifiers_;   // the classifier threads (BEATRICE_GPU_WORKERS)
+    int workers_ = 2;
     bool stop_ = true;
     std::thread flusher_;
     Sink sink_;
@@ -315,15 +489,9 @@ extern "C" void gpu_plugin_set_sink(beatrice::IPacketPlugin* p, gpu_verdict_sink
         g->setVerdictSink(nullptr);
         return;
     }
-    g->setVerdictSink([fn, user](uint64_t seq, const std::vector<beatrice::Packet>& b,
+    g->setVerdictSink([fn, user](uint64_t seq, const beatrice::gpu::HeldBatch& b,
                                  const beatrice::gpu::GpuPacketFilter::Verdicts& v) {
-        std::vector<const uint8_t*> frames(b.size());
-        std::vector<uint32_t> lens(b.size());
-        for (size_t i = 0; i < b.size(); ++i) {
-            frames[i] = b[i].data();
-            lens[i] = (uint32_t)b[i].length();
-        }
-        gpu_verdict_batch c{seq, (uint32_t)b.size(), frames.data(), lens.data(), v.decide.data(),
+        gpu_verdict_batch c{seq, (uint32_t)b.size(), b.frames.data(), b.lens.data(), v.decide.data(),
                             v.pass_idx.data(), (uint32_t)v.pass_idx.size(), v.error_idx.data(),
                             (uint32_t)v.error_idx.size(), v.records.empty() ? nullptr : v.records.data()};
         fn(user, &c);

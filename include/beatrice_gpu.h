@@ -275,7 +275,8 @@ typedef struct bt_opts {
     uint32_t host_chunk_bytes;     /* pinned staging bytes per chunk (0 = default 256 MiB) */
     uint32_t grid_waves;           /* 0 = auto (persistent grid sized to the device)    */
     uint32_t flags;                /* BT_OPT_*                                          */
-    uint32_t host_threads;         /* host-path gather/drain threads (0 = auto, <= 16)  */
+    uint32_t host_threads;         /* host-path threads (0 = auto: BT_HOST_THREADS, else 8,
+                                      at most the usable CPUs (affinity, cgroup quota)); <= 16 */
     uint32_t reserved[3];
 } bt_opts;
 

@@ -6,8 +6,8 @@
  * verdict is known only after its batch ran. Code downstream of PluginManager that wants
  * the verdicts (another plugin, the application) installs a verdict sink on the
  * IPacketPlugin* the manager created: it is called once per classified batch, in arrival
- * order, on the thread that classified it (an onPacket caller or the plugin's flush
- * thread). All pointers are valid for the duration of the call only.
+ * order, one batch at a time, on one of the plugin's classifier threads. All pointers are
+ * valid for the duration of the call only.
  *
  * With BEATRICE_GPU_RECORDS=1 the same kernel pass also parses every packet, and the sink
  * sees each packet's bt_rec: the fields of every walked layer as the reference's
@@ -54,7 +54,8 @@ typedef void (*gpu_verdict_sink_fn)(void* user, const gpu_verdict_batch* batch);
 
 /* Installs (fn != NULL) or removes the verdict sink. */
 void gpu_plugin_set_sink(gpu_plugin* plugin, gpu_verdict_sink_fn fn, void* user);
-/* Classifies the partial batch now (the plugin's flush thread does it on its own
+/* Classifies the partial batches now and returns once every batch queued so far has reached
+ * the sink (the plugin's flush thread queues a partial batch on its own
  * BEATRICE_GPU_FLUSH_US after the batch's first packet). */
 void gpu_plugin_flush(gpu_plugin* plugin);
 /* Packets that passed every filter so far. */

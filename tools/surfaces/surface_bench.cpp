@@ -357,7 +357,7 @@ void bench_parser(const Capture& c, int threads, double seconds) {
     timed("GpuProtocolParser::parseBatch + format(BT_FMT_JSON) of the batch", 2);
 }
 
-void bench_plugin(const Capture& c, int threads, const char* so) {
+void bench_plugin(const Capture& c, int threads, double seconds, const char* so) {
     void* h = dlopen(so, RTLD_LAZY);
     if (!h) {
         std::fprintf(stderr, "dlopen %s: %s\n", so, dlerror());
@@ -385,19 +385,34 @@ void bench_plugin(const Capture& c, int threads, const char* so) {
     flush(p);
     while (seen < std::min<size_t>(c.packets.size(), 70000)) std::this_thread::yield();
     seen = 0;
+    // every thread feeds its shard over and over for `seconds` (steady state: the pending
+    // shards have grown, the device pass is warm), then the last partial batches are flushed
+    std::atomic<uint64_t> fed{0};
+    std::atomic<bool> stop{false};
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
-        th.emplace_back([&, t] { feed(c.packets.size() * t / threads, c.packets.size() * (t + 1) / threads); });
+        th.emplace_back([&, t] {
+            const size_t lo = c.packets.size() * t / threads, hi = c.packets.size() * (t + 1) / threads;
+            const size_t step = 16384;
+            uint64_t mine = 0;
+            for (size_t at = lo; !stop.load(std::memory_order_relaxed); at = at + step < hi ? at + step : lo) {
+                const size_t e = std::min(hi, at + step);
+                feed(at, e);
+                mine += e - at;
+                if (t == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+            }
+            fed += mine;
+        });
     for (auto& x : th) x.join();
     const auto t_fed = Clock::now();
     flush(p);
-    while (seen < c.packets.size()) std::this_thread::yield();
+    while (seen < fed) std::this_thread::yield();
     const auto t1 = Clock::now();
-    char extra[160];
-    std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"batch\": %s", secs(t0, t_fed),
-                  secs(t0, t1), getenv("BEATRICE_GPU_BATCH"));
-    line("plugin onPacket -> verdict sink", c, threads, c.packets.size() / secs(t0, t1), extra);
+    char extra[200];
+    std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"fed\": %llu, \"batch\": %s",
+                  secs(t0, t_fed), secs(t0, t1), (unsigned long long)fed.load(), getenv("BEATRICE_GPU_BATCH"));
+    line("plugin onPacket -> verdict sink", c, threads, fed / secs(t0, t1), extra);
     p->onStop();
     set_sink(p, nullptr, nullptr);
     delete p;
@@ -446,8 +461,8 @@ int main(int argc, char** argv) {
         }
         if (what == "all" || what == "parser") bench_parser(c, threads, seconds);
         if (what == "all" || what == "plugin") {
-            bench_plugin(c, 1, so);
-            bench_plugin(c, threads, so);
+            bench_plugin(c, 1, seconds, so);
+            bench_plugin(c, threads, seconds, so);
         }
     }
     return 0;
