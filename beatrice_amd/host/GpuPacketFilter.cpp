@@ -140,7 +140,7 @@ Result<void> GpuPacketFilter::setCustomFilter(const std::string& name, std::func
 void GpuPacketFilter::updateNeedsPackets() {
     bool any = false;
     for (const auto& [name, entry] : filters_)
-        if (entry.config.enabled && entry.config.type == FilterType::CUSTOM) any = true;
+        if (entry.config.enabled && entry.config.type == FilterType::CUSTOM && entry.customFunc) any = true;
     needsPackets_.store(any, std::memory_order_relaxed);
 }
 

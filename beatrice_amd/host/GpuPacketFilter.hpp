@@ -111,7 +111,7 @@ public:
         return timing_;
     }
 
-    // Whether an enabled CUSTOM filter is installed (its callback gets the whole Packet: a
+    // Whether an enabled CUSTOM filter with a callback is installed (the callback gets the whole Packet: a
     // caller that keeps only packets' bytes for classifyPerPacket(frames, ...) keeps the Packets
     // too while this holds).
     bool needsPackets() const { return needsPackets_.load(std::memory_order_relaxed); }

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <ctime>
 #include <iomanip>
@@ -74,7 +75,9 @@ std::string hex(const uint8_t* b, size_t n) {   // ProtocolParser::bytesToHex (:
 }
 
 std::string fmt_ipv4(const uint8_t* b) {        // :610-619
-    return std::to_string(b[0]) + "." + std::to_string(b[1]) + "." + std::to_string(b[2]) + "." + std::to_string(b[3]);
+    char buf[16];
+    const int n = std::snprintf(buf, sizeof(buf), "%u.%u.%u.%u", b[0], b[1], b[2], b[3]);
+    return std::string(buf, (size_t)n);
 }
 
 std::string fmt_ipv6(const uint8_t* b) {        // :621-631
@@ -137,48 +140,51 @@ FieldValue make_field(const bt_rec& r, const Field& f, uint32_t bias) {
     return v;
 }
 
-const Table* table_of(const std::string& name) {
-    if (name == "ethernet") return &kEth;
-    if (name == "vlan") return &kVlan;
-    if (name == "ipv4") return &kIpv4;
-    if (name == "ipv6") return &kIpv6;
-    if (name == "tcp") return &kTcp;
-    if (name == "udp") return &kUdp;
-    if (name == "icmp") return &kIcmp;
-    return nullptr;
-}
 
-uint32_t bit_of(const std::string& name, int tag) {
-    if (name == "ethernet") return BT_L_ETH;
-    if (name == "vlan") return tag == 1 ? BT_L_VLAN1 : BT_L_VLAN0;
-    if (name == "ipv4") return BT_L_IPV4;
-    if (name == "ipv6") return BT_L_IPV6;
-    if (name == "tcp") return BT_L_TCP;
-    if (name == "udp") return BT_L_UDP;
-    return BT_L_ICMP;
+
+}  // namespace
+
+namespace {
+
+// One walked layer as the record states it (the walk, DESIGN.md R-WALK): its table, slice
+// offset, VLAN tag index and `present` / `ok` bit.
+struct Walked {
+    const Table* table;
+    uint32_t offset;
+    int tag;
+    uint32_t bit;
+};
+
+uint32_t walk_of(const bt_rec& r, Walked* out) {
+    uint32_t k = 0;
+    out[k++] = {&kEth, 0, -1, BT_L_ETH};
+    if (r.present & BT_L_VLAN0) out[k++] = {&kVlan, 12, 0, BT_L_VLAN0};
+    if (r.present & BT_L_VLAN1) out[k++] = {&kVlan, 16, 1, BT_L_VLAN1};
+    if (r.present & BT_L_IPV4) out[k++] = {&kIpv4, r.l3_off, -1, BT_L_IPV4};
+    if (r.present & BT_L_IPV6) out[k++] = {&kIpv6, r.l3_off, -1, BT_L_IPV6};
+    if (r.present & BT_L_TCP) out[k++] = {&kTcp, r.l4_off, -1, BT_L_TCP};
+    if (r.present & BT_L_UDP) out[k++] = {&kUdp, r.l4_off, -1, BT_L_UDP};
+    if (r.present & BT_L_ICMP) out[k++] = {&kIcmp, r.l4_off, -1, BT_L_ICMP};
+    return k;
 }
 
 }  // namespace
 
 std::vector<WalkedLayer> GpuParsedBatch::layers(size_t i) const {
-    const bt_rec& r = recs_.at(i);
+    Walked w[8];
+    const uint32_t k = walk_of(recs_.at(i), w);
     std::vector<WalkedLayer> out;
-    out.push_back({"ethernet", 0, -1});
-    if (r.present & BT_L_VLAN0) out.push_back({"vlan", 12, 0});
-    if (r.present & BT_L_VLAN1) out.push_back({"vlan", 16, 1});
-    if (r.present & BT_L_IPV4) out.push_back({"ipv4", r.l3_off, -1});
-    if (r.present & BT_L_IPV6) out.push_back({"ipv6", r.l3_off, -1});
-    if (r.present & BT_L_TCP) out.push_back({"tcp", r.l4_off, -1});
-    if (r.present & BT_L_UDP) out.push_back({"udp", r.l4_off, -1});
-    if (r.present & BT_L_ICMP) out.push_back({"icmp", r.l4_off, -1});
+    out.reserve(k);
+    for (uint32_t j = 0; j < k; ++j) out.push_back({w[j].table->name, w[j].offset, w[j].tag});
     return out;
 }
 
 ParseResult GpuParsedBatch::layer(size_t i, size_t k) const {
-    const auto ls = layers(i);
-    const WalkedLayer& L = ls.at(k);
-    const Table& t = *table_of(L.name);
-    const bt_rec& r = recs_[i];
+    Walked w[8];
+    const bt_rec& r = recs_.at(i);
+    if (k >= walk_of(r, w)) throw std::out_of_range("GpuParsedBatch::layer: no walked layer " + std::to_string(k));
+    const Walked& L = w[k];
+    const Table& t = *L.table;
     const uint8_t* f = frames_[i];
     const size_t len = lens_[i];
     ParseResult res;   // parsePacketInternal (:238-284)
@@ -187,13 +193,15 @@ ParseResult GpuParsedBatch::layer(size_t i, size_t k) const {
     res.rawData.assign(f + L.offset, f + len);
     res.packetLength = len - L.offset;
     res.parsedBytes = 0;
-    if (!(r.ok & bit_of(L.name, L.tag))) {
+    if (!(r.ok & L.bit)) {
         res.status = ParseStatus::PACKET_TOO_SHORT;
         res.errorMessage = "Packet too short for protocol";
         return res;
     }
     const uint32_t bias = L.tag == 1 ? 2u : 0u;
-    for (const Field& fd : t.fields) res.fields[fd.name] = make_field(r, fd, bias);
+    // inserted one by one in table order, as the reference's result.fields[name] = value, so
+    // the map's iteration order (which the formatters print in) is the reference's
+    for (const Field& fd : t.fields) res.fields.emplace(fd.name, make_field(r, fd, bias));
     res.parsedBytes = t.total;
     return res;
 }

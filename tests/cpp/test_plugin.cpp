@@ -18,6 +18,8 @@
 //   sink     the verdict sink sees every batch once, in order, and each packet's verdict
 //            and deciding filter equal the reference's FilterResult;
 //   threads  onPacket from 4 threads at once: every packet is classified exactly once;
+//   hostre / custom  a host-side PAYLOAD regex (resumed from the bytes a pending batch holds)
+//            and a CUSTOM filter (whole Packets held) give the reference's verdicts;
 //   records  (test_plugin records DATA DESC REC, files written by tests/test_cpp_adapter.py
 //            from a reference golden capture) with BEATRICE_GPU_RECORDS=1 the sink's bt_rec
 //            of every packet equals the golden record the compiled reference's parser
@@ -431,6 +433,13 @@ int main(int argc, char** argv) {
     // a stoi-throwing IP_RANGE past the UDP gate: per-packet errors; short flush
     ok &= pipeline_case(so, fuzz, 5000, 1000, "errors", {{"proto", 1, 3, "udp"}, {"bad", 2, 2, "10.x.0.0/8"},
                                                            {"ports", 3, 1, "1-65535"}});
+    // host-side slots: a PAYLOAD regex outside the GPU subset (\b), resumed on the host from the
+    // batch's held bytes; a CUSTOM filter (no callback: true), with which the plugin keeps whole
+    // Packets for the callback
+    ok &= pipeline_case(so, fuzz, 20000, 2048, "hostre", {{"tcp", 1, 3, "tcp"}, {"word", 4, 2, "\\bHTTP"},
+                                                           {"ports", 3, 1, "0-40000"}});
+    ok &= pipeline_case(so, c3, 5000, 4096, "custom", {{"fn", 5, 3, ""}, {"net", 2, 2, "10.0.0.0/8"},
+                                                         {"ports", 3, 1, "1000-2000"}});
     ok &= threads_case(so, c3);
     std::printf(ok && !g_fail ? "ALL OK\n" : "FAILURES\n");
     return ok && !g_fail ? 0 : 1;
