@@ -50,6 +50,10 @@ constexpr uint32_t kHostSlot = 112;   // bytes of each frame staged for the devi
 // ... and with a GPU PAYLOAD slot in the program: applyPayloadFilter's window ends at most
 // at 14 + 60 + 100 = 174 bytes (src/PacketFilter.cpp:293-309), rounded up to 16
 constexpr uint32_t kHostSlotPayload = 176;
+// ... and for calls that return no records and have no GPU PAYLOAD slot: the filters read
+// bytes 12..37 (kNeedFilter) and such calls never take a second round, so 48 B
+constexpr uint32_t kHostSlotFilter = 48;
+static_assert(kHostSlotFilter >= kNeedFilter && kHostSlotFilter % 16 == 0, "filter-only staging");
 
 struct HostSlot {                      // one half of the double-buffered host pipeline
     hipStream_t stream = nullptr;
@@ -64,11 +68,17 @@ struct HostSlot {                      // one half of the double-buffered host p
 };
 
 // Fixed pool of host threads for the host-batch pipeline's gather / drain copies.
+// run(fn) executes fn(0) .. fn(T-1) once each, T = size(): the caller and whichever workers
+// wake claim the indices from one counter, and the caller waits only for the indices already
+// claimed. On a host whose CPUs are all busy (callers on every CPU, the plugin's onPacket
+// threads) a worker may not be scheduled for a whole time slice; waiting for every worker to
+// take its fixed share made each run as slow as the latest one to wake (0.45 ms per device
+// pass of a 12k-packet batch), whereas here the caller does the unclaimed work.
 class HostPool {
 public:
     explicit HostPool(unsigned n) {
-        for (unsigned i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
         nthreads_ = n ? n : 1;
+        for (unsigned i = 1; i < nthreads_; ++i) th_.emplace_back([this] { loop(); });
     }
     ~HostPool() {
         {
@@ -80,47 +90,62 @@ public:
         for (auto& t : th_) t.join();
     }
     unsigned size() const { return nthreads_; }
-    // runs fn(worker) on every worker (the caller is worker 0) and waits
+    // runs fn(k) for every k in [0, size()) and waits
     void run(const std::function<void(unsigned)>& fn) {
         if (nthreads_ == 1) { fn(0); return; }
         std::lock_guard<std::mutex> one_at_a_time(run_mu_);   // callers on several threads
+        uint32_t g;
         {
             std::lock_guard<std::mutex> lk(m_);
             fn_ = &fn;
-            pending_ = nthreads_ - 1;
-            ++gen_;
+            g = (uint32_t)++gen_;
+            finished_ = 0;
+            claim_.store((uint64_t)g << 32, std::memory_order_release);
         }
         cv_.notify_all();
-        fn(0);
+        execute(g, fn);
         std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [this] { return pending_ == 0; });
+        done_.wait(lk, [this] { return finished_ == nthreads_; });
         fn_ = nullptr;
     }
 
 private:
-    void loop(unsigned id) {
+    // claims indices of run g (the generation in the counter's high half keeps a late
+    // worker from claiming in a later run with an earlier run's function) and runs them
+    void execute(uint32_t g, const std::function<void(unsigned)>& fn) {
+        for (;;) {
+            uint64_t c = claim_.load(std::memory_order_acquire);
+            for (;;) {
+                if ((uint32_t)(c >> 32) != g || (uint32_t)c >= nthreads_) return;
+                if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) break;
+            }
+            fn((unsigned)(uint32_t)c);
+            std::lock_guard<std::mutex> lk(m_);
+            if (++finished_ == nthreads_) done_.notify_one();
+        }
+    }
+    void loop() {
         uint64_t seen = 0;
         for (;;) {
             const std::function<void(unsigned)>* f;
+            uint32_t g;
             {
                 std::unique_lock<std::mutex> lk(m_);
                 cv_.wait(lk, [&] { return gen_ != seen; });
                 seen = gen_;
                 if (stop_) return;
-                f = fn_;
+                f = fn_;   // null when that run has already finished
+                g = (uint32_t)gen_;
             }
-            (*f)(id);
-            {
-                std::lock_guard<std::mutex> lk(m_);
-                if (--pending_ == 0) done_.notify_one();
-            }
+            if (f) execute(g, *f);
         }
     }
     std::vector<std::thread> th_;
     std::mutex m_, run_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)>* fn_ = nullptr;
-    unsigned pending_ = 0, nthreads_ = 1;
+    std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
+    unsigned finished_ = 0, nthreads_ = 1;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
@@ -939,7 +964,9 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
     const uint32_t chunk = c->chunk;
     // bytes staged per frame: the header walk's, or with a GPU PAYLOAD slot in the program
     // the payload window's too (bytes past the staged prefix would be the next frame's)
-    const uint32_t slot = c->dfa_pool.empty() ? kHostSlot : kHostSlotPayload;
+    // (filter-only calls: the filters' 38 B; staging the walk's 112 B took 2-3x the gather
+    // and the copy for IMIX frames)
+    const uint32_t slot = !c->dfa_pool.empty() ? kHostSlotPayload : records ? kHostSlot : kHostSlotFilter;
     uint32_t next = 0, k = 0;
     while (next < n || c->hs[0].busy || c->hs[1].busy) {
         HostSlot& s = c->hs[k & 1];

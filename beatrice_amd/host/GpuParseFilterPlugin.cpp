@@ -94,6 +94,18 @@ struct HeldBatch {
         packets.swap(o.packets);
         std::swap(whole, o.whole);
     }
+    // appends o's packets (same `whole` mode; o is left empty)
+    void append(HeldBatch& o) {
+        if (empty()) {
+            swap(o);
+            return;
+        }
+        keep.insert(keep.end(), std::make_move_iterator(o.keep.begin()), std::make_move_iterator(o.keep.end()));
+        frames.insert(frames.end(), o.frames.begin(), o.frames.end());
+        lens.insert(lens.end(), o.lens.begin(), o.lens.end());
+        packets.insert(packets.end(), std::make_move_iterator(o.packets.begin()), std::make_move_iterator(o.packets.end()));
+        o.clear();
+    }
     // packet i for the host-side filters: the held Packet, or one made from its bytes
     Packet packet(size_t i) const { return whole ? packets[i] : Packet(keep[i], lens[i]); }
 };
@@ -198,14 +210,7 @@ public:
     // Classifies every partial shard now and returns when every batch queued so far has
     // reached the sink (the flush thread does the same on its own after BEATRICE_GPU_FLUSH_US).
     void flush() {
-        for (Shard& sh : shards_) {
-            HeldBatch full;
-            {
-                std::lock_guard<std::mutex> lk(sh.mu);
-                if (!sh.pending.empty()) takeLocked(sh, full);
-            }
-            if (!full.empty()) enqueue(std::move(full));
-        }
+        takePartials(0);
         std::unique_lock<std::mutex> lk(q_mu_);
         const uint64_t upto = next_seq_;
         done_cv_.wait(lk, [&] { return done_seq_ >= upto || wstop_; });
@@ -388,19 +393,46 @@ private:
                 continue;
             }
             lk.unlock();
-            const int64_t due = (Clock::now() - std::chrono::microseconds(flush_us_)).time_since_epoch().count();
-            for (Shard& sh : shards_) {
-                const int64_t f = sh.first.load(std::memory_order_relaxed);
-                if (!f || f > due) continue;
-                HeldBatch full;
-                {
-                    std::lock_guard<std::mutex> sl(sh.mu);
-                    if (!sh.pending.empty()) takeLocked(sh, full);
-                }
-                if (!full.empty()) enqueue(std::move(full));
-            }
+            takePartials(Clock::now().time_since_epoch().count());
             lk.lock();
         }
+    }
+
+    // Queues the partial shards as few batches: when one shard is due (its first packet
+    // arrived flush_us ago, or `now` == 0: an explicit flush), every non-empty shard's packets
+    // go into one merged batch (up to 4 x the batch size each), so a flush tick costs one
+    // device pass rather than one per onPacket thread (16 threads each flushing a few
+    // thousand packets every tick spent most of the device time on per-call costs).
+    void takePartials(int64_t now) {
+        const int64_t due = now - std::chrono::duration_cast<Clock::duration>(std::chrono::microseconds(flush_us_)).count();
+        bool any_due = now == 0;
+        for (Shard& sh : shards_) {
+            const int64_t f = sh.first.load(std::memory_order_relaxed);
+            if (f && f <= due) any_due = true;
+        }
+        if (!any_due) return;
+        HeldBatch merged[2];   // by `whole` mode
+        for (Shard& sh : shards_) {
+            HeldBatch part;
+            {
+                std::lock_guard<std::mutex> sl(sh.mu);
+                if (!sh.pending.empty()) takeLocked(sh, part);
+            }
+            if (part.empty()) continue;
+            HeldBatch& m = merged[part.whole ? 1 : 0];
+            m.append(part);
+            if (m.size() >= 4 * batch_) enqueue(std::move(m)), m.clear();
+            if (part.capacity()) recycleEmpty(std::move(part));
+        }
+        for (HeldBatch& m : merged)
+            if (!m.empty()) enqueue(std::move(m));
+    }
+
+    // a cleared vector set back into circulation
+    void recycleEmpty(HeldBatch&& v) {
+        v.clear();
+        std::lock_guard<std::mutex> lk(q_mu_);
+        if (clean_.size() < kShards) clean_.push_back(std::move(v));
     }
 
     void stopFlusher() {

@@ -2,7 +2,7 @@
 // to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
 // integrator calls").
 //
-//   surface_bench [all|filter|ref|mt|parser|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
+//   surface_bench [all|filter|ref|mt|parser|sizes|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
 //                 [--chunks 16384,65536]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
@@ -208,6 +208,31 @@ void bench_gpu_filter_mt(const Capture& c, int threads, size_t chunk, double sec
     line(apply ? "GpuPacketFilter::applyFilters(vector<Packet>) -> vector<FilterResult>, T callers"
                : "GpuPacketFilter::classify(vector<Packet>), T callers",
          c, threads, done / el, extra);
+}
+
+// One caller, classify() over batches of growing size: the per-call time splits into a fixed
+// cost (host gather start, copies, launch, the wait) and a per-packet cost.
+void bench_call_sizes(const Capture& c, double seconds) {
+    GpuPacketFilter f;
+    add_set(f);
+    for (size_t n : {1024u, 4096u, 16384u, 65536u, 262144u}) {
+        if (n > c.packets.size()) break;
+        const std::vector<Packet> part(c.packets.begin(), c.packets.begin() + n);
+        (void)f.classify(part);
+        uint64_t calls = 0;
+        double dev = 0;
+        const auto t0 = Clock::now();
+        while (secs(t0, Clock::now()) < seconds / 5) {
+            (void)f.classify(part);
+            dev += f.lastBatchTiming().device_s;
+            ++calls;
+        }
+        const double el = secs(t0, Clock::now());
+        char extra[160];
+        std::snprintf(extra, sizeof(extra), "\"batch\": %zu, \"us_per_call\": %.1f, \"device_pass_us\": %.1f", n,
+                      el / calls * 1e6, dev / calls * 1e6);
+        line("GpuPacketFilter::classify(vector<Packet>) by batch size", c, 1, (double)calls * n / el, extra);
+    }
 }
 
 // The floor of any applyFilters(vector) -> vector<FilterResult>: constructing n results,
@@ -460,6 +485,7 @@ int main(int argc, char** argv) {
             }
         }
         if (what == "all" || what == "parser") bench_parser(c, threads, seconds);
+        if (what == "all" || what == "sizes") bench_call_sizes(c, seconds);
         if (what == "all" || what == "plugin") {
             bench_plugin(c, 1, seconds, so);
             bench_plugin(c, threads, seconds, so);
