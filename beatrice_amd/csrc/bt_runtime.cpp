@@ -78,7 +78,9 @@ class HostPool {
 public:
     explicit HostPool(unsigned n) {
         nthreads_ = n ? n : 1;
-        for (unsigned i = 1; i < nthreads_; ++i) th_.emplace_back([this] { loop(); });
+        static const bool fixed = getenv("BT_POOL_FIXED") != nullptr;   // A/B: each worker its own index
+        fixed_ = fixed;
+        for (unsigned i = 1; i < nthreads_; ++i) th_.emplace_back([this, i] { loop(i); });
     }
     ~HostPool() {
         {
@@ -103,7 +105,13 @@ public:
             claim_.store((uint64_t)g << 32, std::memory_order_release);
         }
         cv_.notify_all();
-        execute(g, fn);
+        if (fixed_) {
+            fn(0);
+            std::lock_guard<std::mutex> lk(m_);
+            ++finished_;
+        } else {
+            execute(g, fn);
+        }
         std::unique_lock<std::mutex> lk(m_);
         done_.wait(lk, [this] { return finished_ == nthreads_; });
         fn_ = nullptr;
@@ -124,7 +132,7 @@ private:
             if (++finished_ == nthreads_) done_.notify_one();
         }
     }
-    void loop() {
+    void loop(unsigned id) {
         uint64_t seen = 0;
         for (;;) {
             const std::function<void(unsigned)>* f;
@@ -137,7 +145,14 @@ private:
                 f = fn_;   // null when that run has already finished
                 g = (uint32_t)gen_;
             }
-            if (f) execute(g, *f);
+            if (!f) continue;
+            if (fixed_) {   // round 2's pool: worker id runs index id, the caller waits for all
+                (*f)(id);
+                std::lock_guard<std::mutex> lk(m_);
+                if (++finished_ == nthreads_) done_.notify_one();
+            } else {
+                execute(g, *f);
+            }
         }
     }
     std::vector<std::thread> th_;
@@ -146,6 +161,7 @@ private:
     const std::function<void(unsigned)>* fn_ = nullptr;
     std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
     unsigned finished_ = 0, nthreads_ = 1;
+    bool fixed_ = false;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
