@@ -294,7 +294,7 @@ HostPool& pool_of(bt_ctx* c) {
             // 8, not every usable CPU: with callers on all 16 of a GPU box's CPUs (T callers of
             // one GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool
             // oversubscribes them: C2 applyFilters 136-142 against 163 Mpps, classify 161-163
-            // against 172-192 (tools/surfaces/ab_pool_threads.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
+            // against 172-192 (tools/ab_cmd.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
             const char* e = getenv("BT_HOST_THREADS");
             nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(8u, usable_cpus());
         }
