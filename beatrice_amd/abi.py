@@ -146,7 +146,7 @@ EXPORTS = [
     "bt_filter_compile",
     "bt_filter_program", "bt_filter_compile_host", "bt_reserve", "bt_parse_filter_device",
     "bt_parse_filter_device_async",
-    "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
+    "bt_parse_filter", "bt_parse_filter_ptrs", "bt_host_stage_bytes", "bt_host_register", "bt_host_unregister", "bt_dev_malloc", "bt_dev_free", "bt_memcpy_h2d", "bt_memcpy_d2h", "bt_memset_d",
     "bt_synchronize", "bt_host_parallel", "bt_stream_create", "bt_stream_synchronize", "bt_stream_destroy", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3", "bt_ring_walk_tpv3_gpu",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
@@ -185,6 +185,7 @@ def lib() -> ctypes.CDLL:
                                                         vp]),
         "bt_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+        "bt_host_stage_bytes": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(u32)]),
         "bt_host_register": (ctypes.c_int, [vp, vp, u64, ctypes.POINTER(vp)]),
         "bt_host_unregister": (ctypes.c_int, [vp, vp]),
         "bt_dev_malloc": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),

@@ -963,6 +963,15 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
 
 namespace {
 
+// Bytes of each frame the host pipeline stages (bt_host_stage_bytes): the walk's 112 with
+// records; the filters' 38 B (as 48) for filter-only calls, whose kernels take no second
+// round (staging the walk's 112 B took 2-3x the gather and the copy for IMIX frames); the
+// payload window with a GPU PAYLOAD slot (bytes past the staged prefix would be the next
+// frame's).
+uint32_t stage_bytes(const bt_ctx* c, bool records) {
+    return !c->dfa_pool.empty() ? kHostSlotPayload : records ? kHostSlot : kHostSlotFilter;
+}
+
 // Host batch pipeline shared by bt_parse_filter (base + descriptors) and
 // bt_parse_filter_ptrs (one pointer per frame): frame(i, &len) returns frame i.
 template <class FrameFn>
@@ -980,9 +989,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
     const uint32_t chunk = c->chunk;
     // bytes staged per frame: the header walk's, or with a GPU PAYLOAD slot in the program
     // the payload window's too (bytes past the staged prefix would be the next frame's)
-    // (filter-only calls: the filters' 38 B; staging the walk's 112 B took 2-3x the gather
-    // and the copy for IMIX frames)
-    const uint32_t slot = !c->dfa_pool.empty() ? kHostSlotPayload : records ? kHostSlot : kHostSlotFilter;
+    const uint32_t slot = stage_bytes(c, records != nullptr);
     uint32_t next = 0, k = 0;
     while (next < n || c->hs[0].busy || c->hs[1].busy) {
         HostSlot& s = c->hs[k & 1];
@@ -1118,6 +1125,13 @@ int bt_parse_filter_ptrs(bt_ctx* c, const uint8_t* const* frames, const uint32_t
             return frames[i];
         },
         records, verdict, decide, pass_idx, n_pass);
+}
+
+int bt_host_stage_bytes(const bt_ctx* c, int with_records, uint32_t* bytes) {
+    if (!c || !bytes) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> lk(const_cast<bt_ctx*>(c)->mu);
+    *bytes = stage_bytes(c, with_records != 0);
+    return BT_OK;
 }
 
 int bt_host_register(bt_ctx* c, void* host, uint64_t bytes, void** dev_alias) {

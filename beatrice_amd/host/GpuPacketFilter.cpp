@@ -504,14 +504,41 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<P
     return v;
 }
 
+uint32_t GpuPacketFilter::stagedPrefixBytes(bool withRecords) {
+    const auto lock = lockProgram();
+    uint32_t b = 0;
+    if (bt_host_stage_bytes(ctx_, withRecords ? 1 : 0, &b) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    return b;
+}
+
 GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const uint8_t* const* frames, const uint32_t* lens,
                                                              size_t n, bool withRecords,
-                                                             const std::function<Packet(size_t)>& packetOf) {
+                                                             const std::function<Packet(size_t)>& packetOf,
+                                                             uint32_t readable) {
     Verdicts v;
     const auto lock = lockProgram();
     const InFlight busy(inFlight_);
     if (!n) return v;
     if (!frames || !lens || !packetOf) throw std::invalid_argument("GpuPacketFilter::classifyPerPacket: null argument");
+    // prefixes too short for the program under this lock (a GPU PAYLOAD slot reads the
+    // payload window): the packets' own bytes instead
+    std::vector<Packet> own;
+    std::vector<const uint8_t*> ownFrames;
+    if (readable) {
+        uint32_t need = 0;
+        if (bt_host_stage_bytes(ctx_, withRecords ? 1 : 0, &need) != BT_OK)
+            throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+        if (readable < need) {
+            own.reserve(n);
+            ownFrames.resize(n);
+            for (size_t i = 0; i < n; ++i) {
+                own.push_back(packetOf(i));
+                ownFrames[i] = own.back().data();
+            }
+            frames = ownFrames.data();
+        }
+    }
     const auto t0 = std::chrono::steady_clock::now();
     runFrames(frames, lens, (uint32_t)n, v.decide, withRecords ? &v.records : nullptr);
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /

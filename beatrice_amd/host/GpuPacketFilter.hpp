@@ -89,8 +89,14 @@ public:
     // The same over frames held by the caller (n pointers and lengths, e.g. a batch that keeps
     // only each Packet's bytes alive); packetOf(i) gives packet i for the host-side filters
     // (PAYLOAD regexes outside the GPU subset, CUSTOM callbacks), only for packets that reach one.
+    // `readable` (0 = whole frames): frames[i] may hold only the first `readable` bytes of
+    // packet i (lens[i] stays its true length), e.g. prefixes packed when the packets
+    // arrived; enough when readable >= stagedPrefixBytes(withRecords), otherwise the call
+    // reads the packets' own bytes through packetOf.
     Verdicts classifyPerPacket(const uint8_t* const* frames, const uint32_t* lens, size_t n, bool withRecords,
-                               const std::function<Packet(size_t)>& packetOf);
+                               const std::function<Packet(size_t)>& packetOf, uint32_t readable = 0);
+    // The bytes of each frame a batch call reads with the current program (bt_host_stage_bytes).
+    uint32_t stagedPrefixBytes(bool withRecords);
 
     // Zero-copy form over frames the device already sees (a capture ring registered
     // with bt_host_register): runs parse+filter over `batch` into `out` (device-visible

@@ -15,6 +15,10 @@
 //                          flush thread when no further packet comes (default 2000)
 //   BEATRICE_GPU_WORKERS   classifier threads (default 2, at most 8)
 //   BEATRICE_GPU_DEBUG     1: onStop prints where the classifier threads' time went
+//   BEATRICE_GPU_PACK      1: pack header prefixes at onPacket time (HeldBatch; off by default:
+//                          with frames that are not in the onPacket thread's cache it was
+//                          slower, C3 from 16 threads 29 against 39-43 Mpps,
+//                          profiles/r03/surfaces/ab_plugin_pack.jsonl)
 //   BEATRICE_GPU_FILTERS   ';'-separated  name|TYPE|priority|expression  entries, TYPE one of
 //                          BPF PROTOCOL IP_RANGE PORT_RANGE PAYLOAD CUSTOM
 //
@@ -33,12 +37,14 @@
 //
 // Link with -Wl,-z,nodelete: ~PluginManager dlcloses handles before destroying plugins
 // (src/PluginManager.cpp:26-34).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <condition_variable>
 #include <deque>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -59,12 +65,21 @@ namespace gpu {
 // pass reads (28 B per packet instead of a 216-B Packet copy, whose copy and destruction were
 // most of onPacket's time), plus the whole Packets only while a CUSTOM filter (whose callback
 // gets the Packet, metadata included) is installed.
+//
+// With BEATRICE_GPU_PACK=1 and a program that allows it (no GPU PAYLOAD slot), each packet's
+// first W bytes (the bytes the device pass reads: 48 for verdicts, 112 with records,
+// bt_host_stage_bytes) are also copied, at onPacket time, into `pre` (W bytes per packet, back
+// to back): the classifier's gather then reads one sequential buffer instead of a cache miss
+// per frame, and the copy moves to the onPacket threads (a gain only where they hold the
+// frame in cache, e.g. right after the capture backend wrote it).
 struct HeldBatch {
     std::vector<std::shared_ptr<const uint8_t[]>> keep;
     std::vector<const uint8_t*> frames;
     std::vector<uint32_t> lens;
     std::vector<Packet> packets;   // empty unless the batch started with a CUSTOM filter installed
+    std::vector<uint8_t> pre;      // W bytes per packet when W != 0
     bool whole = false;
+    uint32_t W = 0;
 
     size_t size() const { return frames.size(); }
     bool empty() const { return frames.empty(); }
@@ -73,18 +88,26 @@ struct HeldBatch {
         frames.push_back(p.data());
         lens.push_back((uint32_t)p.length());
         if (whole) packets.push_back(p);
+        if (W) {
+            const size_t at = pre.size();
+            pre.resize(at + W);
+            std::memcpy(pre.data() + at, p.data(), std::min<size_t>(p.length(), W));
+        }
     }
     void clear() {
         keep.clear();
         frames.clear();
         lens.clear();
         packets.clear();
+        pre.clear();
         whole = false;
+        W = 0;
     }
     void reserve(size_t n) {
         keep.reserve(n);
         frames.reserve(n);
         lens.reserve(n);
+        if (W) pre.reserve(n * W);
     }
     size_t capacity() const { return frames.capacity(); }
     void swap(HeldBatch& o) {
@@ -92,9 +115,11 @@ struct HeldBatch {
         frames.swap(o.frames);
         lens.swap(o.lens);
         packets.swap(o.packets);
+        pre.swap(o.pre);
         std::swap(whole, o.whole);
+        std::swap(W, o.W);
     }
-    // appends o's packets (same `whole` mode; o is left empty)
+    // appends o's packets (same `whole` mode and W; o is left empty)
     void append(HeldBatch& o) {
         if (empty()) {
             swap(o);
@@ -104,6 +129,7 @@ struct HeldBatch {
         frames.insert(frames.end(), o.frames.begin(), o.frames.end());
         lens.insert(lens.end(), o.lens.begin(), o.lens.end());
         packets.insert(packets.end(), std::make_move_iterator(o.packets.begin()), std::make_move_iterator(o.packets.end()));
+        pre.insert(pre.end(), o.pre.begin(), o.pre.end());
         o.clear();
     }
     // packet i for the host-side filters: the held Packet, or one made from its bytes
@@ -128,9 +154,11 @@ public:
             records_ = env_int("BEATRICE_GPU_RECORDS", 0) != 0;
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
             workers_ = std::min(8, std::max(1, env_int("BEATRICE_GPU_WORKERS", 2)));
+            pack_ = env_int("BEATRICE_GPU_PACK", 0) != 0;
             filter_ = std::make_shared<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
             whole_ = filter_->needsPackets();
+            stage_ = stageWidth(*filter_);
         }
         {
             std::lock_guard<std::mutex> lk(flush_mu_);
@@ -176,6 +204,7 @@ public:
             if (sh.pending.empty()) {
                 sh.first.store(Clock::now().time_since_epoch().count(), std::memory_order_relaxed);
                 sh.pending.whole = wholePackets();
+                sh.pending.W = stage_.load(std::memory_order_relaxed);
                 armed = true;
             }
             sh.pending.push(packet);             // shares the immutable bytes, no copy
@@ -242,6 +271,15 @@ private:
     // through filter() reaches the batches started after the next one; the packets of batches
     // already pending reach its callback as Packet(bytes, length)).
     bool wholePackets() const { return whole_.load(std::memory_order_relaxed); }
+
+    // Prefix bytes new batches pack per packet: what the device pass reads with the current
+    // program, when that is a header prefix (not with a GPU PAYLOAD slot, whose window the
+    // device reads from the frame itself); only with BEATRICE_GPU_PACK=1.
+    uint32_t stageWidth(GpuPacketFilter& f) const {
+        if (!pack_) return 0;
+        const uint32_t w = f.stagedPrefixBytes(records_);
+        return w <= 112 ? w : 0u;
+    }
 
     static size_t shardOfThisThread() {
         static std::atomic<size_t> next{0};
@@ -318,9 +356,17 @@ private:
             if (f) {
                 try {
                     const HeldBatch& b = q.batch;
-                    v = f->classifyPerPacket(b.frames.data(), b.lens.data(), b.size(), records_,
-                                             [&b](size_t i) { return b.packet(i); });
+                    const uint8_t* const* frames = b.frames.data();
+                    thread_local std::vector<const uint8_t*> packed;
+                    if (b.W) {   // the packed prefixes stand in for the frames
+                        packed.resize(b.size());
+                        for (size_t i = 0; i < b.size(); ++i) packed[i] = b.pre.data() + i * b.W;
+                        frames = packed.data();
+                    }
+                    v = f->classifyPerPacket(frames, b.lens.data(), b.size(), records_,
+                                             [&b](size_t i) { return b.packet(i); }, b.W);
                     whole_ = f->needsPackets();
+                    stage_ = stageWidth(*f);
                     ok = true;
                     prof_.device_ns += (uint64_t)(f->lastBatchTiming().device_s * 1e9);
                 } catch (const std::exception&) {   // the device failed: nobody to throw to here
@@ -411,7 +457,7 @@ private:
             if (f && f <= due) any_due = true;
         }
         if (!any_due) return;
-        HeldBatch merged[2];   // by `whole` mode
+        HeldBatch merged[4];   // by `whole` mode and whether prefixes are packed (W is one value at a time)
         for (Shard& sh : shards_) {
             HeldBatch part;
             {
@@ -419,7 +465,11 @@ private:
                 if (!sh.pending.empty()) takeLocked(sh, part);
             }
             if (part.empty()) continue;
-            HeldBatch& m = merged[part.whole ? 1 : 0];
+            HeldBatch& m = merged[(part.whole ? 1 : 0) + (part.W ? 2 : 0)];
+            if (!m.empty() && m.W != part.W) {   // the program changed between two shards
+                enqueue(std::move(m));
+                m.clear();
+            }
             m.append(part);
             if (m.size() >= 4 * batch_) enqueue(std::move(m)), m.clear();
             if (part.capacity()) recycleEmpty(std::move(part));
@@ -475,6 +525,8 @@ private:
     std::mutex gpu_mu_;                // filter_, sink_
     std::shared_ptr<GpuPacketFilter> filter_;   // a batch in flight holds its own reference
     std::atomic<bool> whole_{false};            // wholePackets()
+    std::atomic<uint32_t> stage_{0};            // stageWidth() of the current program
+    bool pack_ = true;                          // BEATRICE_GPU_PACK
     size_t batch_ = 65536;
     int flush_us_ = 2000;
     bool records_ = false;

@@ -379,6 +379,12 @@ int  bt_parse_filter(bt_ctx* ctx, const uint8_t* base, const bt_pkt_desc* desc, 
 int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                           bt_rec* records, uint64_t* verdict, uint8_t* decide,
                           uint32_t* pass_idx, uint32_t* n_pass);
+/* The bytes of each frame the two calls above read (and stage) with the context's current
+ * program: min(len, *bytes) from the frame's start; 48 for filter-only calls, 112 with
+ * records, 176 when the program has a GPU PAYLOAD slot (with_records: whether the call asks
+ * for records). A caller may pass, in place of a frame, a copy of that many of its first
+ * bytes with the frame's true length (e.g. prefixes packed when the packet arrived). */
+int  bt_host_stage_bytes(const bt_ctx* ctx, int with_records, uint32_t* bytes);
 
 /* Zero-copy ingest: page-lock a host range (an AF_XDP UMEM, an RX descriptor ring,
  * an output array) and map it into the device; *dev_alias is the pointer kernels

@@ -18,8 +18,9 @@
 //   sink     the verdict sink sees every batch once, in order, and each packet's verdict
 //            and deciding filter equal the reference's FilterResult;
 //   threads  onPacket from 4 threads at once: every packet is classified exactly once;
-//   hostre / custom  a host-side PAYLOAD regex (resumed from the bytes a pending batch holds)
-//            and a CUSTOM filter (whole Packets held) give the reference's verdicts;
+//   hostre / gpure / custom  a host-side PAYLOAD regex (resumed from the bytes a pending
+//            batch holds), a GPU PAYLOAD regex (no packed prefixes) and a CUSTOM filter (whole
+//            Packets held) give the reference's verdicts;
 //   records  (test_plugin records DATA DESC REC, files written by tests/test_cpp_adapter.py
 //            from a reference golden capture) with BEATRICE_GPU_RECORDS=1 the sink's bt_rec
 //            of every packet equals the golden record the compiled reference's parser
@@ -438,8 +439,21 @@ int main(int argc, char** argv) {
     // Packets for the callback
     ok &= pipeline_case(so, fuzz, 20000, 2048, "hostre", {{"tcp", 1, 3, "tcp"}, {"word", 4, 2, "\\bHTTP"},
                                                            {"ports", 3, 1, "0-40000"}});
+    // a PAYLOAD regex the GPU runs as a DFA (the device reads the payload window from the
+    // frames, so pending batches pack no prefixes)
+    ok &= pipeline_case(so, fuzz, 20000, 2048, "gpure", {{"tcp", 1, 3, "tcp"}, {"get", 4, 2, "GET|HTTP"},
+                                                          {"ports", 3, 1, "0-40000"}});
     ok &= pipeline_case(so, c3, 5000, 4096, "custom", {{"fn", 5, 3, ""}, {"net", 2, 2, "10.0.0.0/8"},
                                                          {"ports", 3, 1, "1000-2000"}});
+    // the same with header prefixes packed at onPacket time (BEATRICE_GPU_PACK=1)
+    setenv("BEATRICE_GPU_PACK", "1", 1);
+    ok &= pipeline_case(so, c3, 20000, 4096, "c3/pack", {{"proto", 1, 3, "udp"}, {"net", 2, 2, "10.0.0.0/8"},
+                                                           {"ports", 3, 1, "1000-2000"}});
+    ok &= pipeline_case(so, fuzz, 20000, 2048, "hostre/pk", {{"tcp", 1, 3, "tcp"}, {"word", 4, 2, "\\bHTTP"},
+                                                               {"ports", 3, 1, "0-40000"}});
+    ok &= pipeline_case(so, fuzz, 20000, 2048, "gpure/pk", {{"tcp", 1, 3, "tcp"}, {"get", 4, 2, "GET|HTTP"},
+                                                              {"ports", 3, 1, "0-40000"}});
+    unsetenv("BEATRICE_GPU_PACK");
     ok &= threads_case(so, c3);
     std::printf(ok && !g_fail ? "ALL OK\n" : "FAILURES\n");
     return ok && !g_fail ? 0 : 1;
