@@ -393,8 +393,8 @@ private:
             ++prof_.batches;
             lk.lock();
             done_seq_ = q.seq + 1;
-            if (used_.size() < kShards) used_.push_back(std::move(q.batch));
-            else {   // nobody is recycling (no full shards): release here
+            if (used_.size() < kMaxUsed) used_.push_back(std::move(q.batch));
+            else {   // the producers are not recycling (no full shards): release here
                 lk.unlock();
                 q.batch.clear();
                 lk.lock();
@@ -532,6 +532,9 @@ private:
     bool records_ = false;
     // the classifier thread's queue and the vectors recycled through it (q_mu_)
     static constexpr size_t kMaxQueued = 4;
+    // classified batches waiting for a producer to release their packets: each still holds
+    // its packets' buffers, so only a few (the capture's memory is not the plugin's to keep)
+    static constexpr size_t kMaxUsed = 4;
     struct Queued {
         uint64_t seq;
         HeldBatch batch;

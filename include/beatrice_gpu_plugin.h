@@ -56,7 +56,8 @@ typedef void (*gpu_verdict_sink_fn)(void* user, const gpu_verdict_batch* batch);
 void gpu_plugin_set_sink(gpu_plugin* plugin, gpu_verdict_sink_fn fn, void* user);
 /* Classifies the partial batches now and returns once every batch queued so far has reached
  * the sink (the plugin's flush thread queues a partial batch on its own
- * BEATRICE_GPU_FLUSH_US after the batch's first packet). */
+ * BEATRICE_GPU_FLUSH_US after the batch's first packet). Not from inside the sink, which
+ * runs on a classifier thread the call would wait for. */
 void gpu_plugin_flush(gpu_plugin* plugin);
 /* Packets that passed every filter so far. */
 uint64_t gpu_plugin_passed(const gpu_plugin* plugin);
