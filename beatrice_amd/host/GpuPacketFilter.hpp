@@ -161,6 +161,8 @@ private:
     template <class PacketAt>
     Tally scan(size_t n, PacketAt packet, std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
                std::vector<uint32_t>* error_idx);
+    bool scanParallel(size_t n, const std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
+                      std::vector<uint32_t>* error_idx, Tally& t);
     void flushTally(const Tally& t, std::chrono::microseconds per);
 
     void open(const std::vector<int>& devices, const bt_opts* opts);

@@ -150,6 +150,25 @@ static bool filter_case(const char* label, const Capture& cap, const std::vector
                   a[i].reason.c_str(), b[i].passed, b[i].filterName.c_str(), b[i].reason.c_str());
         }
     }
+    {   // classify / classifyPerPacket on their own filter: the same passes (and throw)
+        GpuPacketFilter g2(0);
+        install(g2, specs);
+        for (const auto& r : remove) g2.removeFilter(r);
+        std::exception_ptr ec;
+        GpuPacketFilter::Verdicts v;
+        try { v = g2.classify(cap.packets); } catch (...) { ec = std::current_exception(); }
+        CHECK((bool)ea == (bool)ec, "%s: classify exception mismatch", label);
+        if (ec) {
+            CHECK(what_kind(ea) == what_kind(ec), "%s: classify threw %s", label, what_kind(ec).c_str());
+        } else {
+            std::vector<uint32_t> want;
+            for (size_t i = 0; i < a.size(); ++i)
+                if (a[i].passed) want.push_back((uint32_t)i);
+            CHECK(v.pass_idx == want, "%s: classify pass list (%zu vs %zu)", label, v.pass_idx.size(), want.size());
+            const auto w = g2.classifyPerPacket(cap.packets);
+            CHECK(w.pass_idx == want && w.error_idx.empty(), "%s: classifyPerPacket pass list", label);
+        }
+    }
     auto sa = ref.getStats(), sb = gpu.getStats();
     CHECK(sa.packetsProcessed == sb.packetsProcessed && sa.packetsPassed == sb.packetsPassed &&
               sa.packetsDropped == sb.packetsDropped && sa.filterCounts == sb.filterCounts,
@@ -725,6 +744,14 @@ int main(int argc, char** argv) {
     ok &= filter_case("c3/throw-late", c3, throws_late);
     ok &= filter_case("c4/custom-throw", c4, custom_throw);
     ok &= filter_case("c3/no-filters", c3, {});
+    // batches of >= 65536 packets take the parallel decision scan (a HOST code falls back to
+    // the serial one; a throw stops the tally at the first throwing packet)
+    {
+        Capture big = capture(3, 300000, 0x5EED0033);
+        ok &= filter_case("big/headline", big, headline);
+        ok &= filter_case("big/throw-late", big, throws_late);
+        ok &= filter_case("big/payload+custom", big, host_side);
+    }
     ok &= concurrent_case("c3/headline", c3, headline, 8);
     ok &= concurrent_case("fuzz/payload+custom", fz, host_side, 6);
     ok &= parser_case("c3", c3);
