@@ -53,6 +53,7 @@ constexpr uint32_t kHostSlotPayload = 176;
 // ... and for calls that return no records and have no GPU PAYLOAD slot: the filters read
 // bytes 12..37 (kNeedFilter) and such calls never take a second round, so 48 B
 constexpr uint32_t kHostSlotFilter = 48;
+constexpr uint32_t kGatherAheadDefault = 12;   // frames the host gather prefetches ahead
 static_assert(kHostSlotFilter >= kNeedFilter && kHostSlotFilter % 16 == 0, "filter-only staging");
 
 struct HostSlot {                      // one half of the double-buffered host pipeline
@@ -990,6 +991,11 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
     // bytes staged per frame: the header walk's, or with a GPU PAYLOAD slot in the program
     // the payload window's too (bytes past the staged prefix would be the next frame's)
     const uint32_t slot = stage_bytes(c, records != nullptr);
+    static const bool prefetch = getenv("BT_NO_GATHER_PREFETCH") == nullptr;   // A/B knobs
+    static const uint32_t kGatherAhead = [] {
+        const char* e = getenv("BT_GATHER_AHEAD");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : kGatherAheadDefault;
+    }();
     uint32_t next = 0, k = 0;
     while (next < n || c->hs[0].busy || c->hs[1].busy) {
         HostSlot& s = c->hs[k & 1];
@@ -1021,6 +1027,12 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t p = part[w];
                 for (uint32_t i = a; i < b; ++i) {
+                    if (prefetch && i + kGatherAhead < b) {   // frames far apart: start the miss early
+                        uint32_t l2 = 0;
+                        const uint8_t* g = frame(base_i + i + kGatherAhead, &l2);
+                        __builtin_prefetch(g);
+                        if (((uintptr_t)g & 63u) + std::min(l2, slot) > 64u) __builtin_prefetch(g + 64);
+                    }
                     uint32_t len = 0;
                     const uint8_t* f = frame(base_i + i, &len);
                     const uint32_t m = std::min(len, slot);
