@@ -36,6 +36,10 @@ ap.add_argument("--mix", type=int, default=0,
 ap.add_argument("--gpu-walk", action="store_true",
                 help="with --tpacket: the frame chains are walked on the GPU (bt_ring_walk_tpv3_gpu: the host "
                      "reads only the block headers), descriptors in device memory")
+ap.add_argument("--host-gather", action="store_true",
+                help="with --tpacket: walk each batch of blocks, then bt_parse_filter over the ring and those "
+                     "descriptors (the host pipeline's prefetched gather -> H2D -> kernels -> D2H) instead of "
+                     "the kernels reading the frames in place")
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
 ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="bt_opts.flags (A/B, e.g. 0x8000 no lean PCIe round A)")
 ap.add_argument("--host-threads", type=int, default=0)
@@ -67,6 +71,7 @@ if a.tpacket:
         h_dec = np.zeros(tiles * 64, np.uint8)
         h_ver = np.zeros(tiles, np.uint64)
         h_rec = np.zeros(tiles * 6144, np.uint8) if rec else None
+        h_recs = np.zeros(n * 96, np.uint8) if rec and a.host_gather else None   # bt_rec, AoS
         d_dec, d_ver = ctx.register(h_dec), ctx.register(h_ver)
         d_rec = ctx.register(h_rec) if rec else None
 
@@ -96,6 +101,15 @@ if a.tpacket:
                         counts.append(cnt)
                 else:
                     cnt = counts[k]
+                if a.host_gather:   # synchronous: the host pipeline over the ring + this batch's descriptors
+                    p = lambda arr, off: None if arr is None else arr.ctypes.data + off  # noqa: E731
+                    rc = abi.lib().bt_parse_filter(ctx.h, ring.ctypes.data, h_desc.ctypes.data + 8 * start, cnt,
+                                                   p(h_recs, 96 * start), p(h_ver, 8 * tile), p(h_dec, 64 * tile),
+                                                   None, None)
+                    assert rc == 0, abi.lib().bt_last_error()
+                    start += cnt
+                    tile += (cnt + 63) // 64
+                    continue
                 if gathered:
                     batch = abi.Batch(d_slots + abi.PREFIX_SLOT * start, d_desc + 8 * start, 0, cnt,
                                       abi.PREFIX_SLOT * cnt, abi.DESC_PACKED, abi.BATCH_PREFIXES)
@@ -137,7 +151,8 @@ if a.tpacket:
         walk = time.perf_counter() - t0
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
-        how = f"tpacket_v3 ring, header gather packed per block, every {a.mix}th batch in place, zero-copy, " \
+        how = "tpacket_v3 ring, walk then host gather (bt_parse_filter), " if a.host_gather else \
+            f"tpacket_v3 ring, header gather packed per block, every {a.mix}th batch in place, zero-copy, " \
             if a.gather and a.dense and a.mix else \
             "tpacket_v3 ring, header gather packed per block, zero-copy, " if a.gather and a.dense else \
             "tpacket_v3 ring, header gather into 128-B slots, zero-copy, " if a.gather else \
