@@ -14,16 +14,83 @@
 // packets are independent.
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include <condition_variable>
+#include <functional>
+
 #include "bt_host.h"
+
+namespace {
+
+// One thread per member after the first, kept for the group's life: member k's part of a batch
+// runs on thread k (member 0 on the caller), so a batch costs no thread creation (a plugin's
+// 64k-packet batches over 8 devices had spawned 7 threads per batch).
+class MemberThreads {
+public:
+    explicit MemberThreads(uint32_t members) {
+        for (uint32_t k = 1; k < members; ++k) th_.emplace_back([this, k] { loop(k); });
+    }
+    ~MemberThreads() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // fn(k) for every member k, concurrently; returns when all have
+    void run(const std::function<void(uint32_t)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            pending_ = (uint32_t)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop(uint32_t k) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t)>* f;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = fn_;
+            }
+            (*f)(k);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t)>* fn_ = nullptr;
+    uint32_t pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace
 
 struct bt_group {
     std::vector<bt_ctx*> members;
     std::mutex mu;   // one batch at a time (each member serialises its own calls anyway)
+    std::unique_ptr<MemberThreads> threads;   // members > 1
 };
 
 namespace {
@@ -54,14 +121,10 @@ int run_members(bt_group* g, Fn fn) {
     if (m == 1) return fn(0u);   // one device: no thread
     std::vector<int> rc(m, BT_OK);
     std::vector<std::string> msg(m);
-    std::vector<std::thread> th;
-    th.reserve(m);
-    for (uint32_t k = 0; k < m; ++k)
-        th.emplace_back([&, k] {
-            rc[k] = fn(k);
-            if (rc[k]) msg[k] = bt_last_error();
-        });
-    for (auto& t : th) t.join();
+    g->threads->run([&](uint32_t k) {
+        rc[k] = fn(k);
+        if (rc[k]) msg[k] = bt_last_error();
+    });
     for (uint32_t k = 0; k < m; ++k)
         if (rc[k]) return bt::set_error(rc[k], "group member %u (device %d): %s", k, bt::ctx_device(g->members[k]),
                                         msg[k].c_str());
@@ -149,12 +212,14 @@ int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts,
         }
         g->members.push_back(c);
     }
+    if (n_devices > 1) g->threads = std::make_unique<MemberThreads>(n_devices);
     *out = g;
     return BT_OK;
 }
 
 void bt_group_destroy(bt_group* g) {
     if (!g) return;
+    g->threads.reset();
     for (bt_ctx* c : g->members) bt_destroy(c);
     delete g;
 }
