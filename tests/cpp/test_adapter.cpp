@@ -124,10 +124,19 @@ static std::string what_kind(const std::exception_ptr& e) {
     }
 }
 
+// members > 1: the filter drives a group of that many contexts on device 0 (a device list,
+// as BEATRICE_GPU_DEVICES gives; BT_OPT_GROUP_SHARED_DEVICE lets one GPU stand in for several)
+static bt_opts shared_device_opts() {
+    bt_opts o{};
+    o.flags = BT_OPT_GROUP_SHARED_DEVICE;
+    return o;
+}
+
 static bool filter_case(const char* label, const Capture& cap, const std::vector<Spec>& specs,
-                        const std::vector<std::string>& remove = {}) {
+                        const std::vector<std::string>& remove = {}, int members = 1) {
     PacketFilter ref;
-    GpuPacketFilter gpu(0);
+    const bt_opts shared = shared_device_opts();
+    GpuPacketFilter gpu(std::vector<int>(members, 0), members > 1 ? &shared : nullptr);
     install(ref, specs);
     install(gpu, specs);
     for (const auto& r : remove) {
@@ -751,6 +760,10 @@ int main(int argc, char** argv) {
         ok &= filter_case("big/headline", big, headline);
         ok &= filter_case("big/throw-late", big, throws_late);
         ok &= filter_case("big/payload+custom", big, host_side);
+        // a three-member group (one device standing in for three): split, merged, same results
+        ok &= filter_case("group3/big/headline", big, headline, {}, 3);
+        ok &= filter_case("group3/big/throw-late", big, throws_late, {}, 3);
+        ok &= filter_case("group2/fuzz/payload+custom", fz, host_side, {}, 2);
     }
     ok &= concurrent_case("c3/headline", c3, headline, 8);
     ok &= concurrent_case("fuzz/payload+custom", fz, host_side, 6);
