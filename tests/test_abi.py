@@ -3,12 +3,14 @@ declares, and refuses to run without a GPU (no CPU fallback)."""
 import ctypes
 import os
 import re
+import subprocess
 
 import pytest
 
 from beatrice_amd import abi
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "beatrice_gpu.h")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "beatrice_gpu.h")
 
 
 def declared():
@@ -83,3 +85,30 @@ def test_packed_records_round_trip():
         buf = np.zeros_like(rec)
         assert abi.lib().bt_record_unpack(None, tiled.ctypes.data, n, n, 0, buf.ctypes.data, abi.ctypes.byref(tot)) == 0
         assert tot.value == int(ns.sum()) and np.array_equal(buf, rec)
+
+
+def _dynamic_symbols(path, defined=True):
+    out = subprocess.run(["nm", "-D", "--defined-only" if defined else "--undefined-only", path],
+                         capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_plugin_library_exports_the_plugin_abi():
+    """libgpu_parse_filter_plugin.so: createPlugin (what PluginManager::loadPlugin dlsyms,
+    /root/reference/src/PluginManager.cpp:67-68) and every C hook its header declares; linked
+    -z nodelete (~PluginManager dlcloses before destroying plugins, :26-34); and the only
+    reference symbol it takes from the host process is Packet's out-of-line constructor."""
+    so = os.path.join(ROOT, "beatrice_amd", "libgpu_parse_filter_plugin.so")
+    assert os.path.exists(so), "plugin not built"
+    hdr = open(os.path.join(ROOT, "include", "beatrice_gpu_plugin.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    hooks = set(re.findall(r"\b(gpu_(?:plugin|batch)_[a-z_]+)\s*\(", hdr))
+    assert {"gpu_plugin_set_sink", "gpu_plugin_flush", "gpu_batch_layers", "gpu_batch_format"} <= hooks
+    defined = _dynamic_symbols(so)
+    assert "createPlugin" in defined
+    assert hooks <= defined, hooks - defined
+    dyn = subprocess.run(["readelf", "-d", so], capture_output=True, text=True, check=True).stdout
+    assert "NODELETE" in dyn
+    undefined = {s for s in _dynamic_symbols(so, defined=False) if "8beatrice" in s and "3gpu" not in s}
+    assert undefined <= {"_ZN8beatrice6PacketC1ESt10shared_ptrIA_KhEmNSt6chrono10time_pointINS5_3_V212steady_clock"
+                         "ENS5_8durationIlSt5ratioILl1ELl1000000000EEEEEE"}, undefined
