@@ -574,6 +574,22 @@ int ensure_host(bt_ctx* c) {
     return BT_OK;
 }
 
+// The host pipeline's parallel steps for a chunk of `cnt` packets: on the pool, or for small
+// chunks on the calling thread (every w in turn), where waking the pool cost more than the
+// work (a 1k-packet classify took ~0.1 ms per call).
+template <class Fn>
+void pipeline_run(bt_ctx* c, uint32_t cnt, Fn&& fn) {
+    static const uint32_t below = [] {
+        const char* e = getenv("BT_HOST_INLINE_BELOW");   // A/B knob, 0 = always the pool
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 8192u;
+    }();
+    if (cnt < below) {
+        for (unsigned w = 0, T = c->pool->size(); w < T; ++w) fn(w);
+    } else {
+        c->pool->run(fn);
+    }
+}
+
 // Copies one finished chunk from pinned staging into the caller's buffers.
 void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint8_t* decide) {
     const uint32_t chunk = c->chunk;
@@ -582,7 +598,7 @@ void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint
     const uint64_t* ver = reinterpret_cast<const uint64_t*>(dec + chunk);
     const unsigned T = c->pool->size();
     const uint32_t lo = s.lo, cnt = s.cnt;
-    c->pool->run([&](unsigned w) {   // split on 64-packet boundaries
+    pipeline_run(c, cnt, [&](unsigned w) {   // split on 64-packet boundaries
         const uint32_t tiles = (cnt + 63) / 64;
         const uint32_t t0 = (uint32_t)((uint64_t)tiles * w / T), t1 = (uint32_t)((uint64_t)tiles * (w + 1) / T);
         const uint32_t a = t0 * 64, b = std::min(cnt, t1 * 64);
@@ -1012,7 +1028,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
             const unsigned T = c->pool->size();
             std::vector<uint64_t> part(T + 1, 0);
             const uint32_t base_i = next;
-            c->pool->run([&](unsigned w) {
+            pipeline_run(c, cnt, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t sum = 0;
                 for (uint32_t i = a; i < b; ++i) {
@@ -1023,7 +1039,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 part[w + 1] = sum;
             });
             for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
-            c->pool->run([&](unsigned w) {
+            pipeline_run(c, cnt, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t p = part[w];
                 for (uint32_t i = a; i < b; ++i) {
