@@ -488,6 +488,7 @@ int main(int argc, char** argv) {
         if (what == "all" || what == "sizes") bench_call_sizes(c, seconds);
         if (what == "all" || what == "plugin") {
             bench_plugin(c, 1, seconds, so);
+            if (threads >= 4) bench_plugin(c, threads / 2, seconds, so);   // producers leave CPUs to the plugin
             bench_plugin(c, threads, seconds, so);
         }
     }
