@@ -558,7 +558,11 @@ size_t out_bytes(uint32_t chunk) { return (size_t)chunk * BT_REC_BYTES + chunk +
 int ensure_host(bt_ctx* c) {
     if (c->host_ready) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
-    uint32_t chunk = c->opts.host_chunk_packets ? c->opts.host_chunk_packets : (1u << 20);
+    static const uint32_t default_chunk = [] {   // BT_HOST_CHUNK: A/B knob for the default
+        const char* e = getenv("BT_HOST_CHUNK");
+        return e && atoi(e) >= 64 ? (uint32_t)atoi(e) : (1u << 20);
+    }();
+    uint32_t chunk = c->opts.host_chunk_packets ? c->opts.host_chunk_packets : default_chunk;
     chunk = (chunk + 63) / 64 * 64;
     c->chunk = chunk;
     (void)pool_of(c);
