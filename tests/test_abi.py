@@ -10,6 +10,7 @@ import pytest
 from beatrice_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BT_E_INVALID_ARGUMENT = 1   # include/beatrice_gpu.h (beatrice::ErrorCode::INVALID_ARGUMENT)
 HEADER = os.path.join(ROOT, "include", "beatrice_gpu.h")
 
 
@@ -112,3 +113,12 @@ def test_plugin_library_exports_the_plugin_abi():
     undefined = {s for s in _dynamic_symbols(so, defined=False) if "8beatrice" in s and "3gpu" not in s}
     assert undefined <= {"_ZN8beatrice6PacketC1ESt10shared_ptrIA_KhEmNSt6chrono10time_pointINS5_3_V212steady_clock"
                          "ENS5_8durationIlSt5ratioILl1ELl1000000000EEEEEE"}, undefined
+
+
+def test_host_stage_bytes_refuses_null_arguments():
+    """bt_host_stage_bytes (no GPU needed to refuse): a null context or output is
+    BT_E_INVALID_ARGUMENT, as every entry point of the C-ABI."""
+    b = ctypes.c_uint32(7)
+    assert abi.lib().bt_host_stage_bytes(None, 0, ctypes.byref(b)) == BT_E_INVALID_ARGUMENT
+    assert abi.lib().bt_host_stage_bytes(None, 1, None) == BT_E_INVALID_ARGUMENT
+    assert b.value == 7
