@@ -150,11 +150,13 @@ EXPORTS = [
     "bt_synchronize", "bt_host_parallel", "bt_stream_create", "bt_stream_synchronize", "bt_stream_destroy", "bt_time_device", "bt_time_device_ex", "bt_time_device2", "bt_proto_span", "bt_extract_device", "bt_extract", "bt_time_extract_ex", "bt_time_extract2", "bt_record_gather", "bt_record_gather_planes",
     "bt_ring_walk_tpv3", "bt_ring_release_tpv3", "bt_ring_walk_tpv3_gpu",
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
-    "bt_format_records",
+    "bt_format_records", "bt_format_records_to",
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3", "bt_ring_gather_dense_tpv3",
     "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
 ]
+
+DEST_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)   # bt_format_records_to's dest
 
 _lib = None
 
@@ -224,6 +226,7 @@ def lib() -> ctypes.CDLL:
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
         "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
         "bt_format_records": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, ctypes.POINTER(u64), vp]),
+        "bt_format_records_to": (ctypes.c_int, [vp, vp, u32, u32, DEST_FN, vp, ctypes.POINTER(u64), vp]),
         "bt_record_unpack": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, ctypes.POINTER(u64)]),
         "bt_record_slabs": (u32, [vp]),
         "bt_group_create": (ctypes.c_int, [vp, u32, ctypes.POINTER(Opts), ctypes.POINTER(vp)]),
@@ -274,6 +277,22 @@ def compile_host(filters):
 
 
 FMT_JSON, FMT_XML, FMT_CSV, FMT_HUMAN = range(4)
+
+
+def format_records_once(records: np.ndarray, fmt: int = FMT_JSON, ctx: "Context | None" = None) -> bytes:
+    """bt_format_records_to: the same text as format_records, formatted once."""
+    recs = np.ascontiguousarray(records).view(np.uint8).reshape(-1, 96)
+    held = {}
+
+    def dest(_user, nbytes):
+        held["buf"] = np.empty(max(1, nbytes), np.uint8)
+        return held["buf"].ctypes.data
+
+    cb = DEST_FN(dest)
+    need = ctypes.c_uint64(0)
+    _check(lib().bt_format_records_to(ctx.h if ctx is not None else None, recs.ctypes.data, len(recs), fmt, cb,
+                                      None, ctypes.byref(need), None))
+    return held["buf"][:need.value].tobytes() if "buf" in held else b""
 
 
 def format_records(records: np.ndarray, fmt: int = FMT_JSON, ctx: "Context | None" = None,

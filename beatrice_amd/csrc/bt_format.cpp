@@ -283,20 +283,26 @@ void format_layer(const bt_rec& r, const Layer& L, uint32_t fmt, Out& o) {
 
 using namespace bt;
 
-extern "C" int bt_format_records(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format, char* out,
-                                 uint64_t cap, uint64_t* out_len, uint64_t* pkt_off) {
-    if ((!recs && n) || !out_len || format > BT_FMT_HUMAN)
-        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records: null argument or unknown format %u", format);
+namespace {
+
+// Formats records [0, n) into at most 64 slices on packet boundaries (each worker its own
+// slices, in its own buffer); base[s] = slice s's offset in the whole text, base[n_slices] =
+// its size; pkt_off (n + 1 entries) each packet's offset.
+struct Formatted {
+    std::vector<Out> parts;
+    std::vector<uint64_t> base;
+};
+
+Formatted format_slices(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format, uint64_t* pkt_off) {
     std::call_once(g_order_once, init_orders);
-    // split into at most 64 slices on packet boundaries; each worker formats its slices
-    // into its own buffer, then the slices are placed by a prefix over their sizes
     const uint32_t n_slices = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + 4095) / 4096));
-    std::vector<Out> parts(n_slices);
+    Formatted f;
+    f.parts.resize(n_slices);
     std::vector<std::vector<uint64_t>> offs(pkt_off ? n_slices : 0);
     host_parallel(ctx, [&](unsigned w, unsigned T) {
         for (uint32_t s = w; s < n_slices; s += T) {
             const uint32_t lo = (uint32_t)((uint64_t)n * s / n_slices), hi = (uint32_t)((uint64_t)n * (s + 1) / n_slices);
-            Out& o = parts[s];
+            Out& o = f.parts[s];
             o.s.reserve((size_t)(hi - lo) * (format == BT_FMT_CSV ? 400 : 1200));
             if (pkt_off) offs[s].resize(hi - lo);
             Layer L[8];
@@ -307,22 +313,52 @@ extern "C" int bt_format_records(bt_ctx* ctx, const bt_rec* recs, uint32_t n, ui
             }
         }
     });
-    std::vector<uint64_t> base(n_slices + 1, 0);
-    for (uint32_t s = 0; s < n_slices; ++s) base[s + 1] = base[s] + parts[s].s.size();
-    *out_len = base[n_slices];
+    f.base.assign(n_slices + 1, 0);
+    for (uint32_t s = 0; s < n_slices; ++s) f.base[s + 1] = f.base[s] + f.parts[s].s.size();
     if (pkt_off) {
         for (uint32_t s = 0; s < n_slices; ++s) {
             const uint32_t lo = (uint32_t)((uint64_t)n * s / n_slices);
-            for (size_t j = 0; j < offs[s].size(); ++j) pkt_off[lo + j] = base[s] + offs[s][j];
+            for (size_t j = 0; j < offs[s].size(); ++j) pkt_off[lo + j] = f.base[s] + offs[s][j];
         }
-        pkt_off[n] = base[n_slices];
+        pkt_off[n] = f.base[n_slices];
     }
-    if (!out) return BT_OK;   // size query
-    if (cap < base[n_slices])
-        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records: %llu bytes needed, buffer holds %llu",
-                         (unsigned long long)base[n_slices], (unsigned long long)cap);
+    return f;
+}
+
+void place(bt_ctx* ctx, const Formatted& f, char* out) {
+    const uint32_t n_slices = (uint32_t)f.parts.size();
     host_parallel(ctx, [&](unsigned w, unsigned T) {
-        for (uint32_t s = w; s < n_slices; s += T) std::memcpy(out + base[s], parts[s].s.data(), parts[s].s.size());
+        for (uint32_t s = w; s < n_slices; s += T) std::memcpy(out + f.base[s], f.parts[s].s.data(), f.parts[s].s.size());
     });
+}
+
+}  // namespace
+
+extern "C" int bt_format_records(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format, char* out,
+                                 uint64_t cap, uint64_t* out_len, uint64_t* pkt_off) {
+    if ((!recs && n) || !out_len || format > BT_FMT_HUMAN)
+        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records: null argument or unknown format %u", format);
+    const Formatted f = format_slices(ctx, recs, n, format, pkt_off);
+    *out_len = f.base.back();
+    if (!out) return BT_OK;   // size query
+    if (cap < f.base.back())
+        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records: %llu bytes needed, buffer holds %llu",
+                         (unsigned long long)f.base.back(), (unsigned long long)cap);
+    place(ctx, f, out);
+    return BT_OK;
+}
+
+extern "C" int bt_format_records_to(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format,
+                                    char* (*dest)(void* user, uint64_t bytes), void* user, uint64_t* out_len,
+                                    uint64_t* pkt_off) {
+    if ((!recs && n) || !out_len || !dest || format > BT_FMT_HUMAN)
+        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records_to: null argument or unknown format %u", format);
+    const Formatted f = format_slices(ctx, recs, n, format, pkt_off);
+    *out_len = f.base.back();
+    char* out = dest(user, f.base.back());
+    if (!out && f.base.back())
+        return set_error(BT_E_INVALID_ARGUMENT, "bt_format_records_to: no destination for %llu bytes",
+                         (unsigned long long)f.base.back());
+    if (out) place(ctx, f, out);
     return BT_OK;
 }

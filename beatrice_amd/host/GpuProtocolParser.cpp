@@ -249,12 +249,16 @@ std::vector<GpuParsedBatch::DetectionResult> GpuParsedBatch::detectMultiple(size
 
 namespace {
 std::string format_recs(bt_ctx* ctx, const bt_rec* r, uint32_t n, uint32_t fmt) {
+    // formatted once (bt_format_records_to), placed straight into the string
+    std::string s;
     uint64_t need = 0;
-    if (bt_format_records(ctx, r, n, fmt, nullptr, 0, &need, nullptr) != BT_OK)
+    auto dest = [](void* user, uint64_t bytes) -> char* {
+        auto* str = static_cast<std::string*>(user);
+        str->resize(bytes);
+        return bytes ? &(*str)[0] : nullptr;
+    };
+    if (bt_format_records_to(ctx, r, n, fmt, dest, &s, &need, nullptr) != BT_OK)
         throw std::invalid_argument(std::string("GpuParsedBatch::format: ") + bt_last_error());
-    std::string s(need, '\0');
-    if (need && bt_format_records(ctx, r, n, fmt, &s[0], need, &need, nullptr) != BT_OK)
-        throw std::runtime_error(std::string("GpuParsedBatch::format: ") + bt_last_error());
     return s;
 }
 }  // namespace

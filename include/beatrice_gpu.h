@@ -655,6 +655,12 @@ int  bt_time_extract2(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fi
 #define BT_FMT_HUMAN 3u   /* ParseResult::toHumanReadableString (:315-349) */
 int  bt_format_records(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format, char* out, uint64_t cap,
                        uint64_t* out_len, uint64_t* pkt_off);
+/* The same text in one pass: the records are formatted once, then dest(user, bytes) is called
+ * once with the exact size and returns where to put it (NULL only when bytes == 0); the
+ * size query plus the call above format everything twice. */
+int  bt_format_records_to(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t format,
+                          char* (*dest)(void* user, uint64_t bytes), void* user, uint64_t* out_len,
+                          uint64_t* pkt_off);
 
 /* host-side record gather from the device layout (after a D2H copy) */
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out);

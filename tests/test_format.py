@@ -31,6 +31,19 @@ def test_format_matches_reference(cap, fmt):
     assert ours == want, _first_diff(ours, want)
 
 
+@needs_ref
+@pytest.mark.parametrize("fmt", list(FORMATS))
+def test_single_pass_format_matches_reference(fmt):
+    """bt_format_records_to (formatted once, placed where the caller's dest says) prints
+    exactly the reference's text too; no records: dest gets 0 bytes."""
+    g, _ = load_golden("fuzz")
+    n = min(len(g["desc"]), 3000)
+    ours = abi.format_records_once(g["rec"][:n], FORMATS[fmt])
+    want = ol.ref_format(g["data"], g["desc"], n, FORMATS[fmt])
+    assert ours == want, _first_diff(ours, want)
+    assert abi.format_records_once(g["rec"][:0], FORMATS[fmt]) == b""
+
+
 def test_format_offsets_and_sizes():
     g, _ = load_golden("c4")
     rec = g["rec"][:500]
