@@ -1,0 +1,116 @@
+// bt_host_pool.h — the context's host thread pool (beatrice_amd/csrc/bt_runtime.cpp), in a
+// header of its own so tests/cpp/test_host_pool.cpp can stress it under ThreadSanitizer on the
+// CPU. Host code only.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace bt {
+
+// Fixed pool of host threads for the host-batch pipeline's gather / drain copies.
+// run(fn) executes fn(0) .. fn(T-1) once each, T = size(): the caller and whichever workers
+// wake claim the indices from one counter, and the caller waits only for the indices already
+// claimed. On a host whose CPUs are all busy (callers on every CPU, the plugin's onPacket
+// threads) a worker may not be scheduled for a whole time slice; waiting for every worker to
+// take its fixed share made each run as slow as the latest one to wake (0.45 ms per device
+// pass of a 12k-packet batch), whereas here the caller does the unclaimed work.
+class HostPool {
+public:
+    explicit HostPool(unsigned n) {
+        nthreads_ = n ? n : 1;
+        static const bool fixed = getenv("BT_POOL_FIXED") != nullptr;   // A/B: each worker its own index
+        fixed_ = fixed;
+        for (unsigned i = 1; i < nthreads_; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned size() const { return nthreads_; }
+    // runs fn(k) for every k in [0, size()) and waits
+    void run(const std::function<void(unsigned)>& fn) {
+        if (nthreads_ == 1) { fn(0); return; }
+        std::lock_guard<std::mutex> one_at_a_time(run_mu_);   // callers on several threads
+        uint32_t g;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            g = (uint32_t)++gen_;
+            finished_ = 0;
+            claim_.store((uint64_t)g << 32, std::memory_order_release);
+        }
+        cv_.notify_all();
+        if (fixed_) {
+            fn(0);
+            std::lock_guard<std::mutex> lk(m_);
+            ++finished_;
+        } else {
+            execute(g, fn);
+        }
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return finished_ == nthreads_; });
+        fn_ = nullptr;
+    }
+
+private:
+    // claims indices of run g (the generation in the counter's high half keeps a late
+    // worker from claiming in a later run with an earlier run's function) and runs them
+    void execute(uint32_t g, const std::function<void(unsigned)>& fn) {
+        for (;;) {
+            uint64_t c = claim_.load(std::memory_order_acquire);
+            for (;;) {
+                if ((uint32_t)(c >> 32) != g || (uint32_t)c >= nthreads_) return;
+                if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) break;
+            }
+            fn((unsigned)(uint32_t)c);
+            std::lock_guard<std::mutex> lk(m_);
+            if (++finished_ == nthreads_) done_.notify_one();
+        }
+    }
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            uint32_t g;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = fn_;   // null when that run has already finished
+                g = (uint32_t)gen_;
+            }
+            if (!f) continue;
+            if (fixed_) {   // round 2's pool: worker id runs index id, the caller waits for all
+                (*f)(id);
+                std::lock_guard<std::mutex> lk(m_);
+                if (++finished_ == nthreads_) done_.notify_one();
+            } else {
+                execute(g, *f);
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
+    unsigned finished_ = 0, nthreads_ = 1;
+    bool fixed_ = false;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace bt
