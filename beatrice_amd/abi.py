@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BT_LIB_PATH") or os.path.join(HERE, "libbeatrice_gpu.so")
 
 BT_REC_BYTES = 96
+ABI_VERSION = 2     # include/beatrice_gpu.h BT_ABI_VERSION this binding is written against
 BT_MAX_FILTERS = 64
 
 # FilterType order (reference include/beatrice/PacketFilter.hpp:17-24)
@@ -136,6 +137,24 @@ def proto_span(fields) -> int:
     return span.value
 
 
+class SplitCost(ctypes.Structure):
+    """bt_split_cost: packet cost = round_up(min(len, window), align) + fixed."""
+    _fields_ = [("window", ctypes.c_uint32), ("align", ctypes.c_uint32), ("fixed", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+    def as_tuple(self):
+        return (self.window, self.align, self.fixed)
+
+
+class Placement(ctypes.Structure):
+    """bt_placement: where a context's host work runs (bt_context_placement)."""
+    _fields_ = [("numa_node", ctypes.c_int32), ("pinned_cpus", ctypes.c_uint32), ("pool_threads", ctypes.c_uint32),
+                ("staging_node", ctypes.c_int32), ("reserved", ctypes.c_uint32 * 4)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
 class Tpv3Ring(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("block_size", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32)]
@@ -154,6 +173,9 @@ EXPORTS = [
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3", "bt_ring_gather_dense_tpv3",
     "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
+    "bt_group_split_cost", "bt_group_cost", "bt_group_thread_budget", "bt_group_host_register",
+    "bt_group_host_unregister", "bt_group_parse_filter_mapped", "bt_context_placement", "bt_node_cpus",
+    "bt_usable_cpus", "bt_extract_host", "bt_filter_dfa_pool",
 ]
 
 DEST_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)   # bt_format_records_to's dest
@@ -207,6 +229,8 @@ def lib() -> ctypes.CDLL:
         "bt_proto_span": (ctypes.c_int, [vp, u32, ctypes.POINTER(u64)]),
         "bt_extract_device": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), vp]),
         "bt_extract": (ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, vp]),
+        "bt_extract_host": (ctypes.c_int, [vp, vp, u32, vp, u32, vp, vp, vp]),
+        "bt_filter_dfa_pool": (ctypes.c_int, [vp, vp, u32, ctypes.POINTER(u32)]),
         "bt_time_extract_ex": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), u32,
                                               ctypes.POINTER(Timing)]),
         "bt_time_extract2": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, u32, ctypes.POINTER(ExtractOut), u32, u32,
@@ -237,6 +261,15 @@ def lib() -> ctypes.CDLL:
         "bt_group_parse_filter": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_group_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_group_split": (ctypes.c_int, [vp, u32, u32, vp]),
+        "bt_group_split_cost": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(SplitCost), vp]),
+        "bt_group_cost": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, ctypes.POINTER(SplitCost)]),
+        "bt_group_thread_budget": (ctypes.c_int, [u32, u32, u32, ctypes.POINTER(u32)]),
+        "bt_group_host_register": (ctypes.c_int, [vp, vp, u64]),
+        "bt_group_host_unregister": (ctypes.c_int, [vp, vp]),
+        "bt_group_parse_filter_mapped": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.POINTER(Outputs)]),
+        "bt_context_placement": (ctypes.c_int, [vp, ctypes.POINTER(Placement)]),
+        "bt_node_cpus": (ctypes.c_int, [ctypes.c_int, vp, u32, ctypes.POINTER(u32)]),
+        "bt_usable_cpus": (u32, []),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):   # an older build under BT_LIB_PATH (A/B runs); tests check EXPORTS
@@ -245,6 +278,13 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _ = i32
+    have = L.bt_abi_version()
+    if have < ABI_VERSION:
+        msg = f"{LIB_PATH}: C-ABI version {have}, this binding needs {ABI_VERSION} (rebuild the library)"
+        if not os.environ.get("BT_LIB_PATH"):
+            raise RuntimeError(msg)
+        import sys   # an older build under BT_LIB_PATH (A/B runs): what it lacks fails when called
+        print(f"beatrice_amd.abi: warning: {msg}", file=sys.stderr)
     _lib = L
     return L
 
@@ -404,6 +444,12 @@ class Context:
     def reserve(self, n: int):
         _check(lib().bt_reserve(self.h, n))
 
+    def placement(self) -> dict:
+        """bt_context_placement: NUMA node, pinned CPUs, pool size, staging node."""
+        p = Placement()
+        _check(lib().bt_context_placement(self.h, ctypes.byref(p)))
+        return p.as_dict()
+
     def register(self, arr: np.ndarray) -> int:
         """Page-lock + map a host array (zero-copy); returns its device alias."""
         p = ctypes.c_void_p(0)
@@ -494,12 +540,37 @@ class Context:
         return out
 
 
-def group_split(lens: np.ndarray, parts: int) -> list[tuple[int, int]]:
-    """bt_group_split (host only): the members' [lo, hi) packet ranges."""
+def group_split(lens: np.ndarray, parts: int, cost=None) -> list[tuple[int, int]]:
+    """bt_group_split (host only): the members' [lo, hi) packet ranges; cost = (window,
+    align, fixed) selects bt_group_split_cost."""
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     b = np.zeros(parts + 1, np.uint32)
-    _check(lib().bt_group_split(lens.ctypes.data if len(lens) else None, len(lens), parts, b.ctypes.data))
+    lp = lens.ctypes.data if len(lens) else None
+    if cost is None:
+        _check(lib().bt_group_split(lp, len(lens), parts, b.ctypes.data))
+    else:
+        c = SplitCost(*[int(x) for x in cost], 0)
+        _check(lib().bt_group_split_cost(lp, len(lens), parts, ctypes.byref(c), b.ctypes.data))
     return [(int(b[k]), int(b[k + 1])) for k in range(parts)]
+
+
+def group_thread_budget(members: int, usable: int, requested: int = 0) -> int:
+    """bt_group_thread_budget (host only): host threads per member."""
+    out = ctypes.c_uint32(0)
+    _check(lib().bt_group_thread_budget(members, usable, requested, ctypes.byref(out)))
+    return out.value
+
+
+def node_cpus(node: int) -> list[int]:
+    """bt_node_cpus (host only): the CPUs of NUMA node `node` in this process's affinity set."""
+    cpus = (ctypes.c_int32 * 4096)()
+    n = ctypes.c_uint32(0)
+    _check(lib().bt_node_cpus(node, cpus, 4096, ctypes.byref(n)))
+    return [cpus[i] for i in range(min(n.value, 4096))]
+
+
+def usable_cpus() -> int:
+    return int(lib().bt_usable_cpus())
 
 
 class Group:
@@ -529,6 +600,31 @@ class Group:
 
     def size(self) -> int:
         return int(lib().bt_group_size(self.h))
+
+    def member(self, k: int) -> int:
+        return lib().bt_group_member(self.h, k)
+
+    def placement(self, k: int) -> dict:
+        p = Placement()
+        _check(lib().bt_context_placement(self.member(k), ctypes.byref(p)))
+        return p.as_dict()
+
+    def cost(self, mapped: bool, records: bool, filters: bool, desc_bytes: int = 8):
+        """bt_group_cost: the (window, align, fixed) model a call splits its batch by."""
+        c = SplitCost()
+        _check(lib().bt_group_cost(self.h, int(mapped), int(records), int(filters), desc_bytes, ctypes.byref(c)))
+        return c.as_tuple()
+
+    def register(self, arr: np.ndarray):
+        """bt_group_host_register: page-lock + map a host array into every member's device."""
+        _check(lib().bt_group_host_register(self.h, arr.ctypes.data, arr.nbytes))
+
+    def unregister(self, arr: np.ndarray):
+        _check(lib().bt_group_host_unregister(self.h, arr.ctypes.data))
+
+    def run_mapped(self, batch: Batch, outs: Outputs):
+        """bt_group_parse_filter_mapped: batch / outputs as host addresses in registered ranges."""
+        _check(lib().bt_group_parse_filter_mapped(self.h, ctypes.byref(batch), ctypes.byref(outs)))
 
     def compile(self, filters):
         arr = filter_descs(filters)

@@ -3,140 +3,214 @@
 // The reference daemon is one process whose capture threads feed one plugin set
 // (/root/reference/src/BeatriceContext.cpp:215-278, src/PluginManager.cpp:158-188); a
 // deployed stage there must be able to use every GPU of the node without a launcher. A
-// group is one bt_ctx per device (its own streams, pinned staging and host pool); the
-// filter program is compiled once on the host and installed on every member; a batch
-// is split into contiguous, 64-packet-aligned ranges balanced by the bytes each packet
-// costs to stage (bt_group_split, the C++ form of beatrice_amd/shard.py:shard_bounds),
-// each member runs its range on its own host thread, and the results land straight in
-// the caller's arrays: records, decisions and verdict words at the range's offset (the
-// ranges start on tile boundaries, so verdict words concatenate without shifts), pass
-// indices offset by the range start and concatenated in order. There is no collective:
-// packets are independent.
+// group is one bt_ctx per device (its own streams, pinned staging and host pool, placed on
+// its device's NUMA node); the filter program is compiled once on the host and installed on
+// every member; a batch is split into contiguous, 64-packet-aligned ranges balanced by what
+// each packet costs the call (bt_group_cost: the bytes it stages, or reads over PCIe), each
+// member runs its range on its own host thread, and the results land straight in the
+// caller's arrays: records, decisions and verdict words at the range's offset (the ranges
+// start on tile boundaries, so verdict words concatenate without shifts), pass indices in
+// ascending order. There is no collective: packets are independent.
+//
+// Two ingest forms: host batches (frames anywhere in host memory, gathered by each member's
+// host pool into its pinned staging) and mapped batches (bt_group_parse_filter_mapped: the
+// frames sit in group-registered host memory — a UMEM, a TPACKET_V3 ring — and each member's
+// kernels read its range in place over its own PCIe link, the only ingest that is not
+// bounded by the host's CPUs).
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+
 #include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
-
-#include <condition_variable>
-#include <functional>
 
 #include "bt_host.h"
 
 namespace {
 
-// One thread per member after the first, kept for the group's life: member k's part of a batch
-// runs on thread k (member 0 on the caller), so a batch costs no thread creation (a plugin's
-// 64k-packet batches over 8 devices had spawned 7 threads per batch).
+constexpr uint32_t kTile = 64;
+constexpr uint32_t kMaxPool = 16;   // a context's host pool has at most 16 workers
+
+// One worker thread per member after the first, kept for the group's life, each with its own
+// FIFO of calls: member k's part of a call runs on thread k (member 0's on the caller), so a
+// call creates no thread, and calls from several threads queue per member instead of waiting
+// for each other's whole batch (each member still runs one call at a time: its context
+// serialises them).
 class MemberThreads {
 public:
-    explicit MemberThreads(uint32_t members) {
-        for (uint32_t k = 1; k < members; ++k) th_.emplace_back([this, k] { loop(k); });
+    MemberThreads(uint32_t members, const std::vector<const cpu_set_t*>& pins) : q_(members) {
+        for (uint32_t k = 1; k < members; ++k) {
+            if (pins[k]) {
+                q_[k].pin = *pins[k];
+                q_[k].pinned = true;
+            }
+            q_[k].th = std::thread([this, k] { loop(k); });
+        }
     }
     ~MemberThreads() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-            ++gen_;
+        for (size_t k = 1; k < q_.size(); ++k) {
+            {
+                std::lock_guard<std::mutex> lk(q_[k].m);
+                q_[k].stop = true;
+            }
+            q_[k].cv.notify_one();
+            q_[k].th.join();
         }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
     }
-    // fn(k) for every member k, concurrently; returns when all have
+    // fn(k) for every member k, concurrently; returns when all have. fn must not throw.
     void run(const std::function<void(uint32_t)>& fn) {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            fn_ = &fn;
-            pending_ = (uint32_t)th_.size();
-            ++gen_;
+        Call call;
+        call.fn = &fn;
+        call.pending = (uint32_t)q_.size() - 1;
+        for (size_t k = 1; k < q_.size(); ++k) {
+            {
+                std::lock_guard<std::mutex> lk(q_[k].m);
+                q_[k].jobs.push_back(&call);
+            }
+            q_[k].cv.notify_one();
         }
-        cv_.notify_all();
         fn(0);
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [this] { return pending_ == 0; });
-        fn_ = nullptr;
+        std::unique_lock<std::mutex> lk(call.m);
+        call.cv.wait(lk, [&] { return call.pending == 0; });
     }
 
 private:
+    struct Call {
+        const std::function<void(uint32_t)>* fn = nullptr;
+        std::mutex m;
+        std::condition_variable cv;
+        uint32_t pending = 0;
+    };
+    struct Queue {
+        std::mutex m;
+        std::condition_variable cv;
+        std::deque<Call*> jobs;
+        bool stop = false;
+        bool pinned = false;
+        cpu_set_t pin{};
+        std::thread th;
+    };
     void loop(uint32_t k) {
-        uint64_t seen = 0;
+        Queue& q = q_[k];
+        if (q.pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(q.pin), &q.pin);
         for (;;) {
-            const std::function<void(uint32_t)>* f;
+            Call* c;
             {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (stop_) return;
-                f = fn_;
+                std::unique_lock<std::mutex> lk(q.m);
+                q.cv.wait(lk, [&] { return q.stop || !q.jobs.empty(); });
+                if (q.jobs.empty()) return;   // stop, and nothing left
+                c = q.jobs.front();
+                q.jobs.pop_front();
             }
-            (*f)(k);
-            std::lock_guard<std::mutex> lk(m_);
-            if (--pending_ == 0) done_.notify_one();
+            (*c->fn)(k);
+            std::lock_guard<std::mutex> lk(c->m);
+            if (--c->pending == 0) c->cv.notify_one();
         }
     }
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(uint32_t)>* fn_ = nullptr;
-    uint32_t pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::vector<Queue> q_;
+};
+
+// A host range registered with every member (bt_group_host_register).
+struct Region {
+    uint8_t* host = nullptr;
+    uint64_t bytes = 0;
+    std::vector<uint8_t*> dev;   // member k's alias
 };
 
 }  // namespace
 
 struct bt_group {
     std::vector<bt_ctx*> members;
-    std::mutex mu;   // one batch at a time (each member serialises its own calls anyway)
+    std::shared_mutex prog_mu;   // exclusive: bt_group_filter_compile; shared: batches (every member
+                                 // of one batch runs the same program)
     std::unique_ptr<MemberThreads> threads;   // members > 1
+    std::shared_mutex reg_mu;    // regions (exclusive: register / unregister)
+    std::vector<Region> regions;
+    // mapped calls that want a pass list but gave no verdict words: the group's own
+    // (registered, grown on demand; one such call at a time)
+    std::mutex scratch_mu;
+    uint64_t* scratch = nullptr;
+    size_t scratch_words = 0;
+    std::vector<uint8_t*> scratch_dev;
 };
 
 namespace {
 
-constexpr uint32_t kTile = 64;
+// packet cost = round_up(min(len, window), align) + fixed
+inline uint64_t packet_cost(uint32_t len, const bt_split_cost& c) {
+    uint64_t w = std::min(len, c.window);
+    if (c.align > 1) w = (w + c.align - 1) / c.align * c.align;
+    return w + c.fixed;
+}
 
-// What one packet costs a member: its staged header prefix (<= 128 B), its descriptor and
-// its 96-B record (shard.py's cost model).
-inline uint64_t packet_cost(uint32_t len) { return (uint64_t)std::min(len, 128u) + 8u + 96u; }
+constexpr bt_split_cost kShardCost{128, 1, 8 + 96, 0};   // beatrice_amd/shard.py's default model
 
 struct Range {
     uint32_t lo, hi;
 };
 
-std::vector<Range> split(const uint32_t* lens, uint32_t n, uint32_t parts) {
+std::vector<Range> split(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost& cost) {
     std::vector<uint32_t> b(parts + 1, 0);
-    bt_group_split(lens, n, parts, b.data());
+    bt_group_split_cost(lens, n, parts, &cost, b.data());
     std::vector<Range> r(parts);
     for (uint32_t k = 0; k < parts; ++k) r[k] = {b[k], b[k + 1]};
     return r;
 }
 
 // Runs fn(k) for every member on its own thread; returns the first failure (with its
-// message moved to this thread's bt_last_error).
+// message moved to this thread's bt_last_error). An exception in a member's part (an
+// allocation) becomes BT_E_INTERNAL there: nothing throws across the C-ABI or out of a
+// member thread.
 template <class Fn>
 int run_members(bt_group* g, Fn fn) {
     const uint32_t m = (uint32_t)g->members.size();
-    if (m == 1) return fn(0u);   // one device: no thread
     std::vector<int> rc(m, BT_OK);
     std::vector<std::string> msg(m);
-    g->threads->run([&](uint32_t k) {
-        rc[k] = fn(k);
-        if (rc[k]) msg[k] = bt_last_error();
-    });
+    auto one = [&](uint32_t k) {
+        try {
+            rc[k] = fn(k);
+            if (rc[k]) msg[k] = bt_last_error();
+        } catch (const std::exception& e) {
+            rc[k] = BT_E_INTERNAL;
+            msg[k] = e.what();
+        } catch (...) {
+            rc[k] = BT_E_INTERNAL;
+            msg[k] = "unknown exception";
+        }
+    };
+    if (m == 1) {
+        one(0);   // one device: no thread
+    } else {
+        g->threads->run(one);
+    }
     for (uint32_t k = 0; k < m; ++k)
-        if (rc[k]) return bt::set_error(rc[k], "group member %u (device %d): %s", k, bt::ctx_device(g->members[k]),
-                                        msg[k].c_str());
+        if (rc[k]) {
+            if (m == 1) return bt::set_error(rc[k], "%s", msg[k].c_str());
+            return bt::set_error(rc[k], "group member %u (device %d): %s", k, bt::ctx_device(g->members[k]),
+                                 msg[k].c_str());
+        }
     return BT_OK;
 }
 
-// One host batch over the group: frame(i) gives packet i's bytes and length.
+// One host batch over the group: frames(ctx, lo, cnt, ...) runs packets [lo, lo + cnt).
 template <class Frames>
 int group_batch(bt_group* g, uint32_t n, const uint32_t* lens, Frames frames, bt_rec* records, uint64_t* verdict,
                 uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
     const uint32_t m = (uint32_t)g->members.size();
-    const std::vector<Range> r = split(lens, n, m);
+    const bool want_filter = verdict || decide || pass_idx || n_pass;
+    bt_split_cost cost{};
+    (void)bt_group_cost(g, 0, records != nullptr, want_filter, 8, &cost);
+    const std::vector<Range> r = split(lens, n, m, cost);
     std::vector<std::vector<uint32_t>> pidx(m);
     std::vector<uint32_t> npass(m, 0);
     const bool want_pass = pass_idx || n_pass;
@@ -159,12 +233,76 @@ int group_batch(bt_group* g, uint32_t n, const uint32_t* lens, Frames frames, bt
     return BT_OK;
 }
 
+// Member k's alias of host range [p, p + need) (group-registered); nullptr if none.
+uint8_t* alias_of(const bt_group* g, uint32_t k, const void* p, uint64_t need) {
+    const uint8_t* a = static_cast<const uint8_t*>(p);
+    for (const Region& r : g->regions)
+        if (a >= r.host && a < r.host + r.bytes) {
+            if ((uint64_t)(a - r.host) + need > r.bytes) return nullptr;
+            return r.dev[k] + (a - r.host);
+        }
+    return nullptr;
+}
+
+int alias_all(bt_group* g, void* host, std::vector<uint8_t*>* dev) {
+    const uint32_t m = (uint32_t)g->members.size();
+    dev->assign(m, nullptr);
+    for (uint32_t k = 0; k < m; ++k) {
+        void* d = nullptr;
+        if (hipSetDevice(bt::ctx_device(g->members[k])) != hipSuccess ||
+            hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+            const hipError_t e = hipGetLastError();
+            return bt::set_error(BT_E_INTERNAL, "hipHostGetDevicePointer on member %u (device %d): %s", k,
+                                 bt::ctx_device(g->members[k]), hipGetErrorString(e));
+        }
+        (*dev)[k] = static_cast<uint8_t*>(d);
+    }
+    return BT_OK;
+}
+
+// Every member's device has finished what it queued (before a registered range goes away).
+int sync_devices(bt_group* g) {
+    std::vector<int> done;
+    for (bt_ctx* c : g->members) {
+        const int d = bt::ctx_device(c);
+        if (std::find(done.begin(), done.end(), d) != done.end()) continue;
+        done.push_back(d);
+        if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return bt::set_error(BT_E_INTERNAL, "device %d: %s", d, hipGetErrorString(hipGetLastError()));
+    }
+    return BT_OK;
+}
+
+// Indices of the set bits of verdict words [w0, w1) whose packet index is < n, written
+// ascending from out (out == nullptr: counted only); returns how many.
+uint32_t verdict_bits(const uint64_t* ver, uint32_t w0, uint32_t w1, uint32_t n, uint32_t* out) {
+    uint32_t c = 0;
+    for (uint32_t w = w0; w < w1; ++w) {
+        uint64_t x = ver[w];
+        if ((uint64_t)w * 64 + 64 > n) x &= (n & 63) ? (1ull << (n & 63)) - 1ull : ~0ull;
+        if (!out) {
+            c += (uint32_t)__builtin_popcountll(x);
+            continue;
+        }
+        while (x) {
+            out[c++] = w * 64 + (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+        }
+    }
+    return c;
+}
+
 }  // namespace
 
 extern "C" {
 
 int bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* bounds) {
-    if (!bounds || !parts || (n && !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / zero parts");
+    return bt_group_split_cost(lens, n, parts, &kShardCost, bounds);
+}
+
+int bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
+                        uint32_t* bounds) {
+    if (!bounds || !parts || !cost || (n && !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / zero parts");
     bounds[0] = 0;
     if (parts == 1 || n == 0) {
         for (uint32_t k = 1; k <= parts; ++k) bounds[k] = n;
@@ -177,7 +315,7 @@ int bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* b
     uint64_t run = 0;
     for (uint32_t t = 0; t < ntiles; ++t) {
         const uint32_t e = std::min(n, (t + 1) * kTile);
-        for (uint32_t i = t * kTile; i < e; ++i) run += packet_cost(lens[i]);
+        for (uint32_t i = t * kTile; i < e; ++i) run += packet_cost(lens[i], *cost);
         cum[t] = run;
     }
     const double total = (double)run;
@@ -193,6 +331,14 @@ int bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* b
     return BT_OK;
 }
 
+int bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member) {
+    if (!members || !per_member) return bt::set_error(BT_E_INVALID_ARGUMENT, "zero members / null out");
+    usable = std::max(usable, 1u);
+    if (requested) *per_member = std::min(std::max(requested / members, 1u), 16u);
+    else *per_member = std::min(std::max(usable / members, 1u), 8u);
+    return BT_OK;
+}
+
 int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out) {
     if (!out || !devices || !n_devices) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / no devices");
     *out = nullptr;
@@ -201,10 +347,20 @@ int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts,
             if (devices[i] == devices[j] && !(opts && (opts->flags & BT_OPT_GROUP_SHARED_DEVICE)))
                 return bt::set_error(BT_E_INVALID_ARGUMENT, "device %d listed twice (BT_OPT_GROUP_SHARED_DEVICE "
                                      "allows it, for tests on one GPU)", devices[i]);
+    // one host-thread budget for the whole group, split across the members (an 8-device
+    // group on a 16-CPU host had built 8 pools of 8 threads)
+    bt_opts mo{};
+    if (opts) mo = *opts;
+    uint32_t requested = mo.host_threads;
+    if (!requested) {
+        const char* e = getenv("BT_HOST_THREADS");
+        if (e && atoi(e) > 0) requested = (uint32_t)atoi(e);
+    }
+    (void)bt_group_thread_budget(n_devices, bt::usable_cpus(), requested, &mo.host_threads);
     auto* g = new bt_group();
     for (uint32_t i = 0; i < n_devices; ++i) {
         bt_ctx* c = nullptr;
-        const int rc = bt_create(devices[i], opts, &c);
+        const int rc = bt_create(devices[i], &mo, &c);
         if (rc) {
             const std::string msg = bt_last_error();
             bt_group_destroy(g);
@@ -212,7 +368,16 @@ int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts,
         }
         g->members.push_back(c);
     }
-    if (n_devices > 1) g->threads = std::make_unique<MemberThreads>(n_devices);
+    if (n_devices > 1) {
+        std::vector<const cpu_set_t*> pins;
+        for (bt_ctx* c : g->members) pins.push_back(bt::ctx_pin(c));
+        try {
+            g->threads = std::make_unique<MemberThreads>(n_devices, pins);
+        } catch (const std::exception& e) {
+            bt_group_destroy(g);
+            return bt::set_error(BT_E_RESOURCE, "group threads: %s", e.what());
+        }
+    }
     *out = g;
     return BT_OK;
 }
@@ -220,6 +385,12 @@ int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts,
 void bt_group_destroy(bt_group* g) {
     if (!g) return;
     g->threads.reset();
+    if (!g->regions.empty() || g->scratch) (void)sync_devices(g);
+    for (const Region& r : g->regions) (void)hipHostUnregister(r.host);
+    if (g->scratch) {
+        (void)hipHostUnregister(g->scratch);
+        free(g->scratch);
+    }
     for (bt_ctx* c : g->members) bt_destroy(c);
     delete g;
 }
@@ -232,23 +403,45 @@ bt_ctx* bt_group_member(bt_group* g, uint32_t k) {
 
 int bt_group_filter_compile(bt_group* g, const bt_filter_desc* filters, uint32_t n) {
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
-    std::lock_guard<std::mutex> lk(g->mu);
-    bt::CompiledProgram p;   // compiled once, installed on every device
-    if (int rc = bt::compile_program(filters, n, bt::ctx_flags(g->members[0]), &p)) return rc;
-    return run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
+    try {
+        std::unique_lock<std::shared_mutex> lk(g->prog_mu);
+        bt::CompiledProgram p;   // compiled once, installed on every device
+        if (int rc = bt::compile_program(filters, n, bt::ctx_flags(g->members[0]), &p)) return rc;
+        return run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_filter_compile: %s", e.what());
+    }
+}
+
+int bt_group_cost(bt_group* g, int mapped, int records, int filters, uint32_t desc_bytes, bt_split_cost* out) {
+    if (!g || !out) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
+    *out = bt_split_cost{};
+    out->align = 16;
+    if (mapped) {
+        out->window = records ? 128u : 48u;
+        out->fixed = desc_bytes + (records ? 64u : 0u) + (filters ? 1u : 0u);
+    } else {
+        out->window = bt::stage_bytes_of(g->members[0], records != 0);
+        out->fixed = desc_bytes + (records ? (uint32_t)BT_REC_BYTES : 0u) + (filters ? 1u : 0u);
+    }
+    return BT_OK;
 }
 
 int bt_group_parse_filter(bt_group* g, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n, bt_rec* records,
                           uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
     if (n && (!base || !desc)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
-    std::lock_guard<std::mutex> lk(g->mu);
-    std::vector<uint32_t> lens(n);
-    for (uint32_t i = 0; i < n; ++i) lens[i] = BT_DESC_LEN(desc[i]);
-    return group_batch(g, n, lens.data(),
-                       [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
-                           uint32_t* np) { return bt_parse_filter(c, base, desc + lo, cnt, r, v, d, p, np); },
-                       records, verdict, decide, pass_idx, n_pass);
+    try {
+        std::shared_lock<std::shared_mutex> lk(g->prog_mu);
+        std::vector<uint32_t> lens(n);
+        for (uint32_t i = 0; i < n; ++i) lens[i] = BT_DESC_LEN(desc[i]);
+        return group_batch(g, n, lens.data(),
+                           [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
+                               uint32_t* np) { return bt_parse_filter(c, base, desc + lo, cnt, r, v, d, p, np); },
+                           records, verdict, decide, pass_idx, n_pass);
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_parse_filter: %s", e.what());
+    }
 }
 
 int bt_group_parse_filter_ptrs(bt_group* g, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
@@ -256,11 +449,227 @@ int bt_group_parse_filter_ptrs(bt_group* g, const uint8_t* const* frames, const 
                                uint32_t* n_pass) {
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
     if (n && (!frames || !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
-    std::lock_guard<std::mutex> lk(g->mu);
-    return group_batch(g, n, lens,
-                       [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
-                           uint32_t* np) { return bt_parse_filter_ptrs(c, frames + lo, lens + lo, cnt, r, v, d, p, np); },
-                       records, verdict, decide, pass_idx, n_pass);
+    try {
+        std::shared_lock<std::shared_mutex> lk(g->prog_mu);
+        return group_batch(g, n, lens,
+                           [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
+                               uint32_t* np) { return bt_parse_filter_ptrs(c, frames + lo, lens + lo, cnt, r, v, d, p, np); },
+                           records, verdict, decide, pass_idx, n_pass);
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_parse_filter_ptrs: %s", e.what());
+    }
+}
+
+int bt_group_host_register(bt_group* g, void* host, uint64_t bytes) {
+    if (!g || !host || !bytes) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / empty range");
+    try {
+        std::unique_lock<std::shared_mutex> lk(g->reg_mu);
+        const uint8_t* a = static_cast<const uint8_t*>(host);
+        for (const Region& r : g->regions)
+            if (a < r.host + r.bytes && r.host < a + bytes)
+                return bt::set_error(BT_E_INVALID_ARGUMENT, "range %p + %llu overlaps a registered range", host,
+                                     (unsigned long long)bytes);
+        if (hipSetDevice(bt::ctx_device(g->members[0])) != hipSuccess ||
+            hipHostRegister(host, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess)
+            return bt::set_error(BT_E_INTERNAL, "hipHostRegister: %s", hipGetErrorString(hipGetLastError()));
+        Region r;
+        r.host = static_cast<uint8_t*>(host);
+        r.bytes = bytes;
+        if (int rc = alias_all(g, host, &r.dev)) {
+            (void)hipHostUnregister(host);
+            return rc;
+        }
+        g->regions.push_back(std::move(r));
+        return BT_OK;
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_host_register: %s", e.what());
+    }
+}
+
+int bt_group_host_unregister(bt_group* g, void* host) {
+    if (!g || !host) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
+    std::unique_lock<std::shared_mutex> lk(g->reg_mu);
+    auto it = std::find_if(g->regions.begin(), g->regions.end(), [&](const Region& r) { return r.host == host; });
+    if (it == g->regions.end()) return bt::set_error(BT_E_INVALID_ARGUMENT, "%p is not a registered range", host);
+    // every queued kernel of every member that may read or write the range has finished
+    if (int rc = sync_devices(g)) return rc;
+    if (hipHostUnregister(host) != hipSuccess)
+        return bt::set_error(BT_E_INTERNAL, "hipHostUnregister: %s", hipGetErrorString(hipGetLastError()));
+    g->regions.erase(it);
+    for (bt_ctx* c : g->members) bt::ctx_forget_base(c);   // the address may come back as another kind
+    return BT_OK;
+}
+
+int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_outputs* o) {
+    if (!g || !b || !o) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
+    const uint32_t n = b->n;
+    if (n && !b->base) return bt::set_error(BT_E_INVALID_ARGUMENT, "null packet buffer");
+    if (!b->desc && b->stride == 0 && n) return bt::set_error(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
+    if (b->desc_format > BT_DESC_XDP) return bt::set_error(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
+    if (b->desc && !b->bytes) return bt::set_error(BT_E_INVALID_ARGUMENT, "descriptor batch with bytes == 0");
+    if (o->records && o->n_cap < n) return bt::set_error(BT_E_INVALID_ARGUMENT, "records n_cap %u < n %u", o->n_cap, n);
+    const bool filter = o->verdict || o->decide || o->pass_idx || o->n_pass;
+    const bool want_pass = o->pass_idx || o->n_pass;
+    if (!n || (!filter && !o->records)) {
+        if (o->n_pass) *o->n_pass = 0;
+        return BT_OK;
+    }
+    try {
+        std::shared_lock<std::shared_mutex> plk(g->prog_mu);
+        std::shared_lock<std::shared_mutex> rlk(g->reg_mu);
+        const uint32_t m = (uint32_t)g->members.size();
+        const uint32_t flags = bt::ctx_flags(g->members[0]);
+        const bool aos = (flags & BT_OPT_RECORDS_AOS) != 0;
+        if (o->records && (flags & BT_OPT_RECORDS_PLANES) && m > 1)
+            return bt::set_error(BT_E_INVALID_ARGUMENT, "plane-major records cannot be split across group members");
+        const uint32_t dsz = !b->desc ? 0u : b->desc_format == BT_DESC_XDP ? 16u : 8u;
+        // the split: by what each packet costs its member's PCIe link
+        std::vector<Range> r;
+        if (m == 1) {
+            r.push_back({0, n});
+        } else if (!b->desc) {   // fixed stride: equal cost, equal tile counts
+            const uint32_t tiles = (n + kTile - 1) / kTile;
+            for (uint32_t k = 0; k < m; ++k)
+                r.push_back({std::min(n, (uint32_t)((uint64_t)tiles * k / m) * kTile),
+                             std::min(n, (uint32_t)((uint64_t)tiles * (k + 1) / m) * kTile)});
+        } else {
+            std::vector<uint32_t> lens(n);
+            const uint8_t* d = static_cast<const uint8_t*>(b->desc);
+            if (b->desc_format == BT_DESC_XDP)
+                for (uint32_t i = 0; i < n; ++i) std::memcpy(&lens[i], d + (size_t)i * 16 + 8, 4);
+            else
+                for (uint32_t i = 0; i < n; ++i) lens[i] = BT_DESC_LEN(reinterpret_cast<const uint64_t*>(d)[i]);
+            bt_split_cost cost{};
+            (void)bt_group_cost(g, 1, o->records != nullptr, filter, dsz, &cost);
+            r = split(lens.data(), n, m, cost);
+        }
+        // the verdict words the pass list is built from
+        const uint32_t words = (n + 63) / 64;
+        std::unique_lock<std::mutex> slk(g->scratch_mu, std::defer_lock);
+        uint64_t* ver = o->verdict;
+        std::vector<uint8_t*> ver_dev(m, nullptr);
+        if (!ver && want_pass) {
+            slk.lock();
+            if (g->scratch_words < words) {
+                if (g->scratch) {
+                    (void)hipHostUnregister(g->scratch);
+                    free(g->scratch);
+                    g->scratch = nullptr;
+                    g->scratch_words = 0;
+                }
+                const size_t bytes = ((size_t)words * 8 + 4095) & ~(size_t)4095;
+                void* p = nullptr;
+                if (posix_memalign(&p, 4096, bytes) != 0) return bt::set_error(BT_E_RESOURCE, "scratch verdict words");
+                if (hipSetDevice(bt::ctx_device(g->members[0])) != hipSuccess ||
+                    hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+                    free(p);
+                    return bt::set_error(BT_E_INTERNAL, "hipHostRegister (scratch): %s",
+                                         hipGetErrorString(hipGetLastError()));
+                }
+                g->scratch = static_cast<uint64_t*>(p);
+                g->scratch_words = bytes / 8;
+                if (int rc = alias_all(g, p, &g->scratch_dev)) return rc;
+            }
+            ver = g->scratch;
+            ver_dev = g->scratch_dev;
+        }
+        // every buffer the kernels touch must be group-registered
+        auto need = [&](const void* p, uint64_t bytes, const char* what, uint32_t k, uint8_t** out) -> int {
+            *out = nullptr;
+            if (!p) return BT_OK;
+            *out = alias_of(g, k, p, bytes);
+            if (!*out)
+                return bt::set_error(BT_E_INVALID_ARGUMENT, "%s (%p + %llu) is not inside a group-registered range", what,
+                                     p, (unsigned long long)bytes);
+            return BT_OK;
+        };
+        const uint64_t rec_bytes = aos ? (uint64_t)o->n_cap * BT_REC_BYTES
+                                       : (flags & BT_OPT_RECORDS_PLANES) ? (uint64_t)o->n_cap * 16 * 6
+                                                                          : ((uint64_t)o->n_cap + 63) / 64 * 6144;
+        struct Member {
+            bt_batch b{};
+            bt_outputs o{};
+        };
+        std::vector<Member> mb(m);
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t lo = r[k].lo, cnt = r[k].hi - r[k].lo;
+            uint8_t *base = nullptr, *desc = nullptr, *rec = nullptr, *dec = nullptr, *vw = nullptr;
+            if (int rc = need(b->base, b->bytes ? b->bytes : (uint64_t)n * b->stride, "batch.base", k, &base)) return rc;
+            if (int rc = need(b->desc, (uint64_t)n * dsz, "batch.desc", k, &desc)) return rc;
+            if (int rc = need(o->records, rec_bytes, "out.records", k, &rec)) return rc;
+            if (int rc = need(o->decide, n, "out.decide", k, &dec)) return rc;
+            if (o->verdict) {
+                if (int rc = need(o->verdict, (uint64_t)words * 8, "out.verdict", k, &vw)) return rc;
+            } else if (ver) {
+                vw = ver_dev[k];
+            }
+            Member& x = mb[k];
+            x.b = *b;
+            x.b.n = cnt;
+            if (b->desc) {
+                x.b.base = base;
+                x.b.desc = desc + (size_t)lo * dsz;
+            } else {
+                x.b.base = base + (size_t)lo * b->stride;
+                x.b.bytes = (b->bytes ? b->bytes : (uint64_t)n * b->stride) - (uint64_t)lo * b->stride;
+            }
+            if (rec) {
+                x.o.records = aos ? rec + (size_t)lo * BT_REC_BYTES : rec + (size_t)(lo / kTile) * 6144;
+                x.o.n_cap = (flags & BT_OPT_RECORDS_PLANES) ? o->n_cap : o->n_cap - lo;
+            }
+            x.o.decide = dec ? dec + lo : nullptr;
+            x.o.verdict = vw ? reinterpret_cast<uint64_t*>(vw) + lo / kTile : nullptr;
+        }
+        // phase 1: every member's kernels over its range, then its pass count (per pool worker)
+        std::vector<std::vector<uint32_t>> cnt(m);
+        int rc = run_members(g, [&](uint32_t k) -> int {
+            const uint32_t lo = r[k].lo, hi = r[k].hi;
+            if (lo == hi) return BT_OK;
+            bt_ctx* c = g->members[k];
+            if (int e = bt_parse_filter_device(c, &mb[k].b, &mb[k].o, nullptr)) return e;
+            if (int e = bt_synchronize(c)) return e;
+            if (!want_pass) return BT_OK;
+            const uint32_t w0 = lo / kTile, w1 = (hi + 63) / 64;
+            std::vector<uint32_t>& ck = cnt[k];
+            ck.assign(kMaxPool, 0);
+            bt::host_parallel(c, [&](unsigned w, unsigned T) {
+                const uint32_t a = w0 + (uint32_t)((uint64_t)(w1 - w0) * w / T);
+                const uint32_t e = w0 + (uint32_t)((uint64_t)(w1 - w0) * (w + 1) / T);
+                ck[w] = verdict_bits(ver, a, e, hi, nullptr);
+            });
+            return BT_OK;
+        });
+        if (rc) return rc;
+        if (!want_pass) return BT_OK;
+        // phase 2: each member writes its indices at its offset in the whole list
+        std::vector<uint32_t> at(m + 1, 0);
+        for (uint32_t k = 0; k < m; ++k) {
+            uint32_t s = 0;
+            for (uint32_t x : cnt[k]) s += x;
+            at[k + 1] = at[k] + s;
+        }
+        if (o->pass_idx) {
+            rc = run_members(g, [&](uint32_t k) -> int {
+                const uint32_t lo = r[k].lo, hi = r[k].hi;
+                if (lo == hi) return BT_OK;
+                const uint32_t w0 = lo / kTile, w1 = (hi + 63) / 64;
+                const std::vector<uint32_t>& ck = cnt[k];
+                bt::host_parallel(g->members[k], [&](unsigned w, unsigned T) {
+                    const uint32_t a = w0 + (uint32_t)((uint64_t)(w1 - w0) * w / T);
+                    const uint32_t e = w0 + (uint32_t)((uint64_t)(w1 - w0) * (w + 1) / T);
+                    uint32_t off = at[k];
+                    for (unsigned j = 0; j < w; ++j) off += ck[j];
+                    (void)verdict_bits(ver, a, e, hi, o->pass_idx + off);
+                });
+                return BT_OK;
+            });
+            if (rc) return rc;
+        }
+        if (o->n_pass) *o->n_pass = at[m];
+        return BT_OK;
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_parse_filter_mapped: %s", e.what());
+    }
 }
 
 }  // extern "C"

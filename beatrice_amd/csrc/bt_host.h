@@ -3,6 +3,8 @@
 // bt_last_error(), the context's host thread pool, and filter programs.
 #pragma once
 
+#include <sched.h>
+
 #include <functional>
 #include <vector>
 
@@ -21,6 +23,16 @@ int compile_program(const bt_filter_desc* f, uint32_t n, uint32_t ctx_flags, Com
 int install_program(bt_ctx* c, const CompiledProgram& p);
 uint32_t ctx_flags(const bt_ctx* c);
 int ctx_device(const bt_ctx* c);
+// The CPUs the context's pool workers are pinned to (its device's NUMA node), or NULL.
+const cpu_set_t* ctx_pin(const bt_ctx* c);
+// Drops the context's cached "is this batch base host memory" answer (after an unregister).
+void ctx_forget_base(bt_ctx* c);
+// bt_host_stage_bytes without the C-ABI's checks.
+uint32_t stage_bytes_of(bt_ctx* c, bool records);
+// CPUs this process may use: its affinity set bounded by the cgroup v2 CPU quota.
+unsigned usable_cpus();
+// The CPUs of NUMA node `node` in this process's affinity set (false: none / unknown).
+bool node_cpus(int node, cpu_set_t* out);
 
 // Sets bt_last_error() and returns `code`.
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

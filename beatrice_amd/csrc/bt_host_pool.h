@@ -3,6 +3,9 @@
 // CPU. Host code only.
 #pragma once
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -23,11 +26,19 @@ namespace bt {
 // pass of a 12k-packet batch), whereas here the caller does the unclaimed work.
 class HostPool {
 public:
-    explicit HostPool(unsigned n) {
+    // pin (optional): the CPUs the workers run on, e.g. those of the device's NUMA node
+    // (bt_runtime.cpp place_ctx); the caller, worker 0, stays where it is
+    explicit HostPool(unsigned n, const cpu_set_t* pin = nullptr) {
         nthreads_ = n ? n : 1;
         static const bool fixed = getenv("BT_POOL_FIXED") != nullptr;   // A/B: each worker its own index
         fixed_ = fixed;
-        for (unsigned i = 1; i < nthreads_; ++i) th_.emplace_back([this, i] { loop(i); });
+        if (pin) pin_ = *pin;
+        const bool pinned = pin != nullptr;
+        for (unsigned i = 1; i < nthreads_; ++i)
+            th_.emplace_back([this, i, pinned] {
+                if (pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(pin_), &pin_);
+                loop(i);
+            });
     }
     ~HostPool() {
         {
@@ -109,6 +120,7 @@ private:
     std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
     unsigned finished_ = 0, nthreads_ = 1;
     bool fixed_ = false;
+    cpu_set_t pin_{};
     uint64_t gen_ = 0;
     bool stop_ = false;
 };

@@ -6,6 +6,8 @@
 // failures return a beatrice::ErrorCode value and set a thread-local message.
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -17,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <cctype>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -123,6 +126,11 @@ struct bt_ctx {
     bool host_ready = false;
     std::unique_ptr<HostPool> pool;   // created on first use (pool_of)
     std::once_flag pool_once;
+    // placement (place_ctx): the host NUMA node closest to the device and the CPUs of it this
+    // process may use; the pool's workers run there when `pinned`
+    int numa_node = -1;
+    cpu_set_t pin{};
+    bool pinned = false;
 
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -192,18 +200,103 @@ unsigned usable_cpus() {
     return n;
 }
 
+// "0-3,8,10-11" (a sysfs cpulist) -> set; false if unreadable
+bool parse_cpulist(const char* s, cpu_set_t* out) {
+    CPU_ZERO(out);
+    bool any = false;
+    while (s && *s) {
+        char* e = nullptr;
+        const long a = strtol(s, &e, 10);
+        if (e == s || a < 0) return false;
+        long b = a;
+        s = e;
+        if (*s == '-') {
+            b = strtol(s + 1, &e, 10);
+            if (e == s + 1 || b < a) return false;
+            s = e;
+        }
+        for (long i = a; i <= b && i < CPU_SETSIZE; ++i) CPU_SET((int)i, out);
+        any = true;
+        while (*s == ',' || *s == '\n' || *s == ' ') ++s;
+    }
+    return any;
+}
+
+// The host NUMA node closest to `device`: HIP's attribute, else the PCI function's sysfs
+// numa_node (read from its bus id); -1 when the host has no NUMA information.
+int device_numa_node(int device) {
+    int node = -1;
+    if (hipDeviceGetAttribute(&node, hipDeviceAttributeHostNumaId, device) != hipSuccess) {
+        (void)hipGetLastError();
+        node = -1;
+    }
+    if (node >= 0) return node;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char* p = bus; *p; ++p) *p = (char)tolower((unsigned char)*p);
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE* f = fopen(path, "r")) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    return node;
+}
+
+// The CPUs of NUMA node `node` that this process may run on (its affinity set); false when
+// there are none or the node's cpulist is unreadable.
+bool node_cpus(int node, cpu_set_t* out) {
+    if (node < 0) return false;
+    char path[96];
+    snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+    char buf[4096] = {0};
+    FILE* f = fopen(path, "r");
+    if (!f) return false;
+    const size_t got = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[got] = 0;
+    cpu_set_t nodeset, aff;
+    if (!parse_cpulist(buf, &nodeset)) return false;
+    if (sched_getaffinity(0, sizeof(aff), &aff) != 0) return false;
+    CPU_AND(out, &nodeset, &aff);
+    return CPU_COUNT(out) > 0;
+}
+
+// Places a context's host work next to its device: the pool's workers (gather, drain, ring
+// walk) run on the CPUs of the device's NUMA node. hipHostMalloc without
+// hipHostMallocNumaUser allocates the pinned staging near the current device already (HIP
+// lets the user's policy decide only with that flag, hip_runtime_api.h), and the staging
+// is allocated after hipSetDevice (ensure_host). BT_NUMA_PIN=0 turns the pinning off (A/B).
+void place_ctx(bt_ctx* c) {
+    c->numa_node = device_numa_node(c->device);
+    static const bool off = [] {
+        const char* e = getenv("BT_NUMA_PIN");
+        return e && atoi(e) == 0;
+    }();
+    c->pinned = !off && node_cpus(c->numa_node, &c->pin);
+}
+
+// The pool's size: opts.host_threads, else BT_HOST_THREADS, else 8 (at most the usable
+// CPUs); at most 16. A group sets each member's opts.host_threads from its budget (bt_group.cpp).
+unsigned pool_threads_of(const bt_ctx* c) {
+    unsigned nt = c->opts.host_threads;
+    if (!nt) {
+        // 8, not every usable CPU: with callers on all 16 of a GPU box's CPUs (T callers of
+        // one GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool
+        // oversubscribes them: C2 applyFilters 136-142 against 163 Mpps, classify 161-163
+        // against 172-192 (tools/ab_cmd.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
+        const char* e = getenv("BT_HOST_THREADS");
+        nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(8u, usable_cpus());
+    }
+    return std::min(nt, 16u);
+}
+
 HostPool& pool_of(bt_ctx* c) {
     std::call_once(c->pool_once, [c] {
-        unsigned nt = c->opts.host_threads;
-        if (!nt) {   // auto: BT_HOST_THREADS, else 8 (at most the usable CPUs)
-            // 8, not every usable CPU: with callers on all 16 of a GPU box's CPUs (T callers of
-            // one GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool
-            // oversubscribes them: C2 applyFilters 136-142 against 163 Mpps, classify 161-163
-            // against 172-192 (tools/ab_cmd.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
-            const char* e = getenv("BT_HOST_THREADS");
-            nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(8u, usable_cpus());
-        }
-        c->pool = std::make_unique<HostPool>(std::min(nt, 16u));
+        c->pool = std::make_unique<HostPool>(pool_threads_of(c), c->pinned ? &c->pin : nullptr);
     });
     return *c->pool;
 }
@@ -562,6 +655,7 @@ int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
     c->grid = c->opts.grid_waves ? (int)((c->opts.grid_waves + kWavesPerBlock - 1) / kWavesPerBlock)
                                  : device_grid_blocks(device);
     to_device_program(nullptr, 0, &c->prog);
+    place_ctx(c);
     *out = c;
     return BT_OK;
 }
@@ -575,6 +669,37 @@ int bt_context_device(const bt_ctx* c, int* device, char* pci_bus_id, uint32_t c
     }
     return BT_OK;
 }
+
+int bt_context_placement(bt_ctx* c, bt_placement* out) {
+    if (!c || !out) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    *out = bt_placement{};
+    out->numa_node = c->numa_node;
+    out->pinned_cpus = c->pinned ? (uint32_t)CPU_COUNT(&c->pin) : 0u;
+    out->pool_threads = pool_threads_of(c);
+    out->staging_node = -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->host_ready && c->hs[0].h_in) {   // where the kernel put the pinned staging's first page
+        void* page = c->hs[0].h_in;
+        int status = -1;
+        if (syscall(SYS_move_pages, 0, 1UL, &page, nullptr, &status, 0) == 0 && status >= 0) out->staging_node = status;
+    }
+    return BT_OK;
+}
+
+int bt_node_cpus(int node, int32_t* cpus, uint32_t cap, uint32_t* n) {
+    if (!n || (cap && !cpus)) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    *n = 0;
+    cpu_set_t s;
+    if (!bt::node_cpus(node, &s)) return BT_OK;
+    for (int i = 0; i < CPU_SETSIZE; ++i)
+        if (CPU_ISSET(i, &s)) {
+            if (*n < cap) cpus[*n] = i;
+            ++*n;
+        }
+    return BT_OK;
+}
+
+uint32_t bt_usable_cpus(void) { return bt::usable_cpus(); }
 
 void bt_destroy(bt_ctx* c) {
     if (!c) return;
@@ -691,6 +816,12 @@ int install_program(bt_ctx* c, const CompiledProgram& p) {
 
 uint32_t ctx_flags(const bt_ctx* c) { return c->opts.flags; }
 int ctx_device(const bt_ctx* c) { return c->device; }
+const cpu_set_t* ctx_pin(const bt_ctx* c) { return c->pinned ? &c->pin : nullptr; }
+void ctx_forget_base(bt_ctx* c) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->last_base = nullptr;
+}
+uint32_t stage_bytes_of(bt_ctx* c, bool records);   // defined with the host pipeline
 
 }  // namespace bt
 
@@ -896,6 +1027,17 @@ namespace {
 uint32_t stage_bytes(const bt_ctx* c, bool records) {
     return !c->dfa_pool.empty() ? kHostSlotPayload : records ? kHostSlot : kHostSlotFilter;
 }
+
+}  // namespace
+
+namespace bt {
+uint32_t stage_bytes_of(bt_ctx* c, bool records) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    return stage_bytes(c, records);
+}
+}  // namespace bt
+
+namespace {
 
 // Host batch pipeline shared by bt_parse_filter (base + descriptors) and
 // bt_parse_filter_ptrs (one pointer per frame): frame(i, &len) returns frame i.
@@ -1429,6 +1571,63 @@ int bt_time_extract2(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, u
 int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
                        const bt_extract_out* out, uint32_t iters, bt_timing* t) {
     return bt_time_extract2(c, b, fields, n_fields, out, iters, BT_TIME_KERNEL_EVENTS, t);
+}
+
+// extractValue<T> (src/parser/ProtocolParser.cpp:385-433) on the host for one field of a
+// frame at least the table's span long: bt_extract.hip's decode_field byte loop (its one-window
+// fast path computes the same bits for fields no longer than their type).
+static uint64_t decode_field_host(const ExField& f, const uint8_t* frame) {
+    const uint32_t type = f.ctl & 0xFFu;
+    const bool le = ((f.ctl >> 8) & 0xFFu) == BT_ENDIAN_LITTLE;
+    const uint32_t o = f.offset, L = f.length;
+    switch (type) {
+    case BT_FT_BOOLEAN: return frame[o] != 0 ? 1u : 0u;
+    case BT_FT_BYTES: case BT_FT_STRING: case BT_FT_MAC: case BT_FT_IPV4: case BT_FT_IPV6: case BT_FT_CUSTOM:
+        return 0;
+    default: break;
+    }
+    const uint32_t w = (type == BT_FT_UINT8 || type == BT_FT_INT8) ? 8u
+                     : (type == BT_FT_UINT16 || type == BT_FT_INT16) ? 16u
+                     : (type == BT_FT_UINT32 || type == BT_FT_INT32 || type == BT_FT_FLOAT32) ? 32u : 64u;
+    if ((type == BT_FT_FLOAT32 || type == BT_FT_FLOAT64) && L * 8u != w) return 0;
+    const uint32_t m = w == 64u ? 63u : 31u;
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t sh = (8u * i) & m;
+        if (sh >= w) continue;
+        v |= (uint64_t)frame[o + (le ? i : L - 1u - i)] << sh;
+    }
+    return w == 64u ? v : (v & ((1ull << w) - 1ull));
+}
+
+int bt_extract_host(const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,
+                    uint32_t n_fields, uint8_t* status, uint64_t* values, uint8_t* image) {
+    if (n && (!frames || !lens)) return fail(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
+    ExTable t;
+    bool never = false;
+    uint64_t span64 = 0;
+    int rc = build_table(fields, n_fields, &t, &span64, &never);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool ok = !never && lens[i] >= t.span;
+        if (status) status[i] = ok ? 0u : 9u;   // ParseStatus SUCCESS / PACKET_TOO_SHORT
+        if (values)
+            for (uint32_t k = 0; k < n_fields; ++k) values[(size_t)k * n + i] = ok ? decode_field_host(t.f[k], frames[i]) : 0u;
+        if (image && !never && t.span) {
+            uint8_t* out = image + (size_t)i * t.span;
+            if (ok) std::memcpy(out, frames[i], t.span);
+            else std::memset(out, 0, t.span);
+        }
+    }
+    return BT_OK;
+}
+
+int bt_filter_dfa_pool(const bt_ctx* c, void* out, uint32_t cap, uint32_t* bytes) {
+    if (!c || !bytes || (cap && !out)) return fail(BT_E_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> lk(const_cast<bt_ctx*>(c)->mu);
+    *bytes = (uint32_t)c->dfa_pool.size();
+    if (out && cap) std::memcpy(out, c->dfa_pool.data(), std::min<size_t>(cap, c->dfa_pool.size()));
+    return BT_OK;
 }
 
 int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,

@@ -245,7 +245,6 @@ Result<void> GpuAfPacketBackend::freeDMABuffers() { return Result<void>::success
 GpuTpacketStage::GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring, Options opts)
     : filter_(filter), ring_(ring), opts_(opts) {
     if (!ring_.isOpen()) throw std::runtime_error("GpuTpacketStage: ring is not open");
-    bt_ctx* ctx = filter_.context();
     const bt_tpv3_ring g = ring_.ring();
     ringBase_ = static_cast<uint8_t*>(g.base);
     const uint32_t cap = opts_.maxPackets;
@@ -254,29 +253,32 @@ GpuTpacketStage::GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring, O
     decide_.resize((size_t)tiles * 64);
     verdict_.resize(tiles);
     if (opts_.records) records_.resize((size_t)tiles * 64 * BT_REC_BYTES);
-    auto reg = [&](void* p, size_t bytes, void** dev) {
-        if (bt_host_register(ctx, p, bytes, dev) != BT_OK)
-            throw std::runtime_error(std::string("GpuTpacketStage: bt_host_register: ") + bt_last_error());
-    };
-    reg(ringBase_, ring_.bytes(), &ringDev_);
-    reg(desc_.data(), desc_.size() * sizeof(bt_pkt_desc), &descDev_);
-    reg(decide_.data(), decide_.size(), &decideDev_);
-    reg(verdict_.data(), verdict_.size() * 8, &verdictDev_);
-    if (opts_.records) reg(records_.data(), records_.size(), &recordsDev_);
     if (opts_.gather) {
         slots_.resize((size_t)cap * BT_PREFIX_SLOT + 64);
         slotDesc_.resize(cap);
-        reg(slots_.data(), slots_.size(), &slotsDev_);
-        reg(slotDesc_.data(), slotDesc_.size() * sizeof(bt_pkt_desc), &slotDescDev_);
+    }
+    // registered once with every device of the filter: each reads its range of a batch in
+    // place over its own PCIe link (bt_group_parse_filter_mapped)
+    try {
+        for (auto [p, bytes] : {std::pair<void*, size_t>{ringBase_, ring_.bytes()},
+                                {desc_.data(), desc_.size() * sizeof(bt_pkt_desc)},
+                                {decide_.data(), decide_.size()},
+                                {verdict_.data(), verdict_.size() * 8},
+                                {records_.data(), records_.size()},
+                                {slots_.data(), slots_.size()},
+                                {slotDesc_.data(), slotDesc_.size() * sizeof(bt_pkt_desc)}}) {
+            if (!p || !bytes) continue;
+            filter_.registerHost(p, bytes);
+            registered_.push_back(p);
+        }
+    } catch (...) {
+        for (void* p : registered_) (void)bt_group_host_unregister(filter_.group(), p);
+        throw;
     }
 }
 
 GpuTpacketStage::~GpuTpacketStage() {
-    bt_ctx* ctx = filter_.context();
-    (void)bt_synchronize(ctx);
-    for (void* p : {(void*)ringBase_, (void*)desc_.data(), (void*)decide_.data(), (void*)verdict_.data(),
-                    (void*)records_.data(), (void*)slots_.data(), (void*)slotDesc_.data()})
-        if (p) (void)bt_host_unregister(ctx, p);
+    for (void* p : registered_) (void)bt_group_host_unregister(filter_.group(), p);
 }
 
 const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds timeout) {
@@ -298,19 +300,19 @@ const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds ti
     batch_.verdict = verdict_.data();
     batch_.records = opts_.records ? records_.data() : nullptr;
     batch_.gathered = gathered;
-    bt_batch b{};
-    b.base = static_cast<const uint8_t*>(gathered ? slotsDev_ : ringDev_);
-    b.desc = gathered ? slotDescDev_ : descDev_;
+    bt_batch b{};   // host addresses: the filter's group maps them per device
+    b.base = gathered ? slots_.data() : ringBase_;
+    b.desc = gathered ? slotDesc_.data() : desc_.data();
     b.n = n;
     b.bytes = gathered ? slots_.size() : ring_.bytes();
     b.desc_format = BT_DESC_PACKED;
     b.flags = gathered ? BT_BATCH_PREFIXES : 0u;   // PAYLOAD slots: resolved on the host from the frame
     bt_outputs o{};
-    o.records = recordsDev_;
+    o.records = opts_.records ? records_.data() : nullptr;
     o.n_cap = opts_.maxPackets;
-    o.verdict = static_cast<uint64_t*>(verdictDev_);
-    o.decide = static_cast<uint8_t*>(decideDev_);
-    batch_.pass = filter_.classifyMapped(b, o, decide_.data(), verdict_.data(), [this](uint32_t i) {
+    o.verdict = verdict_.data();
+    o.decide = decide_.data();
+    batch_.pass = filter_.classifyMapped(b, o, [this](uint32_t i) {
         const uint32_t len = length(i);
         std::shared_ptr<uint8_t[]> data(new uint8_t[len]);
         std::memcpy(data.get(), frame(i), len);

@@ -122,9 +122,11 @@ public:
         bool gathered = false;               // the kernels read packed header prefixes
     };
 
-    // The filter supplies the context (device, stream) and the compiled program; the
-    // ring must stay open for the stage's lifetime. Throws std::runtime_error when the
-    // ring cannot be mapped into the device.
+    // The filter supplies the devices and the compiled program: the ring and the stage's
+    // buffers are registered with every device of the filter, and each batch is split across
+    // them, every device reading its range of the ring over its own PCIe link. The ring must
+    // stay open for the stage's lifetime. Throws std::runtime_error when the ring cannot be
+    // mapped into the devices.
     GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring, Options opts);
     GpuTpacketStage(GpuPacketFilter& filter, TpacketV3Ring& ring) : GpuTpacketStage(filter, ring, Options()) {}
     ~GpuTpacketStage();
@@ -147,17 +149,15 @@ private:
     TpacketV3Ring& ring_;
     Options opts_;
     uint8_t* ringBase_ = nullptr;
-    void* ringDev_ = nullptr;
     // registered host buffers: descriptors in, decisions / verdicts / records out
     std::vector<bt_pkt_desc> desc_;
     std::vector<uint8_t> decide_;
     std::vector<uint64_t> verdict_;
     std::vector<uint8_t> records_;
-    void *descDev_ = nullptr, *decideDev_ = nullptr, *verdictDev_ = nullptr, *recordsDev_ = nullptr;
     // header gather: packed prefixes and their descriptors (registered)
     std::vector<uint8_t> slots_;
     std::vector<bt_pkt_desc> slotDesc_;
-    void *slotsDev_ = nullptr, *slotDescDev_ = nullptr;
+    std::vector<void*> registered_;   // with the filter's group
     uint64_t polls_ = 0;
     Batch batch_;
 };

@@ -6,6 +6,7 @@
 #include <sys/mman.h>
 
 #include <chrono>
+#include <cerrno>
 #include <cstdlib>
 #include <exception>
 #include <memory>
@@ -73,7 +74,14 @@ std::vector<int> GpuPacketFilter::devicesFromEnv(int fallback) {
         while (at < s.size()) {
             const size_t comma = s.find(',', at);
             const std::string tok = s.substr(at, comma == std::string::npos ? std::string::npos : comma - at);
-            if (!tok.empty()) d.push_back(std::stoi(tok));
+            if (!tok.empty()) {
+                char* end = nullptr;
+                errno = 0;
+                const long v = std::strtol(tok.c_str(), &end, 10);
+                if (end == tok.c_str() || *end || errno || v < 0 || v > 1 << 20)
+                    throw std::runtime_error("GpuPacketFilter: BEATRICE_GPU_DEVICES: bad device \"" + tok + "\"");
+                d.push_back((int)v);
+            }
             if (comma == std::string::npos) break;
             at = comma + 1;
         }
@@ -82,12 +90,20 @@ std::vector<int> GpuPacketFilter::devicesFromEnv(int fallback) {
     return d;
 }
 
-GpuPacketFilter::GpuPacketFilter(int device, const bt_opts* opts) { open(devicesFromEnv(device), opts); }
+GpuPacketFilter::GpuPacketFilter(int device, const bt_opts* opts) {
+    // an explicit device is that device alone; only the default reads the environment
+    open(device >= 0 ? std::vector<int>{device} : devicesFromEnv(0), opts);
+}
 
 GpuPacketFilter::GpuPacketFilter(const std::vector<int>& devices, const bt_opts* opts) { open(devices, opts); }
 
 void GpuPacketFilter::open(const std::vector<int>& devices, const bt_opts* opts) {
+    if (const char* e = std::getenv("BEATRICE_GPU_HOST_BELOW")) hostBelow_.store(std::strtoull(e, nullptr, 10));
     if (devices.empty()) throw std::invalid_argument("GpuPacketFilter: empty device list");
+    if (bt_abi_version() < BT_ABI_VERSION)   // a libbeatrice_gpu.so older than this header
+        throw std::runtime_error("GpuPacketFilter: libbeatrice_gpu.so has C-ABI version " +
+                                 std::to_string(bt_abi_version()) + ", this adapter needs " +
+                                 std::to_string(BT_ABI_VERSION));
     if (bt_group_create(devices.data(), (uint32_t)devices.size(), opts, &group_) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
     ctx_ = bt_group_member(group_, 0);
@@ -186,6 +202,12 @@ void GpuPacketFilter::compileLocked() {
     bt_filter_program(ctx_, slots.data(), BT_MAX_FILTERS, &m);
     program_.clear();
     rejectReason_.clear();
+    uint32_t pool = 0;
+    if (bt_filter_dfa_pool(ctx_, nullptr, 0, &pool) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
+    dfaPool_.assign(pool, 0);
+    if (pool && bt_filter_dfa_pool(ctx_, dfaPool_.data(), pool, &pool) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
     for (uint32_t k = 0; k < m; ++k) {
         const auto& src = sortedFilters[slots[k].source_index];
         program_.push_back(Slot{src.first, src.second, slots[k]});
@@ -218,13 +240,28 @@ void GpuPacketFilter::rethrow(const Slot& s) const {
     throw std::invalid_argument("stoi");
 }
 
+uint32_t GpuPacketFilter::evalFrame(const uint8_t* d, size_t len) const {
+    for (uint32_t s = 0; s < program_.size(); ++s) {
+        const bt_filter_slot& c = program_[s].compiled;
+        int r;
+        if (c.kind == BT_K_HOST) return (BT_DECIDE_HOST << 6) | s;
+        if (c.kind == BT_K_PAYLOAD) r = bt_payload_dfa_eval(dfaPool_.data() + c.a, d, (uint32_t)len) ? 1 : 0;
+        else r = eval_builtin(c, d, len);
+        if (r == 0) return (BT_DECIDE_REJECT << 6) | s;
+        if (r == 2) return (BT_DECIDE_THROW << 6) | s;
+    }
+    return (BT_DECIDE_PASS << 6) | (program_.empty() ? 0u : (uint32_t)program_.size() - 1);
+}
+
 uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
     const uint8_t* d = p.data();
     const size_t len = p.length();
     for (uint32_t s = first; s < program_.size(); ++s) {
         const Slot& sl = program_[s];
         int r;
-        if (sl.compiled.kind != BT_K_HOST && sl.compiled.kind != BT_K_PAYLOAD) {
+        if (sl.compiled.kind == BT_K_PAYLOAD) {   // the compiled DFA: regex_search's result
+            r = bt_payload_dfa_eval(dfaPool_.data() + sl.compiled.a, d, (uint32_t)len) ? 1 : 0;
+        } else if (sl.compiled.kind != BT_K_HOST) {
             r = eval_builtin(sl.compiled, d, len);
         } else if (sl.entry->config.type == FilterType::CUSTOM) {
             r = sl.entry->customFunc ? (sl.entry->customFunc(p) ? 1 : 0) : 1;   // :323-328
@@ -309,6 +346,10 @@ void GpuPacketFilter::setTiming(double device_s, double host_s) {
 void GpuPacketFilter::runFrames(const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                                 std::vector<uint8_t>& decide, std::vector<bt_rec>* records) {
     decide.resize(n);
+    if (!records && hostSmall(n)) {   // a device round trip costs more than the batch
+        for (uint32_t i = 0; i < n; ++i) decide[i] = (uint8_t)evalFrame(frames[i], lens[i]);
+        return;
+    }
     if (records) records->resize(n);
     if (bt_group_parse_filter_ptrs(group_, frames, lens, n, records ? records->data() : nullptr, nullptr,
                                    decide.data(), nullptr, nullptr) != BT_OK)
@@ -349,7 +390,7 @@ struct GpuPacketFilter::Tally {
     std::exception_ptr ex;  // ... or the exception its CUSTOM callback threw
     // after the stats of the packets before it are applied, as the reference's per-packet
     // loop leaves them (src/PacketFilter.cpp:116, 121-130)
-    void rethrowIfAny(const GpuPacketFilter& f, const std::vector<uint8_t>& decide) const {
+    void rethrowIfAny(const GpuPacketFilter& f, const uint8_t* decide) const {
         if (ex) std::rethrow_exception(ex);
         if (threw) f.rethrow(f.program_[decide[stop] & 63u]);
     }
@@ -360,7 +401,7 @@ struct GpuPacketFilter::Tally {
 // scan): each part tallies its range up to its first throw, and the parts are joined in
 // order up to the first part that threw. Returns false to fall back. (The serial pass took
 // 3.3 ns per packet, more than the device pass of a one-caller classify.)
-bool GpuPacketFilter::scanParallel(size_t n, const std::vector<uint8_t>& decide, std::vector<uint32_t>* pass_idx,
+bool GpuPacketFilter::scanParallel(size_t n, const uint8_t* decide, std::vector<uint32_t>* pass_idx,
                                    std::vector<uint32_t>* error_idx, Tally& t) {
     struct Part {
         uint64_t counted = 0, passed = 0;
@@ -377,7 +418,7 @@ bool GpuPacketFilter::scanParallel(size_t n, const std::vector<uint8_t>& decide,
         size_t n, slots;
         bool want_pass, errors;
         std::vector<Part>* parts;
-    } u{decide.data(), n, slots, pass_idx != nullptr, error_idx != nullptr, &parts};
+    } u{decide, n, slots, pass_idx != nullptr, error_idx != nullptr, &parts};
     auto run = [](void* x, uint32_t w, uint32_t T) {
         auto* u = static_cast<U*>(x);
         for (uint32_t k = w; k < kParts; k += T) {
@@ -431,8 +472,9 @@ bool GpuPacketFilter::scanParallel(size_t n, const std::vector<uint8_t>& decide,
 }
 
 template <class PacketAt>
-GpuPacketFilter::Tally GpuPacketFilter::scan(size_t n, PacketAt packet, std::vector<uint8_t>& decide,
-                                            std::vector<uint32_t>* pass_idx, std::vector<uint32_t>* error_idx) {
+GpuPacketFilter::Tally GpuPacketFilter::scan(size_t n, PacketAt packet, uint8_t* decide,
+                                            std::vector<uint32_t>* pass_idx, std::vector<uint32_t>* error_idx,
+                                            uint64_t* verdict) {
     Tally t;
     if (n >= 65536 && inFlight_.load(std::memory_order_relaxed) == 1) {
         if (scanParallel(n, decide, pass_idx, error_idx, t)) return t;
@@ -462,6 +504,7 @@ GpuPacketFilter::Tally GpuPacketFilter::scan(size_t n, PacketAt packet, std::vec
                 }
             }
             decide[i] = (uint8_t)d;
+            if (verdict && (d >> 6) == BT_DECIDE_PASS) verdict[i / 64] |= 1ull << (i % 64);
         }
         const uint32_t code = d >> 6, slot = d & 63u;
         if (code == BT_DECIDE_THROW) {
@@ -513,7 +556,8 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, decide, nullptr, nullptr);
+    const Tally t =
+        scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, decide.data(), nullptr, nullptr);
     // The FilterResults of the packets before any throw (:102-111), built on the host
     // threads from per-slot strings made once per program: the reference's vector is the
     // result either way, its strings are copied rather than concatenated per packet.
@@ -539,13 +583,53 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
         }
     });
     flushTally(t, per);
-    t.rethrowIfAny(*this, decide);   // earlier packets are counted
+    t.rethrowIfAny(*this, decide.data());   // earlier packets are counted
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return results;
 }
 
+// updateStats (src/PacketFilter.cpp:374-386) for one packet.
+void GpuPacketFilter::tallyOne(uint32_t d, std::chrono::microseconds t) {
+    std::lock_guard<std::mutex> lock(statsMutex_);
+    ++stats_.packetsProcessed;
+    const bool pass = (d >> 6) == BT_DECIDE_PASS;
+    if (pass) ++stats_.packetsPassed;
+    else ++stats_.packetsDropped;
+    stats_.totalProcessingTime += t;
+    if (program_.empty()) {
+        ++stats_.filterCounts[""];
+        return;
+    }
+    ++stats_.filterCounts[pass ? program_.back().name : program_[d & 63u].name];
+}
+
+// One packet (src/PacketFilter.cpp:57-119): decided on the calling thread with the compiled
+// program; the device would cost a round trip for one packet.
 GpuPacketFilter::FilterResult GpuPacketFilter::applyFilters(const Packet& packet) {
-    return applyFilters(std::vector<Packet>{packet}).front();
+    if (!hostSmall(1)) return applyFilters(std::vector<Packet>{packet}).front();
+    const auto lock = lockProgram();
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t d = evalFrame(packet.data(), packet.length());
+    if ((d >> 6) == BT_DECIDE_HOST) {
+        std::lock_guard<std::mutex> host(hostMutex_);   // CUSTOM callbacks one at a time, as the reference
+        d = resolveHost(packet, d & 63u);                // a throwing callback propagates, no stats (:116)
+    }
+    const uint32_t code = d >> 6, slot = d & 63u;
+    if (code == BT_DECIDE_THROW) rethrow(program_[slot]);   // std::stoi's exception, before updateStats
+    FilterResult r;
+    r.passed = code == BT_DECIDE_PASS;
+    if (!program_.empty()) {
+        if (r.passed) {
+            r.filterName = program_.back().name;
+            r.reason = kPassedReason;
+        } else {
+            r.filterName = program_[slot].name;
+            r.reason = rejectReason_[slot];
+        }
+    }
+    r.processingTime = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
+    tallyOne(d, r.processingTime);
+    return r;
 }
 
 GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& packets) {
@@ -560,9 +644,9 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classify(const std::vector<Packet>& p
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
     const Tally t =
-        scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide, &v.pass_idx, nullptr);
+        scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide.data(), &v.pass_idx, nullptr);
     flushTally(t, per);
-    t.rethrowIfAny(*this, v.decide);
+    t.rethrowIfAny(*this, v.decide.data());
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;
 }
@@ -578,8 +662,8 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const std::vector<P
                      (int64_t)packets.size();
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide, &v.pass_idx,
-                         &v.error_idx);
+    const Tally t = scan(packets.size(), [&](size_t i) -> const Packet& { return packets[i]; }, v.decide.data(),
+                         &v.pass_idx, &v.error_idx);
     flushTally(t, per);
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;
@@ -626,64 +710,45 @@ GpuPacketFilter::Verdicts GpuPacketFilter::classifyPerPacket(const uint8_t* cons
                      (int64_t)n;
     const auto t1 = std::chrono::steady_clock::now();
     const double device_s = std::chrono::duration<double>(t1 - t0).count();
-    const Tally t = scan(n, [&](size_t i) { return packetOf(i); }, v.decide, &v.pass_idx, &v.error_idx);
+    const Tally t = scan(n, [&](size_t i) { return packetOf(i); }, v.decide.data(), &v.pass_idx, &v.error_idx);
     flushTally(t, per);
     setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return v;
 }
 
 std::vector<uint32_t> GpuPacketFilter::classifyMapped(const bt_batch& batch, const bt_outputs& out,
-                                                     uint8_t* decideHost, uint64_t* verdictHost,
                                                      const std::function<Packet(uint32_t)>& packetOf) {
     std::vector<uint32_t> pass;
     const auto lock = lockProgram();
+    const InFlight busy(inFlight_);
     if (!batch.n) return pass;
-    if (!out.decide || !decideHost) throw std::invalid_argument("GpuPacketFilter::classifyMapped: decide required");
+    if (!out.decide) throw std::invalid_argument("GpuPacketFilter::classifyMapped: decide required");
     const auto t0 = std::chrono::steady_clock::now();
-    if (bt_parse_filter_device(ctx_, &batch, &out, nullptr) != BT_OK || bt_synchronize(ctx_) != BT_OK)
+    bt_outputs o = out;   // the pass list comes from the host's scan (after host slots)
+    o.pass_idx = nullptr;
+    o.n_pass = nullptr;
+    if (bt_group_parse_filter_mapped(group_, &batch, &o) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
     const auto per = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0) /
                      (int64_t)batch.n;
-    // stats are sums: count per (code, slot) and apply once (before a rethrow too)
-    uint64_t passed = 0, rejected[BT_MAX_FILTERS] = {};
-    uint32_t counted = 0;
-    auto flush = [&] {
-        std::lock_guard<std::mutex> sl(statsMutex_);
-        stats_.packetsProcessed += counted;
-        stats_.packetsPassed += passed;
-        stats_.packetsDropped += counted - passed;
-        stats_.totalProcessingTime += per * (int64_t)counted;
-        if (program_.empty()) {
-            if (counted) stats_.filterCounts[""] += counted;
-            return;
-        }
-        if (passed) stats_.filterCounts[program_.back().name] += passed;
-        for (size_t s = 0; s < program_.size(); ++s)
-            if (rejected[s]) stats_.filterCounts[program_[s].name] += rejected[s];
-    };
-    std::unique_lock<std::mutex> host(hostMutex_, std::defer_lock);   // taken at the first host slot
-    for (uint32_t i = 0; i < batch.n; ++i) {
-        uint32_t d = decideHost[i];
-        if ((d >> 6) == BT_DECIDE_HOST) {
-            if (!host.owns_lock()) host.lock();
-            decideHost[i] = (uint8_t)(d = resolveHost(packetOf(i), d & 63u));
-            if (verdictHost && (d >> 6) == BT_DECIDE_PASS) verdictHost[i / 64] |= 1ull << (i % 64);
-        }
-        const uint32_t code = d >> 6, slot = d & 63u;
-        if (code == BT_DECIDE_THROW) {
-            flush();
-            rethrow(program_[slot]);
-        }
-        ++counted;
-        if (code == BT_DECIDE_PASS) {
-            ++passed;
-            pass.push_back(i);
-        } else {
-            ++rejected[slot];
-        }
-    }
-    flush();
+    const auto t1 = std::chrono::steady_clock::now();
+    const double device_s = std::chrono::duration<double>(t1 - t0).count();
+    const Tally t = scan(batch.n, [&](size_t i) { return packetOf((uint32_t)i); }, out.decide, &pass, nullptr,
+                         out.verdict);
+    flushTally(t, per);
+    t.rethrowIfAny(*this, out.decide);
+    setTiming(device_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     return pass;
+}
+
+void GpuPacketFilter::registerHost(void* p, size_t bytes) {
+    if (bt_group_host_register(group_, p, bytes) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter::registerHost: ") + bt_last_error());
+}
+
+void GpuPacketFilter::unregisterHost(void* p) {
+    if (bt_group_host_unregister(group_, p) != BT_OK)
+        throw std::runtime_error(std::string("GpuPacketFilter::unregisterHost: ") + bt_last_error());
 }
 
 }  // namespace gpu

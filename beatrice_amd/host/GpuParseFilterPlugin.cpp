@@ -155,7 +155,10 @@ public:
             flush_us_ = std::max(1, env_int("BEATRICE_GPU_FLUSH_US", 2000));
             workers_ = std::min(8, std::max(1, env_int("BEATRICE_GPU_WORKERS", 2)));
             pack_ = env_int("BEATRICE_GPU_PACK", 0) != 0;
-            filter_ = std::make_shared<GpuPacketFilter>(env_int("BEATRICE_GPU_DEVICE", 0));
+            // the plugin reads the device list: BEATRICE_GPU_DEVICES=0,1,... (a group), else
+            // BEATRICE_GPU_DEVICE (one device, default 0)
+            filter_ = std::make_shared<GpuPacketFilter>(
+                GpuPacketFilter::devicesFromEnv(env_int("BEATRICE_GPU_DEVICE", 0)));
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
             whole_ = filter_->needsPackets();
             stage_ = stageWidth(*filter_);

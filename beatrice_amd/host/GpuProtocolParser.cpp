@@ -6,6 +6,7 @@
 #include "GpuProtocolParser.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -278,6 +279,7 @@ GpuProtocolParser::GpuProtocolParser(const parser::ProtocolParser::ParserConfig&
     if (bt_create(device, opts, &ctx_) != BT_OK)
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
     if (config_.enablePerformanceMetrics) profiling_ = true;   // :31-35
+    if (const char* e = std::getenv("BEATRICE_GPU_HOST_BELOW")) hostBelow_ = std::strtoull(e, nullptr, 10);
 }
 
 GpuProtocolParser::~GpuProtocolParser() { bt_destroy(ctx_); }
@@ -752,10 +754,15 @@ void GpuProtocolParser::extract(GpuFieldBatch& b) {
     b.values_.assign((size_t)table.size() * n, 0);
     b.image_.assign((size_t)n * b.span_, 0);
     const auto t0 = std::chrono::steady_clock::now();
-    if (n && bt_extract(ctx_, b.frames_.data(), b.lens_.data(), n, table.data(), (uint32_t)table.size(),
-                        b.status_.data(), table.empty() ? nullptr : b.values_.data(),
-                        b.span_ ? b.image_.data() : nullptr) != BT_OK)
-        throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
+    // a small batch (parsePacket's one packet) on this thread: the device's round trip costs more
+    int rc = BT_OK;
+    if (n && n < hostBelow_)
+        rc = bt_extract_host(b.frames_.data(), b.lens_.data(), n, table.data(), (uint32_t)table.size(), b.status_.data(),
+                             table.empty() ? nullptr : b.values_.data(), b.span_ ? b.image_.data() : nullptr);
+    else if (n)
+        rc = bt_extract(ctx_, b.frames_.data(), b.lens_.data(), n, table.data(), (uint32_t)table.size(),
+                        b.status_.data(), table.empty() ? nullptr : b.values_.data(), b.span_ ? b.image_.data() : nullptr);
+    if (rc != BT_OK) throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     const uint64_t ok = (uint64_t)std::count(b.status_.begin(), b.status_.end(), (uint8_t)0);
     countParses(b.def_.name, ok, n - ok, us);

@@ -193,6 +193,13 @@ public:
     bool validatePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol);
     void setConfig(const parser::ProtocolParser::ParserConfig& config);
     const parser::ProtocolParser::ParserConfig& getConfig() const { return config_; }
+    // parsePacket / parsePacketMultipleProtocols and batches of fewer than hostBatchBelow()
+    // packets extract on the calling thread (bt_extract_host: the kernel's extractValue<T>
+    // decode) instead of paying a device round trip (~0.1 ms per bt_extract call). Default
+    // BEATRICE_GPU_HOST_BELOW, else kHostBelowDefault; 0 sends every call to the device.
+    static constexpr size_t kHostBelowDefault = 512;
+    void setHostBatchBelow(size_t n) { hostBelow_ = n; }
+    size_t hostBatchBelow() const { return hostBelow_; }
 
     // ---- text and bytes of a ParseResult (ProtocolParser.hpp:74-75, 84-89) ----
     // formatPacket: the reference's ParseResult::toJsonString / toXmlString / toCsvString /
@@ -240,6 +247,7 @@ private:
     void extract(GpuFieldBatch& b);
     void countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us);
     bt_ctx* ctx_ = nullptr;
+    size_t hostBelow_ = kHostBelowDefault;
     parser::ProtocolParser::ParserConfig config_;
     std::unordered_map<std::string, parser::ProtocolDefinition> protocols_;   // as the reference's protocols_
     std::unordered_map<std::string, std::function<bool(const std::vector<uint8_t>&, const parser::ParseResult&)>>

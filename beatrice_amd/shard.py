@@ -14,14 +14,50 @@ import numpy as np
 TILE = 64
 
 
-def shard_bounds(lengths: np.ndarray, world: int, by_bytes: bool = True):
+# The per-packet cost model: round_up(min(len, window), align) + fixed bytes. The default is
+# the device-resident strong-scaling case (header window + descriptor + 96-B record in HBM);
+# the in-process group weighs each call by what it moves (bt_group_cost, mirrored by
+# group_cost below).
+DEFAULT_COST = (128, 1, 8 + 96)
+
+
+def packet_cost(lengths, cost=DEFAULT_COST) -> np.ndarray:
+    window, align, fixed = cost
+    w = np.minimum(np.asarray(lengths, dtype=np.int64), window)
+    if align > 1:
+        w = (w + align - 1) // align * align
+    return w + fixed
+
+
+def group_cost(mapped: bool, records: bool, filters: bool, desc_bytes: int = 8, stage_bytes: int = 48):
+    """bt_group_cost (include/beatrice_gpu.h): what one packet costs a group member.
+    Host batches stage round_up(min(len, stage_bytes), 16) bytes (bt_host_stage_bytes: 48
+    filter-only, 112 with records, 176 with a GPU PAYLOAD slot), copy its descriptor up and
+    its 96-B bt_rec and decision byte back; mapped batches read the header window over the
+    member's PCIe link (the lean 48 B filter-only, the walk's 128 with records) and write
+    packed record slabs (~64 B) and the decision."""
+    if mapped:
+        return (128 if records else 48, 16, desc_bytes + (64 if records else 0) + (1 if filters else 0))
+    return (stage_bytes, 16, desc_bytes + (96 if records else 0) + (1 if filters else 0))
+
+
+def member_threads(members: int, usable: int, requested: int = 0) -> int:
+    """bt_group_thread_budget: host threads per group member. `requested` is the whole
+    group's budget (split evenly, 1..16 each); auto gives usable / members, 1..8 each."""
+    usable = max(usable, 1)
+    if requested:
+        return min(max(requested // members, 1), 16)
+    return min(max(usable // members, 1), 8)
+
+
+def shard_bounds(lengths: np.ndarray, world: int, by_bytes: bool = True, cost=DEFAULT_COST):
     """Contiguous [lo, hi) packet ranges, one per rank, tile-aligned."""
     n = len(lengths)
     if world <= 1 or n == 0:
         return [(0, n)] + [(n, n)] * max(0, world - 1)
     ntiles = (n + TILE - 1) // TILE
     if by_bytes:
-        cost = np.minimum(np.asarray(lengths, dtype=np.int64), 128) + 8 + 96
+        cost = packet_cost(lengths, cost)
         tile_cost = np.add.reduceat(cost, np.arange(0, n, TILE))
         cum = np.cumsum(tile_cost)
         targets = cum[-1] * np.arange(1, world) / world

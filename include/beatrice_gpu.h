@@ -75,7 +75,11 @@
 extern "C" {
 #endif
 
-#define BT_ABI_VERSION 1
+/* ABI history: 1 = round 1-3. 2 = round 4: a descriptor batch must state bt_batch.bytes
+ * (0 was "unbounded" before and is now BT_E_INVALID_ARGUMENT); bt_group_host_register /
+ * bt_group_parse_filter_mapped / bt_group_split_cost / bt_context_placement added. Hosts
+ * built against an older header should check bt_abi_version() >= the version they need. */
+#define BT_ABI_VERSION 2
 
 /* ---- status codes (values of beatrice::ErrorCode, reference include/beatrice/Error.hpp:11-26) */
 #define BT_OK                    0
@@ -336,12 +340,34 @@ int  bt_device_count(int* out);
 /* The context's device: its HIP ordinal and PCI bus id ("0000:05:00.0"; cap >= 16), so
  * that processes sharing a node can check they drive distinct GPUs. */
 int  bt_context_device(const bt_ctx* ctx, int* device, char* pci_bus_id, uint32_t cap);
+/* Where the context's host work runs: the host NUMA node closest to its device (HIP's
+ * hipDeviceAttributeHostNumaId, else the PCI function's sysfs numa_node; -1 unknown), how
+ * many CPUs of that node (in this process's affinity set) its pool workers are pinned to
+ * (0 = not pinned; BT_NUMA_PIN=0 turns pinning off), the pool's size, and the node of the
+ * host pipeline's pinned staging (-1 until a host batch allocated it). */
+typedef struct bt_placement {
+    int32_t  numa_node;
+    uint32_t pinned_cpus;
+    uint32_t pool_threads;
+    int32_t  staging_node;
+    uint32_t reserved[4];
+} bt_placement;
+int  bt_context_placement(bt_ctx* ctx, bt_placement* out);
+/* Host-only helpers: the CPUs of NUMA node `node` this process may use (*n = 0 if none or
+ * unknown; at most cap written), and the CPUs it may use at all (affinity set bounded by
+ * the cgroup v2 quota). */
+int  bt_node_cpus(int node, int32_t* cpus, uint32_t cap, uint32_t* n);
+uint32_t bt_usable_cpus(void);
 
 /* Compile the enabled filters: stable sort by priority (descending), parse each
  * expression once. The C++ adapter (beatrice_amd/host) passes filters already in
  * the reference's own evaluation order so ties match libstdc++ exactly. */
 int  bt_filter_compile(bt_ctx* ctx, const bt_filter_desc* filters, uint32_t n);
 int  bt_filter_program(const bt_ctx* ctx, bt_filter_slot* out, uint32_t cap, uint32_t* n_slots);
+/* The compiled program's PAYLOAD DFA tables (BT_K_PAYLOAD slot s: bytes [s.a, s.a + s.b) of
+ * the pool, a blob for bt_payload_dfa_eval): *bytes = the pool's size, min(cap, size) bytes
+ * copied to out. For hosts that evaluate small batches on the CPU with the same program. */
+int  bt_filter_dfa_pool(const bt_ctx* ctx, void* out, uint32_t cap, uint32_t* bytes);
 /* host-only helper: compile without a context (no device needed) */
 int  bt_filter_compile_host(const bt_filter_desc* filters, uint32_t n,
                             bt_filter_slot* out, uint32_t cap, uint32_t* n_slots);
@@ -510,6 +536,51 @@ int      bt_group_parse_filter_ptrs(bt_group* group, const uint8_t* const* frame
  * inner bound a multiple of 64, member k taking [bounds[k], bounds[k+1]); balanced by the
  * cost min(len, 128) + 8 + 96 bytes per packet (beatrice_amd/shard.py:shard_bounds). */
 int      bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* bounds);
+/* The same with a cost model: packet cost = round_up(min(len, window), align) + fixed.
+ * The group's calls weigh packets by what each call moves (bt_group_cost). */
+typedef struct bt_split_cost {
+    uint32_t window;               /* bytes of each frame the call reads / stages         */
+    uint32_t align;                /* ... rounded up to this (1 = exact)                  */
+    uint32_t fixed;                /* per-packet bytes independent of the length          */
+    uint32_t reserved;
+} bt_split_cost;
+int      bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
+                             uint32_t* bounds);
+/* The cost model a group call uses (mapped: bt_group_parse_filter_mapped, else the host
+ * batches), for a call that asks for records / filter outputs, with desc_bytes-byte
+ * descriptors (8 packed, 16 xdp_desc, 0 fixed stride):
+ *   host batches: window = bt_host_stage_bytes (48 / 112 / 176), align 16,
+ *                 fixed = desc_bytes + 96 (records, bt_rec D2H) + 1 (decision D2H)
+ *   mapped:       window = 128 with records (the walk's wide window) else 48 (the lean
+ *                 46-B first round), align 16, fixed = desc_bytes + 64 (records: packed
+ *                 slabs) + 1 (decision) — all of it PCIe traffic of the member's link. */
+int      bt_group_cost(bt_group* group, int mapped, int records, int filters, uint32_t desc_bytes,
+                       bt_split_cost* out);
+/* Host threads per member: `requested` (opts.host_threads, else BT_HOST_THREADS; 0 = auto)
+ * is the whole group's budget, split evenly (at least 1, at most 16 each); auto gives each
+ * member usable / members, at least 1 and at most 8 (one context alone: min(8, usable), the
+ * single-context default). Host only; bt_group_create applies it. */
+int      bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member);
+
+/* Zero-copy over the group (AF_XDP UMEM, TPACKET_V3 ring, output arrays): page-lock a host
+ * range once (portable, mapped) and map it into every member's device; each member reads
+ * it through its own alias over its own PCIe link. Ranges must not overlap. Unregister
+ * waits for every member's device first. */
+int      bt_group_host_register(bt_group* group, void* host, uint64_t bytes);
+int      bt_group_host_unregister(bt_group* group, void* host);
+/* bt_parse_filter_device over group-registered host memory, split across the members:
+ * `batch` and `out` hold HOST addresses. batch.base / batch.desc and out.records /
+ * out.verdict / out.decide must lie in ranges registered with bt_group_host_register;
+ * out.pass_idx / out.n_pass are written by the host and may be any host memory. The batch
+ * is split on 64-packet tiles by bt_group_cost(mapped) and member k runs its range
+ * [lo, hi) with its own alias of every buffer: descriptors from desc + lo (fixed stride:
+ * base + lo * stride), records at the range's tile (tiled: + lo / 64 * 6144 bytes, n_cap -
+ * lo; BT_OPT_RECORDS_AOS: + lo * 96; plane-major records cannot be split and are
+ * refused with more than one member), decisions at + lo, verdict words at + lo / 64. The
+ * pass list is built from the verdict words on the members' host threads (out.verdict, or
+ * the group's own registered words when the caller asked for none), in ascending order.
+ * Synchronous: every output is complete on return. */
+int      bt_group_parse_filter_mapped(bt_group* group, const bt_batch* batch, const bt_outputs* out);
 
 /* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
 int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);
@@ -628,6 +699,11 @@ int  bt_extract_device(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* f
 int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                 const bt_field_def* fields, uint32_t n_fields, uint8_t* status, uint64_t* values,
                 uint8_t* image);
+/* The same outputs computed on the calling thread, no device: for batches too small to pay
+ * for a device round trip (GpuProtocolParser::parsePacket of one packet; ≈ 0.1 ms per
+ * bt_extract call). extractValue<T>'s bits exactly as bt_extract_tile decodes them. */
+int  bt_extract_host(const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,
+                     uint32_t n_fields, uint8_t* status, uint64_t* values, uint8_t* image);
 /* bt_extract_device `iters` times on the context's stream, each launch timed by an event
  * pair from its own dispatch packet (bt_timing.main_* = the extraction kernel). For
  * benchmarks; the outputs are those of the last launch. BT_E_INVALID_ARGUMENT for an empty

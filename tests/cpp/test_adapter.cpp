@@ -703,6 +703,135 @@ static bool plugin_case(const Capture& cap, const char* so) {
     return true;
 }
 
+// ---- small calls: a single packet / a small batch is decided (parsed) on the host -------
+// GpuPacketFilter::applyFilters(const Packet&) and batches below hostBatchBelow() run the
+// compiled program on the calling thread; GpuProtocolParser::parsePacket extracts on it.
+// Both branches (host, and the device with setHostBatchBelow(0)) against the reference.
+static Capture load_capture(const char* path) {   // u64 n, n x u64 desc, u64 bytes, data
+    Capture c;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return c;
+    uint64_t n = 0, nb = 0;
+    if (std::fread(&n, 8, 1, f) == 1) {
+        c.desc.resize(n);
+        if (std::fread(c.desc.data(), 8, n, f) == n && std::fread(&nb, 8, 1, f) == 1) {
+            c.data.resize(nb + 64);
+            if (std::fread(c.data.data(), 1, nb, f) != nb) c.desc.clear();
+        }
+    }
+    std::fclose(f);
+    for (uint64_t d : c.desc) {
+        const uint8_t* fr = c.data.data() + (d & 0xFFFFFFFFFFFFull);
+        c.packets.emplace_back(std::shared_ptr<const uint8_t[]>(fr, [](const uint8_t*) {}), (size_t)(d >> 48));
+    }
+    return c;
+}
+
+static bool small_filter_case(const char* label, const Capture& cap, const std::vector<Spec>& specs) {
+    PacketFilter ref;
+    GpuPacketFilter host(0), dev(0);   // host: default threshold; dev: every call on the device
+    dev.setHostBatchBelow(0);
+    install(ref, specs);
+    install(host, specs);
+    install(dev, specs);
+    CHECK(host.hostBatchBelow() > 100, "%s: host threshold %zu", label, host.hostBatchBelow());
+    size_t threw = 0;
+    for (size_t i = 0; i < cap.packets.size(); ++i) {   // one packet per call
+        PacketFilter::FilterResult a, b, c;
+        std::exception_ptr ea, eb, ec;
+        try { a = ref.applyFilters(cap.packets[i]); } catch (...) { ea = std::current_exception(); }
+        try { b = host.applyFilters(cap.packets[i]); } catch (...) { eb = std::current_exception(); }
+        if (i % 7 == 0) {   // the device branch is a round trip per packet: a sample
+            try { c = dev.applyFilters(cap.packets[i]); } catch (...) { ec = std::current_exception(); }
+            CHECK((bool)ea == (bool)ec && (!ea || what_kind(ea) == what_kind(ec)) &&
+                      (ea || (a.passed == c.passed && a.filterName == c.filterName && a.reason == c.reason)),
+                  "%s: device branch, packet %zu", label, i);
+        }
+        CHECK((bool)ea == (bool)eb, "%s: packet %zu exception ref=%d host=%d", label, i, (bool)ea, (bool)eb);
+        if (ea) {
+            CHECK(what_kind(ea) == what_kind(eb), "%s: packet %zu %s vs %s", label, i, what_kind(ea).c_str(),
+                  what_kind(eb).c_str());
+            ++threw;
+            continue;
+        }
+        CHECK(a.passed == b.passed && a.filterName == b.filterName && a.reason == b.reason,
+              "%s: packet %zu ref=(%d,%s) host=(%d,%s)", label, i, a.passed, a.filterName.c_str(), b.passed,
+              b.filterName.c_str());
+    }
+    auto sa = ref.getStats(), sb = host.getStats();
+    CHECK(sa.packetsProcessed == sb.packetsProcessed && sa.packetsPassed == sb.packetsPassed &&
+              sa.packetsDropped == sb.packetsDropped && sa.filterCounts == sb.filterCounts,
+          "%s: per-packet stats differ (processed %lu/%lu)", label, (unsigned long)sa.packetsProcessed,
+          (unsigned long)sb.packetsProcessed);
+    // small batches (host) and the same batches on the device
+    for (size_t lo = 0; lo < cap.packets.size(); lo += 100) {
+        const std::vector<Packet> part(cap.packets.begin() + lo,
+                                       cap.packets.begin() + std::min(cap.packets.size(), lo + 100));
+        std::vector<PacketFilter::FilterResult> a, b, c;
+        std::exception_ptr ea, eb, ec;
+        try { a = ref.applyFilters(part); } catch (...) { ea = std::current_exception(); }
+        try { b = host.applyFilters(part); } catch (...) { eb = std::current_exception(); }
+        try { c = dev.applyFilters(part); } catch (...) { ec = std::current_exception(); }
+        CHECK((bool)ea == (bool)eb && (bool)ea == (bool)ec, "%s: batch at %zu exceptions", label, lo);
+        if (ea) {
+            CHECK(what_kind(ea) == what_kind(eb) && what_kind(ea) == what_kind(ec), "%s: batch at %zu exception kind",
+                  label, lo);
+            continue;
+        }
+        for (size_t i = 0; i < a.size(); ++i)
+            CHECK(a[i].passed == b[i].passed && a[i].filterName == b[i].filterName && a[i].passed == c[i].passed &&
+                      a[i].filterName == c[i].filterName,
+                  "%s: batch at %zu packet %zu", label, lo, i);
+        GpuPacketFilter::Verdicts v = host.classify(part), w = dev.classify(part);
+        CHECK(v.decide == w.decide && v.pass_idx == w.pass_idx, "%s: classify host/device at %zu", label, lo);
+    }
+    sa = ref.getStats();
+    sb = host.getStats();
+    CHECK(sa.packetsProcessed == sb.packetsProcessed && sa.packetsPassed == sb.packetsPassed &&
+              sa.filterCounts == sb.filterCounts,
+          "%s: stats after batches differ", label);
+    std::printf("ok   small   %-22s %zu single-packet calls (%zu threw), batches of 100 on host and device\n", label,
+                cap.packets.size(), threw);
+    return true;
+}
+
+static bool small_parser_case(const char* label, const Capture& cap) {
+    using namespace beatrice::parser;
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    ProtocolParser ref(cfg);
+    beatrice::gpu::GpuProtocolParser host(cfg, 0), dev(cfg, 0);
+    dev.setHostBatchBelow(0);
+    for (auto p : {BuiltinProtocols::createEthernetProtocol(), BuiltinProtocols::createVLANProtocol(),
+                   BuiltinProtocols::createIPv4Protocol(), BuiltinProtocols::createIPv6Protocol(),
+                   BuiltinProtocols::createTCPProtocol(), BuiltinProtocols::createUDPProtocol(),
+                   BuiltinProtocols::createICMPProtocol()}) {
+        ref.registerProtocol(p);
+        host.registerProtocol(p);
+        dev.registerProtocol(p);
+    }
+    auto walk = host.parseBatch(cap.packets);
+    size_t nres = 0;
+    for (size_t i = 0; i < cap.packets.size(); ++i) {
+        const uint8_t* f = cap.packets[i].data();
+        const size_t len = cap.packets[i].length();
+        for (const auto& L : walk.layers(i)) {   // parsePacket(slice, name) per walked layer
+            const std::vector<uint8_t> v(f + L.offset, f + len);
+            if (!same_result(label, i, ref.parsePacket(v, L.name), host.parsePacket(v, L.name))) return false;
+            if (i % 5 == 0 && !same_result(label, i, ref.parsePacket(v, L.name), dev.parsePacket(v, L.name))) return false;
+            ++nres;
+        }
+        const std::vector<uint8_t> v(f, f + len);   // every protocol over the whole frame (too-short ones too)
+        auto w = ref.parsePacketMultipleProtocols(v), g = host.parsePacketMultipleProtocols(v);
+        CHECK(w.size() == g.size(), "%s: multiple size", label);
+        for (size_t k = 0; k < w.size(); ++k)
+            if (!same_result(label, i, w[k], g[k])) return false;
+    }
+    std::printf("ok   small   parser %-15s %zu parsePacket(slice, name) calls on the host, a fifth on the device\n",
+                label, nres);
+    return true;
+}
+
 // A crash names where it happened (the test's stdout is a pipe, so its buffered lines are lost).
 static void on_fatal(int sig) {
     void* frames[64];
@@ -716,8 +845,32 @@ int main(int argc, char** argv) {
     std::setvbuf(stdout, nullptr, _IOLBF, 0);
     signal(SIGSEGV, on_fatal);
     signal(SIGABRT, on_fatal);
-    const char* plugin_so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
     using T = PacketFilter::FilterType;
+    if (argc > 2 && std::string(argv[1]) == "small") {   // test_adapter small <capture.bin> <label>
+        const Capture cap = load_capture(argv[2]);
+        const char* label = argc > 3 ? argv[3] : argv[2];
+        if (cap.packets.empty()) {
+            std::printf("FAILED: cannot read %s\n", argv[2]);
+            return 1;
+        }
+        const std::vector<Spec> sets[] = {
+            {{"proto", T::PROTOCOL, "udp", 3, true, 0}, {"net", T::IP_RANGE, "10.0.0.0/8", 2, true, 0},
+             {"ports", T::PORT_RANGE, "1000-2000", 1, true, 0}},
+            {{"tcp", T::PROTOCOL, "tcp", 3, true, 0}, {"get", T::PAYLOAD, "GET|HTTP", 2, true, 0},
+             {"cust", T::CUSTOM, "", 2, true, 1}, {"ports", T::PORT_RANGE, "0-2047", 1, true, 0}},
+            {{"a", T::PORT_RANGE, "0-1023", 1, true, 0}, {"zeta", T::BPF, "tcp", 1, true, 0},
+             {"q", T::PROTOCOL, "ip", 1, true, 0}, {"hi", T::BPF, "udp tcp", 5, true, 0}},
+            {{"udp", T::BPF, "udp", 2, true, 0}, {"bad", T::IP_RANGE, "10.0.0.0/x", 1, true, 0}},
+            {{"c", T::CUSTOM, "", 1, true, 3}, {"re", T::PAYLOAD, "(a|b)+c\\d", 2, true, 0}},
+            {}};
+        const char* names[] = {"headline", "payload+custom", "ties", "throw", "custom-throw+dfa", "none"};
+        bool ok = true;
+        for (int k = 0; k < 6; ++k) ok &= small_filter_case((std::string(label) + "/" + names[k]).c_str(), cap, sets[k]);
+        ok &= small_parser_case(label, cap);
+        std::printf("%s (%d failures)\n", ok && !g_fail ? "ALL OK" : "FAILED", g_fail);
+        return ok && !g_fail ? 0 : 1;
+    }
+    const char* plugin_so = argc > 1 ? argv[1] : "beatrice_amd/libgpu_parse_filter_plugin.so";
     Capture c3 = capture(3, 20000, 0x5EED0003), c4 = capture(4, 12000, 0x5EED0004), fz = capture(9, 30000, 0x5EED0009);
     const std::vector<Spec> headline = {{"proto", T::PROTOCOL, "udp", 3, true, 0},
                                         {"net", T::IP_RANGE, "10.0.0.0/8", 2, true, 0},

@@ -27,6 +27,7 @@
 #include <fstream>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "beatrice/PacketFilter.hpp"
@@ -45,7 +46,7 @@ using beatrice::gpu::GpuPacketFilter;
 using beatrice::gpu::GpuTpacketStage;
 using beatrice::gpu::TpacketV3Ring;
 
-static int g_fail = 0;
+static std::atomic<int> g_fail{0};
 #define CHECK(cond, ...)                                                  \
     do {                                                                  \
         if (!(cond)) {                                                    \
@@ -170,13 +171,37 @@ static std::string kind_of(const std::exception_ptr& e) {
     }
 }
 
+static const std::vector<Spec> kHeadline = {{"proto", PacketFilter::FilterType::PROTOCOL, "udp", 3, 0},
+                                            {"net", PacketFilter::FilterType::IP_RANGE, "10.0.0.0/8", 2, 0},
+                                            {"ports", PacketFilter::FilterType::PORT_RANGE, "1000-2000", 1, 0}};
+static const std::vector<Spec> kLoopback = {{"bpf", PacketFilter::FilterType::BPF, "udp", 4, 0},
+                                            {"lo", PacketFilter::FilterType::IP_RANGE, "127.0.0.0/8", 3, 0},
+                                            {"pay", PacketFilter::FilterType::PAYLOAD, "v6|btc|\\x01", 2, 0},
+                                            {"odd", PacketFilter::FilterType::CUSTOM, "", 1, 1}};
+static const std::vector<Spec> kHost = {{"tcp", PacketFilter::FilterType::BPF, "tcp", 3, 0},
+                                        {"get", PacketFilter::FilterType::PAYLOAD, "GET|HTTP", 2, 0},
+                                        {"len", PacketFilter::FilterType::CUSTOM, "", 1, 1}};
+static const std::vector<Spec> kThrow = {{"udp", PacketFilter::FilterType::PROTOCOL, "udp", 2, 0},
+                                         {"bad", PacketFilter::FilterType::PORT_RANGE, "1000-", 1, 0}};
+
+// A filter over `members` contexts of device 0 (a group sharing the one GPU of the test box:
+// each member still has its own streams and host threads and reads its range of every batch).
+static bt_opts shared_opts() {
+    bt_opts o{};
+    o.flags = BT_OPT_GROUP_SHARED_DEVICE;
+    return o;
+}
+
 static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32_t nb, const std::vector<Spec>& specs,
-                       uint32_t maxBlocks, bool records, bool gather = false, uint32_t inPlaceEvery = 0) {
+                       uint32_t maxBlocks, bool records, bool gather = false, uint32_t inPlaceEvery = 0,
+                       uint32_t members = 1) {
     // fresh copy of the image: the stage hands blocks back (status -> kernel)
     std::vector<uint8_t> mem(ring_mem, ring_mem + (size_t)bs * nb);
     TpacketV3Ring ring;
     CHECK(ring.attach(mem.data(), bs, nb).isSuccess(), "%s: attach", label);
-    GpuPacketFilter gpu(0);
+    const bt_opts so = shared_opts();
+    GpuPacketFilter gpu(std::vector<int>(members, 0), &so);
+    CHECK(gpu.deviceCount() == members, "%s: %u members", label, gpu.deviceCount());
     PacketFilter ref;
     install(gpu, specs);
     install(ref, specs);
@@ -271,23 +296,65 @@ static bool stage_case(const char* label, uint8_t* ring_mem, uint32_t bs, uint32
           (unsigned long)sb.packetsProcessed, (unsigned long)sa.packetsPassed, (unsigned long)sb.packetsPassed);
     CHECK(total > 0, "%s: nothing drained", label);
     CHECK(!gather || gathered > 0, "%s: no batch was gathered", label);
-    std::printf("ok   stage %-20s %lu frames in %u batches (%u gathered), %lu passed%s\n", label, (unsigned long)total,
-                batches, gathered, (unsigned long)passed, records ? ", records equal" : "");
+    std::printf("ok   stage %-24s %lu frames in %u batches (%u gathered), %lu passed%s, %u device(s)\n", label,
+                (unsigned long)total, batches, gathered, (unsigned long)passed, records ? ", records equal" : "",
+                members);
     return true;
 }
 
-static const std::vector<Spec> kHeadline = {{"proto", PacketFilter::FilterType::PROTOCOL, "udp", 3, 0},
-                                            {"net", PacketFilter::FilterType::IP_RANGE, "10.0.0.0/8", 2, 0},
-                                            {"ports", PacketFilter::FilterType::PORT_RANGE, "1000-2000", 1, 0}};
-static const std::vector<Spec> kLoopback = {{"bpf", PacketFilter::FilterType::BPF, "udp", 4, 0},
-                                            {"lo", PacketFilter::FilterType::IP_RANGE, "127.0.0.0/8", 3, 0},
-                                            {"pay", PacketFilter::FilterType::PAYLOAD, "v6|btc|\\x01", 2, 0},
-                                            {"odd", PacketFilter::FilterType::CUSTOM, "", 1, 1}};
-static const std::vector<Spec> kHost = {{"tcp", PacketFilter::FilterType::BPF, "tcp", 3, 0},
-                                        {"get", PacketFilter::FilterType::PAYLOAD, "GET|HTTP", 2, 0},
-                                        {"len", PacketFilter::FilterType::CUSTOM, "", 1, 1}};
-static const std::vector<Spec> kThrow = {{"udp", PacketFilter::FilterType::PROTOCOL, "udp", 2, 0},
-                                         {"bad", PacketFilter::FilterType::PORT_RANGE, "1000-", 1, 0}};
+// Per-GPU ring sharding: PACKET_FANOUT_HASH gives each GPU worker its own ring, a
+// flow always landing in the same one. Here a capture is split by the kernel's flow hash
+// stand-in (the 5-tuple's symmetric sum) into `rings` ring images, each drained by its own
+// filter + GpuTpacketStage on its own thread (its own context on the test box's one GPU),
+// and every ring's decisions are checked against the reference PacketFilter; together the
+// rings must see every frame once.
+static uint32_t flow_of(const uint8_t* f, uint32_t len) {
+    if (len < 38 || f[12] != 0x08 || f[13] != 0x00) return 0;
+    uint32_t h = (uint32_t)f[23];
+    for (int i = 26; i < 34; ++i) h += f[i];
+    for (int i = 34; i < 38; ++i) h += f[i];
+    return h * 2654435761u;
+}
+
+static bool stage_fanout(uint32_t rings) {
+    const uint32_t n = 200000, bs = 1u << 20;
+    std::vector<uint64_t> desc(n);
+    std::vector<uint8_t> data(bt_synth_layout(3, n, 91, desc.data()));
+    bt_synth_fill(3, n, 91, desc.data(), data.data(), 8);
+    // per ring: the frames of its flows, packed in capture order
+    std::vector<std::vector<uint64_t>> part(rings);
+    std::vector<std::vector<uint8_t>> bytes(rings);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* f = data.data() + BT_DESC_OFF(desc[i]);
+        const uint32_t len = (uint32_t)BT_DESC_LEN(desc[i]);
+        const uint32_t r = flow_of(f, len) % rings;
+        part[r].push_back(BT_DESC(bytes[r].size(), len));
+        bytes[r].insert(bytes[r].end(), f, f + len);
+    }
+    std::vector<std::vector<uint8_t>> ringmem(rings);
+    std::vector<uint64_t> used(rings, 0);
+    for (uint32_t r = 0; r < rings; ++r) {
+        bt_synth_tpv3_pack(bytes[r].data(), part[r].data(), part[r].size(), bs, nullptr, 1ull << 40, nullptr, &used[r]);
+        ringmem[r].resize(used[r] * bs);
+        CHECK(bt_synth_tpv3_pack(bytes[r].data(), part[r].data(), part[r].size(), bs, ringmem[r].data(), used[r], nullptr,
+                                 &used[r]) == part[r].size(), "fanout: ring %u packing", r);
+    }
+    std::vector<int> ok(rings, 0);
+    std::vector<std::thread> th;
+    for (uint32_t r = 0; r < rings; ++r)
+        th.emplace_back([&, r] {
+            char label[64];
+            std::snprintf(label, sizeof(label), "fanout %u/%u", r, rings);
+            ok[r] = stage_case(label, ringmem[r].data(), bs, (uint32_t)used[r], kHeadline, 8, r == 0);
+        });
+    for (auto& t : th) t.join();
+    size_t total = 0;
+    for (uint32_t r = 0; r < rings; ++r) total += part[r].size();
+    CHECK(total == n, "fanout: %zu frames over the rings, %u captured", total, n);
+    for (uint32_t r = 0; r < rings; ++r) CHECK(ok[r], "fanout: ring %u", r);
+    std::printf("ok   fanout  %u rings, one stage + context each, %u frames once each\n", rings, n);
+    return true;
+}
 
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "";
@@ -310,6 +377,13 @@ int main(int argc, char** argv) {
         stage_case("lo/headline gathered", img.data(), bs, nb, kHeadline, 1, true, true);
         stage_case("lo/payload+custom g", img.data(), bs, nb, kLoopback, 2, false, true, 2);
         stage_case("lo/throws gathered", img.data(), bs, nb, kThrow, 1, false, true);
+        stage_case("lo/headline 2 dev", img.data(), bs, nb, kHeadline, 4, true, false, 0, 2);
+        stage_case("lo/payload+custom 3 dev", img.data(), bs, nb, kLoopback, 4, false, false, 0, 3);
+        stage_case("lo/throws 2 dev", img.data(), bs, nb, kThrow, 4, false, false, 0, 2);
+        stage_case("lo/headline g 3 dev", img.data(), bs, nb, kHeadline, 4, true, true, 2, 3);
+    } else if (mode == "stage-fanout") {
+        stage_fanout(2);
+        stage_fanout(3);
     } else if (mode == "stage-synth") {
         const uint32_t n = 300000, bs = 1u << 20;
         std::vector<uint64_t> desc(n);
@@ -327,12 +401,17 @@ int main(int argc, char** argv) {
         stage_case("c3/host-slots", ring.data(), bs, (uint32_t)used, kHost, 32, false);
         stage_case("c3/headline gathered", ring.data(), bs, (uint32_t)used, kHeadline, 8, true, true);
         stage_case("c3/host-slots mixed", ring.data(), bs, (uint32_t)used, kHost, 8, false, true, 3);
+        stage_case("c3/headline 2 dev", ring.data(), bs, (uint32_t)used, kHeadline, 8, true, false, 0, 2);
+        stage_case("c3/headline 3 dev", ring.data(), bs, (uint32_t)used, kHeadline, 16, true, false, 0, 3);
+        stage_case("c3/host-slots 2 dev", ring.data(), bs, (uint32_t)used, kHost, 32, false, false, 0, 2);
+        stage_case("c3/headline g 2 dev", ring.data(), bs, (uint32_t)used, kHeadline, 8, true, true, 2, 2);
     } else {
-        std::printf("usage: test_capture backend | stage <ring.bin> <block_size> <n_blocks> | stage-synth\n");
+        std::printf("usage: test_capture backend | stage <ring.bin> <block_size> <n_blocks> | stage-synth | "
+                    "stage-fanout\n");
         return 2;
     }
     if (g_fail) {
-        std::printf("%d FAILED\n", g_fail);
+        std::printf("%d FAILED\n", g_fail.load());
         return 1;
     }
     std::printf("ALL OK\n");

@@ -75,3 +75,27 @@ def layout_violations(ring: np.ndarray, block_size: int, n_blocks: int):
             if blk_len != off + ((mac + snap + 7) & ~7):
                 bad.append((b, "blk_len", blk_len))
     return bad
+
+
+def umem_capture(frames_data, desc, chunk=2048, shuffle_seed=5):
+    """An AF_XDP-style UMEM (anonymous mmap, numBuffers x bufferSize chunks, headroom 0,
+    reference src/AF_XDPBackend.cpp:683-720) holding each frame at the start of a chunk,
+    plus the RX ring's xdp_desc {addr, len, options} (shuffled chunk order, as after
+    fill-ring recycling)."""
+    import mmap
+
+    from beatrice_amd import synth
+    n = len(desc)
+    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+    assert ln.max() <= chunk
+    mm = mmap.mmap(-1, n * chunk)
+    umem = np.frombuffer(mm, dtype=np.uint8)
+    order = np.random.default_rng(shuffle_seed).permutation(n)
+    for i in range(n):
+        c = order[i] * chunk
+        umem[c:c + ln[i]] = frames_data[off[i]:off[i] + ln[i]]
+    xdp = np.zeros((n, 2), np.uint64)
+    xdp[:, 0] = order.astype(np.uint64) * chunk
+    xdp[:, 1] = ln.astype(np.uint64)               # len in the low 32 bits, options = 0
+    packed = synth.make_desc(order.astype(np.uint64) * chunk, ln)
+    return mm, umem, xdp, packed

@@ -30,7 +30,8 @@ def test_every_declared_symbol_is_exported():
 
 
 def test_abi_version_and_struct_sizes():
-    assert abi.lib().bt_abi_version() == 1
+    assert abi.lib().bt_abi_version() == abi.ABI_VERSION == 2
+    assert ctypes.sizeof(abi.SplitCost) == 16 and ctypes.sizeof(abi.Placement) == 32
     assert ctypes.sizeof(abi.Opts) == 32
     assert ctypes.sizeof(abi.Batch) == 40
     assert ctypes.sizeof(abi.Outputs) == 48

@@ -40,6 +40,7 @@ def test_plugin_sink_records_equal_reference_goldens(cap, tmp_path):
     """BEATRICE_GPU_RECORDS=1: the plugin's sink hands out each packet's parse record from
     the same kernel pass; tests/cpp/test_plugin compares them with the golden records the
     compiled reference's ProtocolParser produced for the same frames."""
+    import numpy as np
     from conftest import load_golden
     g, _ = load_golden(cap)
     paths = []
@@ -54,3 +55,25 @@ def test_plugin_sink_records_equal_reference_goldens(cap, tmp_path):
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "ALL OK" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["c3", "c4", "edge"])
+def test_small_calls_host_and_device_branches(cap, tmp_path):
+    """Single-packet applyFilters / small batches / parsePacket(slice, name): the host branch
+    (the compiled program and extractor on the calling thread) and the device branch
+    (setHostBatchBelow(0)) against the compiled reference, on the golden captures."""
+    import numpy as np
+    from conftest import load_golden
+    g, _ = load_golden(cap)
+    desc = np.ascontiguousarray(g["desc"], dtype=np.uint64)
+    data = np.ascontiguousarray(g["data"], dtype=np.uint8)
+    path = tmp_path / f"{cap}.bin"
+    with open(path, "wb") as fh:
+        fh.write(np.uint64(len(desc)).tobytes())
+        fh.write(desc.tobytes())
+        fh.write(np.uint64(data.nbytes).tobytes())
+        fh.write(data.tobytes())
+    r = subprocess.run([BIN, "small", str(path), cap], capture_output=True, text=True, timeout=600, cwd=ROOT)
+    print(r.stdout[-4000:])
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]

@@ -48,3 +48,32 @@ def test_span_is_get_total_length():
     with pytest.raises(abi.BtError):   # BOOLEAN of length 0: the reference reads fieldData[0] of an empty vector
         abi.proto_span([(0, 0, abi.FT_BOOLEAN, 0)])
     assert abi.proto_span([(70000, 4, abi.FT_UINT32, 2)]) == 70004
+
+
+@pytest.mark.parametrize("name", list(MAN["tables"]))
+def test_host_extractor_matches_reference(name):
+    """bt_extract_host (the product's small-batch path for GpuProtocolParser::parsePacket, no
+    device) against the compiled reference's goldens: status, extractValue<T> bits and the
+    field bytes of every frame."""
+    import ctypes
+    t = MAN["tables"][name]
+    n = MAN["n"]
+    data, desc = G["data"], G["desc"][:n]
+    off, ln = (desc & np.uint64(0xFFFFFFFFFFFF)).astype(np.int64), (desc >> np.uint64(48)).astype(np.int64)
+    bufs = [np.ascontiguousarray(data[o:o + l]) if l else np.zeros(1, np.uint8) for o, l in zip(off, ln)]
+    ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    lens = ln.astype(np.uint32)
+    arr, nf = abi.field_table(t)
+    span = abi.proto_span(t)
+    span = span if span <= 0xFFFF else 0
+    st = np.zeros(n, np.uint8)
+    val = np.zeros(max(1, nf * n), np.uint64)
+    img = np.zeros(max(1, n * span), np.uint8)
+    lib = abi.lib()
+    rc = lib.bt_extract_host(ptrs, lens.ctypes.data, n, arr, nf, st.ctypes.data,
+                             val.ctypes.data if nf else None, img.ctypes.data if span else None)
+    assert rc == 0
+    assert np.array_equal(st, G[f"status__{name}"]), name
+    assert np.array_equal(val[:nf * n].reshape(nf, n), G[f"values__{name}"]), name
+    fb = ol.field_bytes_of_image(img[:n * span].reshape(n, span), t) if span else np.zeros((n, 0), np.uint8)
+    assert np.array_equal(fb, G[f"fb__{name}"]), name

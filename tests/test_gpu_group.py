@@ -86,3 +86,217 @@ def test_group_edge_sizes_and_errors():
     with pytest.raises(abi.BtError) as e:
         abi.Group([0, 0])                  # a device twice without the test flag
     assert "listed twice" in str(e.value)
+
+
+# ---- zero-copy over the group (bt_group_host_register + bt_group_parse_filter_mapped) --------
+
+C3_SET = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+          {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+          {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True, verdict=True, pass_list=True):
+    """Registers the batch and the device-written outputs with the group, runs the mapped call,
+    unregisters. Returns the outputs (records still in the tiled device layout)."""
+    tiles = max(1, (n + 63) // 64)
+    h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
+    h_dec = np.zeros(tiles * 64, np.uint8)
+    h_ver = np.zeros(tiles, np.uint64) if verdict else None
+    pidx = np.full(max(n, 1), 0xFFFFFFFF, np.uint32)
+    npass = np.zeros(1, np.uint32)
+    held = [a for a in (base, desc, h_rec, h_dec, h_ver) if a is not None]
+    for a in held:
+        grp.register(a)
+    try:
+        batch = abi.Batch(_ptr(base), _ptr(desc), stride, n, base.nbytes, fmt, 0)
+        outs = abi.Outputs(_ptr(h_rec), n, _ptr(h_ver), _ptr(h_dec), _ptr(pidx) if pass_list else None,
+                           npass.ctypes.data)
+        grp.run_mapped(batch, outs)
+    finally:
+        for a in held:
+            grp.unregister(a)
+    return {"rec_tiled": h_rec, "records": abi.untile_records(h_rec, n) if records else None,
+            "decide": h_dec[:n], "verdict": h_ver, "pass_idx": pidx[:int(npass[0])], "n_pass": int(npass[0])}
+
+
+def _single_zero_copy(ctx, base, desc, n, fmt, filters):
+    """The same batch through one context's bt_parse_filter_device (round 3's zero-copy path)."""
+    ctx.compile(filters)
+    tiles = max(1, (n + 63) // 64)
+    h_rec = np.zeros(tiles * 6144, np.uint8)
+    h_dec = np.zeros(tiles * 64, np.uint8)
+    h_ver = np.zeros(tiles, np.uint64)
+    held = [base, desc, h_rec, h_dec, h_ver]
+    dev = [ctx.register(a) for a in held]
+    try:
+        ctx.run_device(abi.Batch(dev[0], dev[1], 0, n, base.nbytes, fmt, 0),
+                       abi.Outputs(dev[2], n, dev[4], dev[3], None, None))
+        ctx.synchronize()
+    finally:
+        for a in held:
+            ctx.unregister(a)
+    return h_rec, h_dec[:n], h_ver
+
+
+def _check_filter(out, dec, n):
+    assert np.array_equal(out["decide"], dec)
+    bits = (dec >> 6) == 0
+    if out["verdict"] is not None:
+        vb = np.unpackbits(out["verdict"].view(np.uint8), bitorder="little")
+        assert np.array_equal(vb[:n].astype(bool), bits) and not vb[n:].any()
+    exp = np.nonzero(bits)[0].astype(np.uint32)
+    assert out["n_pass"] == len(exp)
+    assert np.array_equal(out["pass_idx"], exp)
+
+
+@pytest.mark.parametrize("members", [1, 2, 3])
+def test_group_mapped_umem_xdp_equals_oracle_and_single_context(members):
+    """SURVEY §8(f) rank 1 over several devices: an AF_XDP UMEM and its xdp_desc RX ring
+    registered once with the group; each member reads its range of the ring in place."""
+    from ring_util import umem_capture
+    n = 40000
+    data, desc = synth.capture(synth.C3, n, seed=0x51)
+    mm, umem, xdp, packed = umem_capture(data, desc)
+    grp = _group(members)
+    try:
+        grp.compile(C3_SET)
+        out = _run_mapped(grp, umem, xdp, n, fmt=abi.DESC_XDP)
+        nov = _run_mapped(grp, umem, xdp, n, fmt=abi.DESC_XDP, records=False, verdict=False)  # scratch verdict
+        nop = _run_mapped(grp, umem, xdp, n, fmt=abi.DESC_XDP, records=False, pass_list=False)
+    finally:
+        grp.close()
+    rec, dec, npass = ol.oracle_run(umem, packed, n, C3_SET)
+    assert np.array_equal(out["records"], rec)
+    _check_filter(out, dec, n)
+    _check_filter(nov, dec, n)
+    assert np.array_equal(nop["decide"], dec) and nop["n_pass"] == npass and not nop["pass_idx"].size
+    ctx = abi.Context(0)
+    try:
+        s_rec, s_dec, s_ver = _single_zero_copy(ctx, umem, xdp, n, abi.DESC_XDP, C3_SET)
+    finally:
+        ctx.close()
+    assert np.array_equal(out["rec_tiled"], s_rec), "tiled record bytes differ from the single-context run"
+    assert np.array_equal(out["decide"], s_dec) and np.array_equal(out["verdict"], s_ver)
+    del umem
+    mm.close()
+
+
+@pytest.mark.parametrize("members", [2, 3])
+@pytest.mark.parametrize("cap", ["c4", "edge", "http"])
+def test_group_mapped_fixture_matches_reference(cap, members):
+    """The reference fixtures read in place by 2 / 3 members: records + decisions against the
+    compiled reference, with a GPU PAYLOAD slot on the http capture."""
+    g, man = load_golden(cap)
+    sets = ["c3"] + (["payload_re_0", "payload_chain"] if cap == "http" else [])
+    data, desc = np.ascontiguousarray(g["data"]), np.ascontiguousarray(g["desc"], dtype=np.uint64)
+    n = len(desc)
+    for s in sets:
+        filters = man["filter_sets"][s]
+        grp = _group(members)
+        try:
+            grp.compile(filters)
+            out = _run_mapped(grp, data, desc, n)
+        finally:
+            grp.close()
+        assert np.array_equal(out["records"], g["rec"])
+        compare_decisions(out["decide"], g[f"code__{s}"], g[f"src__{s}"], filters, where=f"mapped{members}/{cap}/{s}")
+
+
+@pytest.mark.parametrize("members", [2, 3])
+def test_group_mapped_kernel_written_ring(members):
+    """The kernel-written TPACKET_V3 ring (tests/golden/ring_lo.npz) registered with the group and
+    walked into ring-relative descriptors: each member reads its frames in place."""
+    import json
+    import os
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    bs, nb = (int(x) for x in z["geometry"])
+    ring = z["ring"].copy()
+    desc, taken = abi.ring_walk_tpv3(ring, bs, nb)
+    assert taken == nb and np.array_equal(desc, z["desc"])
+    n = len(desc)
+    for k, s in enumerate(man["rings"]["ring_lo"]["filter_sets"]):
+        filters = man["filter_sets"][s]
+        grp = _group(members)
+        try:
+            grp.compile(filters)
+            out = _run_mapped(grp, ring, desc, n, records=(k == 0))
+        finally:
+            grp.close()
+        if k == 0:
+            assert np.array_equal(out["records"], z["rec"])
+        compare_decisions(out["decide"], z[f"code__{s}"], z[f"src__{s}"], filters, where=f"ring_lo/mapped{members}/{s}")
+        bits = np.unpackbits(out["verdict"].view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(bits, (out["decide"] >> 6) == 0)
+
+
+def test_group_mapped_fixed_stride_and_edges():
+    """Fixed-stride 64-B frames (C2) split evenly by tiles, n not a tile multiple, fewer tiles
+    than members, n = 0."""
+    grp = _group(3)
+    try:
+        grp.compile(C3_SET)
+        for n in (0, 1, 65, 129, 100003):
+            buf, desc = synth.capture(synth.C2, max(n, 1), seed=n + 1)
+            assert np.array_equal(synth.desc_off(desc), np.arange(max(n, 1)) * 64)
+            buf = np.ascontiguousarray(buf[:max(n, 1) * 64])
+            out = _run_mapped(grp, buf, None, n, stride=64)
+            if n == 0:
+                assert out["n_pass"] == 0
+                continue
+            rec, dec, _ = ol.oracle_run(buf, desc[:n], n, C3_SET)
+            assert np.array_equal(out["records"], rec), n
+            _check_filter(out, dec, n)
+    finally:
+        grp.close()
+
+
+def test_group_mapped_refuses_unregistered_and_bad_layouts():
+    grp = _group(2)
+    data, desc = synth.capture(synth.C3, 1000, seed=3)
+    try:
+        grp.compile(C3_SET)
+        dec = np.zeros(1024, np.uint8)
+        grp.register(data)
+        grp.register(dec)
+        with pytest.raises(abi.BtError) as e:    # descriptors not registered
+            grp.run_mapped(abi.Batch(data.ctypes.data, desc.ctypes.data, 0, 1000, data.nbytes, 0, 0),
+                           abi.Outputs(None, 0, None, dec.ctypes.data, None, None))
+        assert "not inside a group-registered range" in str(e.value)
+        with pytest.raises(abi.BtError):         # overlapping registration
+            grp.register(data[16:])
+        grp.unregister(dec)
+        grp.unregister(data)
+        with pytest.raises(abi.BtError):         # not registered any more
+            grp.unregister(data)
+    finally:
+        grp.close()
+    pl = _group(2, flags=abi.OPT_RECORDS_PLANES)
+    try:
+        pl.compile(C3_SET)
+        with pytest.raises(abi.BtError) as e:
+            _run_mapped(pl, data, desc, 1000)
+        assert "plane-major" in str(e.value)
+    finally:
+        pl.close()
+
+
+def test_group_placement_and_budget():
+    """Every member reports its NUMA placement; the group's host threads are one budget."""
+    grp = _group(4)
+    try:
+        per = abi.group_thread_budget(4, abi.usable_cpus())
+        for k in range(4):
+            p = grp.placement(k)
+            assert p["pool_threads"] == per
+            if p["pinned_cpus"]:
+                assert p["numa_node"] >= 0 and p["pinned_cpus"] == len(abi.node_cpus(p["numa_node"]))
+        assert grp.cost(True, False, True, 16) == (48, 16, 17)
+        assert grp.cost(False, True, True, 8) == (112, 16, 105)
+    finally:
+        grp.close()

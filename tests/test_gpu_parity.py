@@ -6,6 +6,7 @@ import pytest
 
 import oracle_lib as ol
 from beatrice_amd import abi, synth
+from ring_util import umem_capture
 from conftest import load_golden
 from golden_util import CAPTURES, compare_decisions, eval_order
 
@@ -193,34 +194,12 @@ def test_graph_replay_outputs(gpu_ctx):
     check_filter_outputs(out, n)
 
 
-def _umem(frames_data, desc, chunk=2048, shuffle_seed=5):
-    """An AF_XDP-style UMEM (anonymous mmap, numBuffers x bufferSize chunks, headroom 0,
-    reference src/AF_XDPBackend.cpp:683-720) holding each frame at the start of a chunk,
-    plus the RX ring's xdp_desc {addr, len, options} (shuffled chunk order, as after
-    fill-ring recycling)."""
-    import mmap
-    n = len(desc)
-    off, ln = synth.desc_off(desc), synth.desc_len(desc)
-    assert ln.max() <= chunk
-    mm = mmap.mmap(-1, n * chunk)
-    umem = np.frombuffer(mm, dtype=np.uint8)
-    order = np.random.default_rng(shuffle_seed).permutation(n)
-    for i in range(n):
-        c = order[i] * chunk
-        umem[c:c + ln[i]] = frames_data[off[i]:off[i] + ln[i]]
-    xdp = np.zeros((n, 2), np.uint64)
-    xdp[:, 0] = order.astype(np.uint64) * chunk
-    xdp[:, 1] = ln.astype(np.uint64)               # len in the low 32 bits, options = 0
-    packed = synth.make_desc(order.astype(np.uint64) * chunk, ln)
-    return mm, umem, xdp, packed
-
-
 def test_zero_copy_umem_ingest(gpu_ctx):
     """AF_XDP UMEM + RX xdp_desc ring consumed zero-copy — both
     registered with bt_host_register, the kernel reads the header windows over PCIe."""
     n = 50000
     data, desc = synth.capture(synth.C3, n, seed=31)
-    mm, umem, xdp, packed = _umem(data, desc)
+    mm, umem, xdp, packed = umem_capture(data, desc)
     filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
                {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
                {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]

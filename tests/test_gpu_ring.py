@@ -97,6 +97,16 @@ def test_cpp_stage_synthetic_ring():
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
 
 
+def test_cpp_stage_per_gpu_fanout_rings():
+    """Per-GPU ring sharding: a capture split by flow into 2 and 3 TPACKET_V3 ring
+    images, one GpuPacketFilter + GpuTpacketStage per ring, drained concurrently, each ring's
+    decisions equal to the reference PacketFilter's and every frame seen once."""
+    assert os.path.exists(CAPTURE_BIN), "tests/cpp/test_capture not built (make -C tests/cpp)"
+    r = subprocess.run([CAPTURE_BIN, "stage-fanout"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 def _run_gathered(ctx, ring, bs, nb, filters, dense=False):
     """bt_ring_gather_tpv3 (dense: bt_ring_gather_dense_tpv3) -> device run over the prefix
     slots (BT_BATCH_PREFIXES), slots and outputs in registered host memory."""

@@ -92,3 +92,69 @@ def test_native_group_split_rejects_bad_arguments():
     from beatrice_amd import abi
     with pytest.raises(abi.BtError):
         abi.group_split(np.zeros(10, np.uint32), 0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_native_split_cost_equals_shard_bounds(seed):
+    """bt_group_split_cost (every cost model the group uses) against shard.shard_bounds."""
+    from beatrice_amd import abi
+    rng = np.random.default_rng(100 + seed)
+    models = [shard.DEFAULT_COST] + [shard.group_cost(m, r, f, d, sb) for m in (False, True) for r in (False, True)
+                                     for f in (False, True) for d in (0, 8, 16) for sb in (48, 112, 176)]
+    models += [(int(rng.integers(1, 300)), int(rng.choice([1, 4, 16, 64])), int(rng.integers(0, 200)))
+               for _ in range(8)]
+    for n in (0, 1, 64, 65, 4097, int(rng.integers(1, 200000))):
+        lens = rng.choice([0, 14, 42, 60, 64, 90, 128, 512, 1500, 9000], size=n).astype(np.uint32)
+        for cost in models:
+            for parts in (1, 2, 3, 8):
+                assert abi.group_split(lens, parts, cost) == shard.shard_bounds(lens, parts, cost=cost), \
+                    (n, parts, cost)
+
+
+def test_split_cost_balances_what_the_call_moves():
+    """A verdict-only host batch stages 48 B of each frame: with that model an IMIX batch's
+    members stage equal bytes, where the old 128 + 104 model over-weighted long frames."""
+    _, desc = synth.capture(synth.C3, 200000)
+    ln = synth.desc_len(desc)
+    model = shard.group_cost(False, False, True)
+    for w in (2, 4, 8):
+        b = shard.shard_bounds(ln, w, cost=model)
+        staged = [int(shard.packet_cost(ln[lo:hi], model).sum()) for lo, hi in b]
+        assert max(staged) / (sum(staged) / w) < 1.01
+        old = shard.shard_bounds(ln, w)
+        staged_old = [int(shard.packet_cost(ln[lo:hi], model).sum()) for lo, hi in old]
+        assert max(staged) <= max(staged_old)
+
+
+def test_thread_budget_matches_mirror():
+    """bt_group_thread_budget: one host-thread budget per group, split across members."""
+    from beatrice_amd import abi
+    for members in range(1, 17):
+        for usable in (1, 2, 8, 16, 64, 256):
+            for requested in (0, 1, 4, 16, 64, 128):
+                got = abi.group_thread_budget(members, usable, requested)
+                assert got == shard.member_threads(members, usable, requested)
+                assert 1 <= got <= 16
+    assert shard.member_threads(1, 16) == 8        # one context: the single-context default
+    assert shard.member_threads(8, 16) == 2        # 8 GPUs on a 16-CPU job: 16 threads in all
+    assert shard.member_threads(8, 128) == 8
+    with pytest.raises(abi.BtError):
+        abi.group_thread_budget(0, 16, 0)
+
+
+def test_node_cpus_are_this_process_cpus():
+    """bt_node_cpus: a NUMA node's CPUs this process may run on (the pool workers' pin set)."""
+    from beatrice_amd import abi
+    nodes = sorted(int(d[4:]) for d in os.listdir("/sys/devices/system/node") if d.startswith("node")) \
+        if os.path.isdir("/sys/devices/system/node") else []
+    allowed = os.sched_getaffinity(0)
+    seen = set()
+    for node in nodes:
+        cpus = abi.node_cpus(node)
+        assert set(cpus) <= allowed
+        assert not (set(cpus) & seen)
+        seen |= set(cpus)
+    if nodes:
+        assert seen == allowed or seen <= allowed
+    assert abi.node_cpus(-1) == [] and abi.node_cpus(100000) == []
+    assert 1 <= abi.usable_cpus() <= len(allowed)
