@@ -175,7 +175,7 @@ EXPORTS = [
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
     "bt_group_split_cost", "bt_group_cost", "bt_group_thread_budget", "bt_group_host_register",
     "bt_group_host_unregister", "bt_group_parse_filter_mapped", "bt_context_placement", "bt_node_cpus",
-    "bt_usable_cpus", "bt_extract_host", "bt_filter_dfa_pool",
+    "bt_usable_cpus", "bt_extract_host", "bt_filter_dfa_pool", "bt_group_split_plan",
 ]
 
 DEST_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)   # bt_format_records_to's dest
@@ -262,6 +262,7 @@ def lib() -> ctypes.CDLL:
         "bt_group_parse_filter_ptrs": (ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp]),
         "bt_group_split": (ctypes.c_int, [vp, u32, u32, vp]),
         "bt_group_split_cost": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(SplitCost), vp]),
+        "bt_group_split_plan": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(SplitCost), vp]),
         "bt_group_cost": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, ctypes.POINTER(SplitCost)]),
         "bt_group_thread_budget": (ctypes.c_int, [u32, u32, u32, ctypes.POINTER(u32)]),
         "bt_group_host_register": (ctypes.c_int, [vp, vp, u64]),
@@ -540,9 +541,10 @@ class Context:
         return out
 
 
-def group_split(lens: np.ndarray, parts: int, cost=None) -> list[tuple[int, int]]:
+def group_split(lens: np.ndarray, parts: int, cost=None, plan=False) -> list[tuple[int, int]]:
     """bt_group_split (host only): the members' [lo, hi) packet ranges; cost = (window,
-    align, fixed) selects bt_group_split_cost."""
+    align, fixed) selects bt_group_split_cost, plan=True bt_group_split_plan (what the
+    group's calls use)."""
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     b = np.zeros(parts + 1, np.uint32)
     lp = lens.ctypes.data if len(lens) else None
@@ -550,7 +552,8 @@ def group_split(lens: np.ndarray, parts: int, cost=None) -> list[tuple[int, int]
         _check(lib().bt_group_split(lp, len(lens), parts, b.ctypes.data))
     else:
         c = SplitCost(*[int(x) for x in cost], 0)
-        _check(lib().bt_group_split_cost(lp, len(lens), parts, ctypes.byref(c), b.ctypes.data))
+        fn = lib().bt_group_split_plan if plan else lib().bt_group_split_cost
+        _check(fn(lp, len(lens), parts, ctypes.byref(c), b.ctypes.data))
     return [(int(b[k]), int(b[k + 1])) for k in range(parts)]
 
 

@@ -131,6 +131,10 @@ struct Region {
 
 struct bt_group {
     std::vector<bt_ctx*> members;
+    // members that share a device (BT_OPT_GROUP_SHARED_DEVICE): the device part of a mapped
+    // call runs one member at a time per device when `serial_shared` (BT_GROUP_SHARED_SERIAL)
+    std::vector<std::shared_ptr<std::mutex>> dev_mu;   // per member, shared by members of one device
+    bool serial_shared = false;
     std::shared_mutex prog_mu;   // exclusive: bt_group_filter_compile; shared: batches (every member
                                  // of one batch runs the same program)
     std::unique_ptr<MemberThreads> threads;   // members > 1
@@ -159,10 +163,62 @@ struct Range {
     uint32_t lo, hi;
 };
 
-std::vector<Range> split(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost& cost) {
+// The split a group call uses: bt_group_split_cost's exact per-tile costs for up to kExactTiles
+// tiles; for larger batches the cost of one tile in every S (the middle tile of each run of S,
+// about kExactTiles samples) stands for its run, and each cut lands on the tile where the
+// interpolated running cost reaches total * k / parts. Exact costs read every descriptor on
+// one thread before any member starts: for 16M packets that took ~45 ms, against 22 ms for a
+// whole zero-copy pass over them (e2e --group 2, profiles/r04); the sampled split reads 1/S.
+constexpr uint32_t kExactTiles = 4096;
+
+template <class LenAt>
+uint64_t tile_cost(LenAt len, uint32_t n, uint32_t t, const bt_split_cost& c) {
+    uint64_t s = 0;
+    const uint32_t e = std::min(n, (t + 1) * kTile);
+    for (uint32_t i = t * kTile; i < e; ++i) s += packet_cost(len(i), c);
+    return s;
+}
+
+template <class LenAt>
+std::vector<Range> split_by(LenAt len, uint32_t n, uint32_t parts, const bt_split_cost& cost) {
+    std::vector<Range> r(parts, Range{n, n});
+    r[0].lo = 0;
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    if (parts == 1 || n == 0) {
+        r[0].hi = n;
+        return r;
+    }
+    const uint32_t S = ntiles <= kExactTiles ? 1u : (ntiles + kExactTiles - 1) / kExactTiles;
+    const uint32_t G = (ntiles + S - 1) / S;   // runs of S tiles
+    std::vector<double> cum(G);
+    double run = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t t0 = g * S, t1 = std::min(ntiles, t0 + S);
+        if (S == 1) {
+            run += (double)tile_cost(len, n, t0, cost);
+        } else {   // the run's middle tile (a whole one: the last tile may be partial) for all of it
+            const uint32_t mid = std::min(t0 + (t1 - t0) / 2, ntiles >= 2 && n % kTile ? ntiles - 2 : ntiles - 1);
+            run += (double)tile_cost(len, n, mid, cost) * (double)(t1 - t0);
+        }
+        cum[g] = run;
+    }
     std::vector<uint32_t> b(parts + 1, 0);
-    bt_group_split_cost(lens, n, parts, &cost, b.data());
-    std::vector<Range> r(parts);
+    for (uint32_t k = 1; k < parts; ++k) {
+        const double target = run * (double)k / (double)parts;
+        const uint32_t g = (uint32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        uint32_t tile;   // the first tile whose running cost reaches the target, + 1 (shard.py's cut)
+        if (g >= G) {
+            tile = ntiles;
+        } else {
+            const uint32_t t0 = g * S, t1 = std::min(ntiles, t0 + S);
+            const double before = g ? cum[g - 1] : 0.0, per = (cum[g] - before) / (double)(t1 - t0);
+            const double need = per > 0 ? (target - before) / per : 0.0;
+            tile = t0 + std::min(t1 - t0, (uint32_t)std::max(1.0, std::ceil(need)));
+        }
+        const uint64_t cut = std::min<uint64_t>((uint64_t)std::min(tile, ntiles) * kTile, n);
+        b[k] = (uint32_t)std::max<uint64_t>(cut, b[k - 1]);
+    }
+    b[parts] = n;
     for (uint32_t k = 0; k < parts; ++k) r[k] = {b[k], b[k + 1]};
     return r;
 }
@@ -203,30 +259,34 @@ int run_members(bt_group* g, Fn fn) {
 }
 
 // One host batch over the group: frames(ctx, lo, cnt, ...) runs packets [lo, lo + cnt).
-template <class Frames>
-int group_batch(bt_group* g, uint32_t n, const uint32_t* lens, Frames frames, bt_rec* records, uint64_t* verdict,
+template <class LenAt, class Frames>
+int group_batch(bt_group* g, uint32_t n, LenAt len, Frames frames, bt_rec* records, uint64_t* verdict,
                 uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
     const uint32_t m = (uint32_t)g->members.size();
     const bool want_filter = verdict || decide || pass_idx || n_pass;
     bt_split_cost cost{};
     (void)bt_group_cost(g, 0, records != nullptr, want_filter, 8, &cost);
-    const std::vector<Range> r = split(lens, n, m, cost);
-    std::vector<std::vector<uint32_t>> pidx(m);
+    const std::vector<Range> r = split_by(len, n, m, cost);
     std::vector<uint32_t> npass(m, 0);
     const bool want_pass = pass_idx || n_pass;
+    // member k lists its passes (indices relative to its range) at pass_idx + lo, inside its own
+    // range of the caller's array (it has at most cnt of them)
     int rc = run_members(g, [&](uint32_t k) -> int {
         const uint32_t lo = r[k].lo, cnt = r[k].hi - r[k].lo;
         if (!cnt) return BT_OK;
-        if (pass_idx) pidx[k].resize(cnt);
         return frames(g->members[k], lo, cnt, records ? records + lo : nullptr, verdict ? verdict + lo / kTile : nullptr,
-                      decide ? decide + lo : nullptr, pass_idx ? pidx[k].data() : nullptr,
+                      decide ? decide + lo : nullptr, pass_idx ? pass_idx + lo : nullptr,
                       want_pass ? &npass[k] : nullptr);
     });
     if (rc) return rc;
-    uint32_t at = 0;
-    for (uint32_t k = 0; k < m; ++k) {
-        if (pass_idx)
-            for (uint32_t j = 0; j < npass[k]; ++j) pass_idx[at + j] = pidx[k][j] + r[k].lo;
+    // then they move down to their place in the whole list, in member order (member k's place
+    // starts at or below its range's start, so nothing unread is overwritten)
+    uint32_t at = npass[0];
+    for (uint32_t k = 1; k < m; ++k) {
+        if (pass_idx) {
+            const uint32_t lo = r[k].lo;
+            for (uint32_t j = 0; j < npass[k]; ++j) pass_idx[at + j] = pass_idx[lo + j] + lo;
+        }
         at += npass[k];
     }
     if (n_pass) *n_pass = at;
@@ -331,6 +391,18 @@ int bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const 
     return BT_OK;
 }
 
+int bt_group_split_plan(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost, uint32_t* bounds) {
+    if (!bounds || !parts || !cost || (n && !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / zero parts");
+    try {
+        const std::vector<Range> r = split_by([lens](uint32_t i) { return lens[i]; }, n, parts, *cost);
+        for (uint32_t k = 0; k < parts; ++k) bounds[k] = r[k].lo;
+        bounds[parts] = n;
+        return BT_OK;
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_split_plan: %s", e.what());
+    }
+}
+
 int bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member) {
     if (!members || !per_member) return bt::set_error(BT_E_INVALID_ARGUMENT, "zero members / null out");
     usable = std::max(usable, 1u);
@@ -367,6 +439,19 @@ int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts,
             return bt::set_error(rc, "group member %u (device %d): %s", i, devices[i], msg.c_str());
         }
         g->members.push_back(c);
+    }
+    {
+        std::vector<std::pair<int, std::shared_ptr<std::mutex>>> by_dev;
+        for (uint32_t i = 0; i < n_devices; ++i) {
+            auto it = std::find_if(by_dev.begin(), by_dev.end(), [&](const auto& x) { return x.first == devices[i]; });
+            if (it == by_dev.end()) {
+                by_dev.emplace_back(devices[i], std::make_shared<std::mutex>());
+                it = by_dev.end() - 1;
+            }
+            g->dev_mu.push_back(it->second);
+        }
+        const char* e = getenv("BT_GROUP_SHARED_SERIAL");
+        g->serial_shared = e && atoi(e) != 0;
     }
     if (n_devices > 1) {
         std::vector<const cpu_set_t*> pins;
@@ -433,9 +518,7 @@ int bt_group_parse_filter(bt_group* g, const uint8_t* base, const bt_pkt_desc* d
     if (n && (!base || !desc)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
     try {
         std::shared_lock<std::shared_mutex> lk(g->prog_mu);
-        std::vector<uint32_t> lens(n);
-        for (uint32_t i = 0; i < n; ++i) lens[i] = BT_DESC_LEN(desc[i]);
-        return group_batch(g, n, lens.data(),
+        return group_batch(g, n, [desc](uint32_t i) { return (uint32_t)BT_DESC_LEN(desc[i]); },
                            [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
                                uint32_t* np) { return bt_parse_filter(c, base, desc + lo, cnt, r, v, d, p, np); },
                            records, verdict, decide, pass_idx, n_pass);
@@ -451,7 +534,7 @@ int bt_group_parse_filter_ptrs(bt_group* g, const uint8_t* const* frames, const 
     if (n && (!frames || !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
     try {
         std::shared_lock<std::shared_mutex> lk(g->prog_mu);
-        return group_batch(g, n, lens,
+        return group_batch(g, n, [lens](uint32_t i) { return lens[i]; },
                            [&](bt_ctx* c, uint32_t lo, uint32_t cnt, bt_rec* r, uint64_t* v, uint8_t* d, uint32_t* p,
                                uint32_t* np) { return bt_parse_filter_ptrs(c, frames + lo, lens + lo, cnt, r, v, d, p, np); },
                            records, verdict, decide, pass_idx, n_pass);
@@ -533,15 +616,18 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
                 r.push_back({std::min(n, (uint32_t)((uint64_t)tiles * k / m) * kTile),
                              std::min(n, (uint32_t)((uint64_t)tiles * (k + 1) / m) * kTile)});
         } else {
-            std::vector<uint32_t> lens(n);
             const uint8_t* d = static_cast<const uint8_t*>(b->desc);
-            if (b->desc_format == BT_DESC_XDP)
-                for (uint32_t i = 0; i < n; ++i) std::memcpy(&lens[i], d + (size_t)i * 16 + 8, 4);
-            else
-                for (uint32_t i = 0; i < n; ++i) lens[i] = BT_DESC_LEN(reinterpret_cast<const uint64_t*>(d)[i]);
             bt_split_cost cost{};
             (void)bt_group_cost(g, 1, o->records != nullptr, filter, dsz, &cost);
-            r = split(lens.data(), n, m, cost);
+            if (b->desc_format == BT_DESC_XDP)
+                r = split_by([d](uint32_t i) {
+                    uint32_t l;
+                    std::memcpy(&l, d + (size_t)i * 16 + 8, 4);
+                    return l;
+                }, n, m, cost);
+            else
+                r = split_by([d](uint32_t i) { return (uint32_t)BT_DESC_LEN(reinterpret_cast<const uint64_t*>(d)[i]); },
+                             n, m, cost);
         }
         // the verdict words the pass list is built from
         const uint32_t words = (n + 63) / 64;
@@ -626,8 +712,12 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
             const uint32_t lo = r[k].lo, hi = r[k].hi;
             if (lo == hi) return BT_OK;
             bt_ctx* c = g->members[k];
-            if (int e = bt_parse_filter_device(c, &mb[k].b, &mb[k].o, nullptr)) return e;
-            if (int e = bt_synchronize(c)) return e;
+            {
+                std::unique_lock<std::mutex> dl(*g->dev_mu[k], std::defer_lock);
+                if (g->serial_shared) dl.lock();
+                if (int e = bt_parse_filter_device(c, &mb[k].b, &mb[k].o, nullptr)) return e;
+                if (int e = bt_synchronize(c)) return e;
+            }
             if (!want_pass) return BT_OK;
             const uint32_t w0 = lo / kTile, w1 = (hi + 63) / 64;
             std::vector<uint32_t>& ck = cnt[k];

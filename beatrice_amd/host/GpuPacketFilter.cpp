@@ -330,7 +330,10 @@ struct InFlight {
 
 template <class Fn>
 void GpuPacketFilter::forRanges(size_t n, Fn&& fn) {
-    if (inFlight_.load(std::memory_order_relaxed) > 1) {
+    // small ranges on the caller: waking the host pool costs ~10-15 us, more than the work
+    // (classify of 1-256 packets spent 15 us per call there, profiles/r04/surfaces)
+    constexpr size_t kInlineBelow = 8192;
+    if (n < kInlineBelow || inFlight_.load(std::memory_order_relaxed) > 1) {
         if (n) fn(size_t(0), n);
     } else {
         parallel_ranges(ctx_, n, [&](size_t lo, size_t hi) { fn(lo, hi); });

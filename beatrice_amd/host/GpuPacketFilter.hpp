@@ -138,7 +138,10 @@ public:
     // any batch — instead of paying a device round trip (~0.1 ms per call whatever its size,
     // against ~0.5 us per packet for the reference, src/PacketFilter.cpp:57-119). Default:
     // BEATRICE_GPU_HOST_BELOW, else kHostBelowDefault; 0 sends every call to the device.
-    static constexpr size_t kHostBelowDefault = 512;
+    // Measured (surface_bench single, profiles/r04/surfaces): classify() on the host costs
+    // ~0.2 us + 7-12 ns per packet, on the device 23-35 us + ~9 ns per packet; 2048 keeps the
+    // host's share of a batch's CPU time below the device pass's wall time.
+    static constexpr size_t kHostBelowDefault = 2048;
     void setHostBatchBelow(size_t n) { hostBelow_.store(n, std::memory_order_relaxed); }
     size_t hostBatchBelow() const { return hostBelow_.load(std::memory_order_relaxed); }
 

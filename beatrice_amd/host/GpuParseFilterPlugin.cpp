@@ -396,10 +396,17 @@ private:
             ++prof_.batches;
             lk.lock();
             done_seq_ = q.seq + 1;
-            if (used_.size() < kMaxUsed) used_.push_back(std::move(q.batch));
-            else {   // the producers are not recycling (no full shards): release here
+            if (used_.size() < kMaxUsed && !queue_.empty()) {
+                used_.push_back(std::move(q.batch));   // a producer releases it (recycleOne)
+            } else {
+                // the producers are not recycling (no full shards), or nothing else is queued
+                // (traffic stopped: release now rather than hold the capture's buffers until
+                // the next burst): the classifier releases this batch and the parked ones
+                std::vector<HeldBatch> drop;
+                if (queue_.empty()) drop.swap(used_);
                 lk.unlock();
                 q.batch.clear();
+                drop.clear();
                 lk.lock();
             }
             done_cv_.notify_all();
@@ -591,10 +598,11 @@ extern "C" void gpu_plugin_set_sink(beatrice::IPacketPlugin* p, gpu_verdict_sink
 extern "C" uint32_t gpu_batch_layers(const gpu_verdict_batch* b, uint32_t i, gpu_walked_layer* out, uint32_t cap) {
     if (!b || !b->records || i >= b->n) return 0;
     const bt_rec& r = b->records[i];
-    gpu_walked_layer l[6];
+    // a kernel record holds at most 5 layers; a caller's record may set every present bit (8)
+    gpu_walked_layer l[8];
     uint32_t k = 0;
     auto add = [&](const char* name, uint32_t off, int32_t tag, uint32_t bit) {
-        l[k++] = {name, off, tag, (r.ok & bit) ? 1u : 0u};
+        if (k < 8) l[k++] = {name, off, tag, (r.ok & bit) ? 1u : 0u};
     };
     add("ethernet", 0, -1, BT_L_ETH);   // the walk (DESIGN.md R-WALK), from the record's bitmaps
     if (r.present & BT_L_VLAN0) add("vlan", 12, 0, BT_L_VLAN0);

@@ -546,6 +546,12 @@ typedef struct bt_split_cost {
 } bt_split_cost;
 int      bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
                              uint32_t* bounds);
+/* The split the group's calls use: bt_group_split_cost up to 4096 tiles; above, the cost of
+ * one tile in every S (~4096 samples) stands for its run of S tiles and the cuts interpolate
+ * within a run (an exact pass over 16M descriptors took ~45 ms on one thread before any
+ * member started). Same form of bounds. */
+int      bt_group_split_plan(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
+                             uint32_t* bounds);
 /* The cost model a group call uses (mapped: bt_group_parse_filter_mapped, else the host
  * batches), for a call that asks for records / filter outputs, with desc_bytes-byte
  * descriptors (8 packed, 16 xdp_desc, 0 fixed stride):

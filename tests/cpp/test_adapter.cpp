@@ -763,7 +763,11 @@ static bool small_filter_case(const char* label, const Capture& cap, const std::
               sa.packetsDropped == sb.packetsDropped && sa.filterCounts == sb.filterCounts,
           "%s: per-packet stats differ (processed %lu/%lu)", label, (unsigned long)sa.packetsProcessed,
           (unsigned long)sb.packetsProcessed);
-    // small batches (host) and the same batches on the device
+    // small batches (host) and the same batches on the device; classify on filters of their own
+    GpuPacketFilter hostc(0), devc(0);
+    devc.setHostBatchBelow(0);
+    install(hostc, specs);
+    install(devc, specs);
     for (size_t lo = 0; lo < cap.packets.size(); lo += 100) {
         const std::vector<Packet> part(cap.packets.begin() + lo,
                                        cap.packets.begin() + std::min(cap.packets.size(), lo + 100));
@@ -782,7 +786,7 @@ static bool small_filter_case(const char* label, const Capture& cap, const std::
             CHECK(a[i].passed == b[i].passed && a[i].filterName == b[i].filterName && a[i].passed == c[i].passed &&
                       a[i].filterName == c[i].filterName,
                   "%s: batch at %zu packet %zu", label, lo, i);
-        GpuPacketFilter::Verdicts v = host.classify(part), w = dev.classify(part);
+        GpuPacketFilter::Verdicts v = hostc.classify(part), w = devc.classify(part);
         CHECK(v.decide == w.decide && v.pass_idx == w.pass_idx, "%s: classify host/device at %zu", label, lo);
     }
     sa = ref.getStats();

@@ -120,7 +120,8 @@ def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True,
         for a in held:
             grp.unregister(a)
     return {"rec_tiled": h_rec, "records": abi.untile_records(h_rec, n) if records else None,
-            "decide": h_dec[:n], "verdict": h_ver, "pass_idx": pidx[:int(npass[0])], "n_pass": int(npass[0])}
+            "decide": h_dec[:n], "verdict": h_ver, "pass_idx": pidx[:int(npass[0])] if pass_list else pidx[:0],
+            "n_pass": int(npass[0])}
 
 
 def _single_zero_copy(ctx, base, desc, n, fmt, filters):

@@ -158,3 +158,24 @@ def test_node_cpus_are_this_process_cpus():
         assert seen == allowed or seen <= allowed
     assert abi.node_cpus(-1) == [] and abi.node_cpus(100000) == []
     assert 1 <= abi.usable_cpus() <= len(allowed)
+
+
+@pytest.mark.parametrize("cfg", [synth.C3, synth.C4, synth.FUZZ])
+def test_group_split_plan_exact_when_small_balanced_when_large(cfg):
+    """bt_group_split_plan (the split group calls use): identical to the exact split up to 4096
+    tiles; above it, sampled, still tile-aligned, contiguous and within 2 % of balance."""
+    from beatrice_amd import abi
+    _, desc = synth.capture(cfg, 1 << 20, seed=7)
+    ln = synth.desc_len(desc).astype(np.uint32)
+    for model in (shard.group_cost(True, False, True), shard.group_cost(True, True, True, 16),
+                  shard.group_cost(False, True, True, 8, 112)):
+        for n in (1000, 4096 * 64, 4096 * 64 + 1, 700001, 1 << 20):
+            for parts in (2, 3, 8):
+                plan = abi.group_split(ln[:n], parts, model, plan=True)
+                if (n + 63) // 64 <= 4096:
+                    assert plan == shard.shard_bounds(ln[:n], parts, cost=model)
+                    continue
+                assert plan[0][0] == 0 and plan[-1][1] == n
+                assert all(lo % 64 == 0 for lo, _ in plan) and all(plan[i][1] == plan[i + 1][0] for i in range(parts - 1))
+                c = [int(shard.packet_cost(ln[lo:hi], model).sum()) for lo, hi in plan]
+                assert max(c) / (sum(c) / parts) < 1.02, (n, parts, model, c)

@@ -43,13 +43,87 @@ ap.add_argument("--host-gather", action="store_true",
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
 ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="bt_opts.flags (A/B, e.g. 0x8000 no lean PCIe round A)")
 ap.add_argument("--host-threads", type=int, default=0)
+ap.add_argument("--group", type=int, default=0,
+                help="drive a bt_group of N members (devices 0..N-1; members share device 0 when fewer GPUs "
+                     "are visible, labelled 'shared device'): host gather (bt_group_parse_filter) and zero-copy "
+                     "(bt_group_host_register + bt_group_parse_filter_mapped) rows, with host CPU-seconds per Mpkt")
 a = ap.parse_args()
 cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4}[a.config]
 data, desc = synth.capture(cfg, a.packets)
+
+
+def page_nodes(arr, samples=8):
+    """NUMA nodes of a few of the array's pages (move_pages(2) query; -1 unknown)."""
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    base, nb = arr.ctypes.data, arr.nbytes
+    pages = (ctypes.c_void_p * samples)(*[(base + nb * i // samples) & ~4095 for i in range(samples)])
+    status = (ctypes.c_int * samples)()
+    if libc.syscall(279, 0, ctypes.c_ulong(samples), pages, None, status, 0) != 0:
+        return []
+    return sorted(set(int(x) for x in status))
+
+
+FILTERS = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+           {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+           {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+
+if a.group:
+    import numpy as np
+    m = a.group
+    shared = abi.device_count() < m
+    devices = [0] * m if shared else list(range(m))
+    grp = abi.Group(devices, host_chunk_packets=a.chunk, host_threads=a.host_threads,
+                    flags=a.flags | (abi.OPT_GROUP_SHARED_DEVICE if shared else 0))
+    grp.compile(FILTERS)
+    n = a.packets
+    where = {"members": m, "devices": devices, "shared_device": shared, "usable_cpus": abi.usable_cpus(),
+             "placement": [grp.placement(k) for k in range(m)], "data_nodes": page_nodes(data),
+             "numa_pin": os.environ.get("BT_NUMA_PIN", "1"), "shared_serial": os.environ.get("BT_GROUP_SHARED_SERIAL", "0")}
+
+    def timed(fn):
+        best, cpu = 1e9, 0.0
+        fn()   # warm
+        for _ in range(a.reps):
+            c0, t0 = time.process_time(), time.perf_counter()
+            fn()
+            dt, dc = time.perf_counter() - t0, time.process_time() - c0
+            if dt < best:
+                best, cpu = dt, dc
+        return best, cpu
+
+    for mode in ("verdicts", "records+verdicts"):
+        rec = mode != "verdicts"
+        best, cpu = timed(lambda: grp.run_host(data, desc, records=rec))
+        print(json.dumps({"config": a.config, "flags": a.flags, "mode": f"group {m}, host gather, {mode}",
+                          "packets": n, "seconds": round(best, 4), "mpps": round(n / best / 1e6, 1),
+                          "host_cpu_s_per_mpkt": round(cpu / (n / 1e6), 4), "cost_model": grp.cost(False, rec, True),
+                          **where}), flush=True)
+    tiles = (n + 63) // 64
+    h_dec = np.zeros(tiles * 64, np.uint8)
+    h_ver = np.zeros(tiles, np.uint64)
+    for arr in (data, desc, h_dec, h_ver):
+        grp.register(arr)
+    for mode in ("verdicts", "records+verdicts"):
+        rec = mode != "verdicts"
+        h_rec = np.zeros(tiles * 6144, np.uint8) if rec else None
+        if rec:
+            grp.register(h_rec)
+        batch = abi.Batch(data.ctypes.data, desc.ctypes.data, 0, n, data.nbytes, abi.DESC_PACKED, 0)
+        outs = abi.Outputs(h_rec.ctypes.data if rec else None, n, h_ver.ctypes.data, h_dec.ctypes.data, None, None)
+        best, cpu = timed(lambda: grp.run_mapped(batch, outs))
+        print(json.dumps({"config": a.config, "flags": a.flags, "mode": f"group {m}, zero-copy in and out, {mode}",
+                          "packets": n, "seconds": round(best, 4), "mpps": round(n / best / 1e6, 1),
+                          "host_cpu_s_per_mpkt": round(cpu / (n / 1e6), 4), "cost_model": grp.cost(True, rec, True),
+                          **where}), flush=True)
+        if rec:
+            grp.unregister(h_rec)
+    for arr in (data, desc, h_dec, h_ver):
+        grp.unregister(arr)
+    grp.close()
+    sys.exit(0)
 ctx = abi.Context(0, host_chunk_packets=a.chunk, host_threads=a.host_threads, flags=a.flags)
-ctx.compile([{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
-             {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
-             {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}])
+ctx.compile(FILTERS)
 if a.tpacket:
     import numpy as np
     ring, rdesc, used = synth.tpv3_ring(data, desc)
@@ -237,4 +311,5 @@ for mode in ("verdicts", "records+verdicts"):
     d2h = a.packets * (1 + 1 / 8 + (96 if rec else 0))
     print(json.dumps({"config": a.config, "flags": a.flags, "mode": mode, "packets": a.packets, "seconds": round(best, 4),
                       "mpps": round(a.packets / best / 1e6, 1), "h2d_GBps": round(h2d / best / 1e9, 2),
-                      "d2h_GBps": round(d2h / best / 1e9, 2), "n_pass": out["n_pass"]}), flush=True)
+                      "d2h_GBps": round(d2h / best / 1e9, 2), "n_pass": out["n_pass"], "data_nodes": page_nodes(data),
+                      "placement": ctx.placement(), "numa_pin": os.environ.get("BT_NUMA_PIN", "1")}), flush=True)

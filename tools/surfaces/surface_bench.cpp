@@ -2,8 +2,8 @@
 // to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
 // integrator calls").
 //
-//   surface_bench [all|filter|ref|mt|parser|sizes|plugin] [--packets N] [--seconds S] [--threads T] [--plugin SO]
-//                 [--chunks 16384,65536]
+//   surface_bench [all|filter|ref|mt|parser|sizes|single|group|plugin] [--packets N] [--seconds S] [--threads T]
+//                 [--plugin SO] [--chunks 16384,65536] [--members 1,2,4]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
 // (the reference's batch type, include/beatrice/Packet.hpp) and C3's 5-tuple filter set:
@@ -19,6 +19,9 @@
 //             on its own shard in chunks (the reference's pattern above, one instance);
 //   parser    ProtocolParser::parsePacket per walked layer against GpuProtocolParser::parseBatch
 //             (records, ParseResults on demand, JSON text): bench_parser below;
+//   single    one packet per call (applyFilters(const Packet&), parsePacket(slice, name)) and small
+//             classify() batches, host branch against device branch: bench_single below;
+//   group     one GpuPacketFilter over a device group of 1 / 2 / 4 members: bench_group below;
 //   plugin    libgpu_parse_filter_plugin.so through createPlugin(): onPacket from 1 and from
 //             T threads (PluginManager::processPacket's per-packet call), until the verdict
 //             sink has seen every packet.
@@ -32,6 +35,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <fstream>
 #include <memory>
 #include <string>
@@ -382,6 +386,149 @@ void bench_parser(const Capture& c, int threads, double seconds) {
     timed("GpuProtocolParser::parseBatch + format(BT_FMT_JSON) of the batch", 2);
 }
 
+// Single-packet calls and small batches (VERDICT r03 "stop charging single-packet callers a
+// device round trip"): the reference's per-packet entries on one thread against the drop-in's
+// host branch (the compiled program / extractor on the calling thread) and its device branch
+// (setHostBatchBelow(0): one device round trip per call); then classify() by batch size on
+// both branches, which places the default threshold (kHostBelowDefault).
+void bench_single(const Capture& c, double seconds) {
+    using namespace beatrice::parser;
+    const size_t n = std::min<size_t>(c.packets.size(), 1u << 16);
+    auto per_packet = [&](const char* what, auto&& call, size_t limit) {
+        uint64_t done = 0;
+        (void)call(c.packets[0]);
+        const auto t0 = Clock::now();
+        for (size_t i = 0; secs(t0, Clock::now()) < seconds; i = (i + 1) % std::min(n, limit)) {
+            call(c.packets[i]);
+            ++done;
+        }
+        const double el = secs(t0, Clock::now());
+        char extra[96];
+        std::snprintf(extra, sizeof(extra), "\"us_per_call\": %.3f, \"seconds\": %.3f", el / done * 1e6, el);
+        line(what, c, 1, done / el, extra);
+    };
+    {
+        PacketFilter ref;
+        add_set(ref);
+        per_packet("ref PacketFilter::applyFilters(const Packet&)", [&](const Packet& p) { return ref.applyFilters(p).passed; },
+                   n);
+        GpuPacketFilter host, dev;
+        add_set(host);
+        add_set(dev);
+        dev.setHostBatchBelow(0);
+        per_packet("GpuPacketFilter::applyFilters(const Packet&), host branch",
+                   [&](const Packet& p) { return host.applyFilters(p).passed; }, n);
+        per_packet("GpuPacketFilter::applyFilters(const Packet&), device round trip",
+                   [&](const Packet& p) { return dev.applyFilters(p).passed; }, n);
+        for (size_t b : {1u, 4u, 16u, 64u, 256u, 512u, 1024u, 4096u}) {
+            const std::vector<Packet> part(c.packets.begin(), c.packets.begin() + std::min(n, (size_t)b));
+            for (int branch = 0; branch < 2; ++branch) {
+                GpuPacketFilter& f = branch ? dev : host;
+                (void)f.classify(part);
+                uint64_t calls = 0;
+                const auto t0 = Clock::now();
+                while (secs(t0, Clock::now()) < seconds / 8) {
+                    (void)f.classify(part);
+                    ++calls;
+                }
+                const double el = secs(t0, Clock::now());
+                char extra[128];
+                std::snprintf(extra, sizeof(extra), "\"batch\": %zu, \"branch\": \"%s\", \"us_per_call\": %.2f", part.size(),
+                              branch ? "device" : "host", el / calls * 1e6);
+                line("GpuPacketFilter::classify(vector<Packet>) small batch", c, 1, (double)calls * part.size() / el,
+                     extra);
+            }
+        }
+    }
+    {   // parsePacket(slice, name) per walked layer: the reference, the host branch, the device
+        ProtocolParser::ParserConfig cfg;
+        cfg.enablePerformanceMetrics = false;
+        ProtocolParser rp(cfg);
+        beatrice::gpu::GpuProtocolParser hp(cfg, 0), dp(cfg, 0);
+        dp.setHostBatchBelow(0);
+        for (auto pr : {BuiltinProtocols::createEthernetProtocol(), BuiltinProtocols::createVLANProtocol(),
+                        BuiltinProtocols::createIPv4Protocol(), BuiltinProtocols::createIPv6Protocol(),
+                        BuiltinProtocols::createTCPProtocol(), BuiltinProtocols::createUDPProtocol(),
+                        BuiltinProtocols::createICMPProtocol()}) {
+            rp.registerProtocol(pr);
+            hp.registerProtocol(pr);
+            dp.registerProtocol(pr);
+        }
+        const std::vector<Packet> pk(c.packets.begin(), c.packets.begin() + n);
+        const auto b = hp.parseBatch(pk);
+        std::vector<std::pair<std::vector<uint8_t>, std::string>> slices;
+        for (size_t i = 0; i < n && slices.size() < 200000; ++i)
+            for (const auto& l : b.layers(i))
+                slices.emplace_back(std::vector<uint8_t>(pk[i].data() + l.offset, pk[i].data() + pk[i].length()), l.name);
+        auto per_layer = [&](const char* what, auto&& parse, size_t limit) {
+            uint64_t done = 0;
+            const auto t0 = Clock::now();
+            for (size_t i = 0; secs(t0, Clock::now()) < seconds; i = (i + 1) % std::min(slices.size(), limit)) {
+                const ParseResult r = parse(slices[i].first, slices[i].second);
+                (void)r;
+                ++done;
+            }
+            const double el = secs(t0, Clock::now());
+            char extra[96];
+            std::snprintf(extra, sizeof(extra), "\"us_per_layer\": %.3f, \"seconds\": %.3f", el / done * 1e6, el);
+            line(what, c, 1, done / el, extra);   // mpps here = M layers / s
+        };
+        per_layer("ref ProtocolParser::parsePacket(slice, name), layers",
+                  [&](const std::vector<uint8_t>& v, const std::string& nm) { return rp.parsePacket(v, nm); }, slices.size());
+        per_layer("GpuProtocolParser::parsePacket(slice, name), host branch, layers",
+                  [&](const std::vector<uint8_t>& v, const std::string& nm) { return hp.parsePacket(v, nm); }, slices.size());
+        per_layer("GpuProtocolParser::parsePacket(slice, name), device round trip, layers",
+                  [&](const std::vector<uint8_t>& v, const std::string& nm) { return dp.parsePacket(v, nm); }, slices.size());
+    }
+}
+
+// An in-process device group (bt_group) behind one GpuPacketFilter: classify() of the whole
+// capture from one caller and from T callers, for groups of `members` contexts (on device 0 when
+// the box has fewer GPUs: "shared_device"), with the process's CPU time per million packets.
+void bench_group(const Capture& c, int threads, double seconds, const std::vector<int>& member_counts) {
+    int ndev = 0;
+    (void)bt_device_count(&ndev);
+    for (int m : member_counts) {
+        const bool shared = ndev < m;
+        std::vector<int> devs;
+        for (int k = 0; k < m; ++k) devs.push_back(shared ? 0 : k);
+        bt_opts o{};
+        if (shared) o.flags = BT_OPT_GROUP_SHARED_DEVICE;
+        GpuPacketFilter f(devs, &o);
+        add_set(f);
+        (void)f.classify(c.packets);
+        for (int callers : {1, threads}) {
+            std::atomic<uint64_t> done{0};
+            std::atomic<bool> stop{false};
+            const double cpu0 = (double)std::clock() / CLOCKS_PER_SEC;
+            const auto t0 = Clock::now();
+            std::vector<std::thread> th;
+            const size_t chunk = callers == 1 ? c.packets.size() : 65536;
+            for (int t = 0; t < callers; ++t)
+                th.emplace_back([&, t] {
+                    const size_t lo = c.packets.size() * t / callers, hi = c.packets.size() * (t + 1) / callers;
+                    const std::vector<Packet> shard(c.packets.begin() + lo, c.packets.begin() + hi);
+                    std::vector<Packet> part;
+                    uint64_t mine = 0;
+                    for (size_t at = 0; !stop.load(std::memory_order_relaxed); at = (at + chunk) % shard.size()) {
+                        part.assign(shard.begin() + at, shard.begin() + std::min(shard.size(), at + chunk));
+                        mine += f.classify(part).decide.size();
+                        if (t == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+                    }
+                    done += mine;
+                });
+            for (auto& x : th) x.join();
+            const double el = secs(t0, Clock::now());
+            const double cpu = (double)std::clock() / CLOCKS_PER_SEC - cpu0;
+            char extra[200];
+            std::snprintf(extra, sizeof(extra),
+                          "\"members\": %d, \"shared_device\": %s, \"chunk\": %zu, \"host_cpu_s_per_mpkt\": %.4f, "
+                          "\"seconds\": %.3f", m, shared ? "true" : "false", chunk, cpu / (done / 1e6), el);
+            line("GpuPacketFilter(group)::classify(vector<Packet>)", c, callers, done / el, extra);
+        }
+    }
+}
+
 void bench_plugin(const Capture& c, int threads, double seconds, const char* so) {
     void* h = dlopen(so, RTLD_LAZY);
     if (!h) {
@@ -452,11 +599,20 @@ int main(int argc, char** argv) {
     int threads = usable_cpus();
     const char* so = "beatrice_amd/libgpu_parse_filter_plugin.so";
     std::vector<size_t> chunks = {16384, 65536};
+    std::vector<int> members = {1, 2, 4};
     for (int i = 2; i + 1 < argc; i += 2) {
         if (!std::strcmp(argv[i], "--packets")) n2 = n3 = (uint32_t)std::atol(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--seconds")) seconds = std::atof(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--threads")) threads = std::atoi(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--plugin")) so = argv[i + 1];
+        else if (!std::strcmp(argv[i], "--members")) {   // comma-separated group sizes of "group"
+            members.clear();
+            for (const char* q = argv[i + 1]; *q;) {
+                members.push_back(std::atoi(q));
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
         else if (!std::strcmp(argv[i], "--chunks")) {   // comma-separated chunk sizes of the T-caller runs
             chunks.clear();
             for (const char* q = argv[i + 1]; *q;) {
@@ -486,6 +642,8 @@ int main(int argc, char** argv) {
         }
         if (what == "all" || what == "parser") bench_parser(c, threads, seconds);
         if (what == "all" || what == "sizes") bench_call_sizes(c, seconds);
+        if (what == "all" || what == "single") bench_single(c, seconds);
+        if (what == "all" || what == "group") bench_group(c, threads, seconds, members);
         if (what == "all" || what == "plugin") {
             bench_plugin(c, 1, seconds, so);
             if (threads >= 4) bench_plugin(c, threads / 2, seconds, so);   // producers leave CPUs to the plugin
