@@ -1153,231 +1153,6 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     }
 }
 
-// ---- bt_parse_filter_pipe2: round B one tile ahead -----------------------------------
-// bt_parse_filter_pipe waits for tile t's round B (the chunks round A did not read) at the top
-// of iteration t, right after issuing it, behind tile t - 1's stores: with one load counter
-// retired in issue order the wait covers those stores too, and round B's dependent latency
-// is exposed once per tile. It runs for most C4 tiles (QinQ, IPv6, IP / TCP options), which
-// move their line floor at 5.23 TB/s against 5.44-5.87 for C3 / C2.
-// pipe2 keeps two LDS images per wave and runs one tile ahead: iteration t
-//   1. waits for round A of t + 1 (issued one iteration ago), stages it into the other
-//      image, plans and issues round B of t + 1;
-//   2. issues round A of t + 2 and the descriptors of t + 3;
-//   3. parses and filters tile t from its image and issues its stores;
-//   4. waits for round B of t + 1 with everything issued after it still in flight, and
-//      stages it.
-// So round B of t + 1 is in flight during tile t's parse, filter and stores, and round A of
-// t + 1 during all of tile t. Every load and store is unconditional (8 round-A and 8 round-B
-// loads per tile, lanes with nothing to read load the zero line), so each wait is a fixed
-// count. FILTER 0 / 1 only: PAYLOAD slots stage their windows in the LDS row.
-template <int DW>
-__device__ __forceinline__ void issue_round_a_pipe2(const MainArgs& a, uint32_t lane, const TileDesc<DW>& d,
-                                                    Stage<-1>& st, bool wide, uint32_t need_max) {
-    decode_desc<DW>(d.me, st.off, st.len);
-    const uint32_t c = lane & 3u;
-    st.wide = wide;
-    const bool ntl = (a.nt & 2u) && !wide;
-    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        uint64_t qo;
-        uint32_t ql;
-        decode_desc<DW>(d.q[j], qo, ql);
-        const uint64_t a0 = qo & ~15ull;
-        const uint64_t addr = a0 + 16u * c;
-        const uint32_t sq = (uint32_t)qo & 15u;
-        st.qa0[j] = a0;
-        const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + min(ql, a.lean);
-        const bool ok = (16u * c < a_end) & (addr + 16u <= a.bytes);
-        st.v[j] = ld16(ok ? a.base + addr : zero, ntl);
-        const bool okb = wide & (16u * (c + 4u) < a_end) & (addr + 64u + 16u <= a.bytes);
-        st.v[4 + j] = ld16(okb ? a.base + addr + 64u : zero, false);   // always issued: a fixed count
-    }
-}
-
-// Round B's plan for one staged tile (round_b's decision, without its loads): this lane's
-// word lo | end << 8 (0: nothing), and the wave's load mode for the tile after it.
-__device__ __forceinline__ uint32_t plan_round_b(const MainArgs& a, uint32_t s, uint64_t my_off, uint32_t my_len,
-                                                 bool live, bool this_wide, uint32_t need_max, const uint32_t* w0,
-                                                 bool& wide_next) {
-    const uint32_t a_end = this_wide ? round_a_end_wide(my_off & ~15ull, s, my_len, need_max)
-                                     : min(64u, s + min(my_len, a.lean));
-    const bool cov = a_end >= s + min(my_len, 28u);
-    const uint32_t end = !live ? 0u : cov ? s + header_end(w0, my_len, kNeedFilter) : s + min(my_len, need_max);
-    const uint32_t lo = (a_end + 15u) >> 4;
-    const bool my_nb = end > 16u * lo;
-    bool wide = __popcll(__ballot(end > 64u)) > 32;
-    if (a.nt & 12u) wide = (a.nt & 8u) != 0u;
-    wide_next = wide;
-    return my_nb ? (lo | (end << 8)) : 0u;
-}
-
-struct RoundB {
-    uint4 v[8];
-    uint32_t cs[8];   // chunk of the row each load fills (8: none)
-};
-
-// Round B's loads for tile t: always 8 per lane (k = 0, 1 x 4 packets per instruction).
-__device__ __forceinline__ void issue_round_b2(const MainArgs& a, uint32_t t, uint32_t lane, const uint64_t* qa0,
-                                               uint32_t my_b, RoundB& rb) {
-    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
-#pragma unroll
-    for (uint32_t k = 0; k < 2; ++k)
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t q = j * 16u + (lane >> 2);
-            const uint32_t qb = (uint32_t)__shfl((int)my_b, (int)q);
-            const uint32_t c = (qb & 0xFFu) + (lane & 3u) + 4u * k;
-            const uint64_t addr = qa0[j] + 16u * c;
-            const bool want = (c < 8u) & (16u * c < (qb >> 8));   // never overwrite round A's chunks
-            rb.cs[4 * k + j] = want ? c : 8u;
-            const bool ok = want & (t * 64u + q < a.n) & (addr + 16u <= a.bytes);
-            rb.v[4 * k + j] = ld16(ok ? a.base + addr : zero, false);
-        }
-}
-
-__device__ __forceinline__ void stage_round_b2(const RoundB& rb, uint32_t* img, uint32_t lane) {
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-        if (rb.cs[i] < 8u) {
-            uint32_t* dst = img + ((i & 3u) * 16u + (lane >> 2)) * (uint32_t)kRowDwords + rb.cs[i] * 4u;
-            dst[0] = rb.v[i].x; dst[1] = rb.v[i].y; dst[2] = rb.v[i].z; dst[3] = rb.v[i].w;
-        }
-    }
-}
-
-template <int REC, int FILTER, int DW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void bt_parse_filter_pipe2(MainArgs a, DevProgram prog) {
-    static_assert(REC == kRecTiled || REC == kRecNone, "pipe2: tiled records or none");
-    static_assert(FILTER == 0 || FILTER == 1, "pipe2: no PAYLOAD slots");
-    constexpr uint32_t kRow = kRowDwords;
-    constexpr uint32_t kImg = kWave * kRow;
-    __shared__ uint32_t lds_all[kWavesPerBlock * 2 * kImg + 32];   // two images per wave + tail pad
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t* imgs = lds_all + wid * (2 * kImg);
-
-    const uint32_t total_waves = gridDim.x * kWavesPerBlock;
-    const uint32_t gw = blockIdx.x * kWavesPerBlock + wid;
-    uint32_t t, t_end, step;
-    if (a.blocked) {
-        const uint32_t per = (a.ntiles + total_waves - 1) / total_waves;
-        t = gw * per;
-        t_end = min(a.ntiles, t + per);
-        step = 1;
-    } else {
-        t = gw;
-        t_end = a.ntiles;
-        step = total_waves;
-    }
-    if (t >= t_end) return;
-    const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
-    const HotProgram hot = hot_program(prog);
-
-    // prologue: tile t's round A (waited, staged), its round B (issued), round A of t + step and
-    // the descriptors of t + 2 step, stand-ins for a tile's stores, then round B of t (waited)
-    Stage<-1> st;
-    RoundB rb;
-    TileDesc<DW> dn;
-    uint32_t cur = 0;
-    load_desc_pipe<DW>(a, t, true, lane, dn);
-    issue_round_a_pipe2<DW>(a, lane, dn, st, false, need_max);
-    load_desc_pipe<DW>(a, t + step, t + step < t_end, lane, dn);
-    stage_to_lds<-1>(st, imgs, lane);
-    wave_lds_sync();
-    uint64_t my_off = st.off;
-    uint32_t my_len = st.len;
-    uint32_t s = (uint32_t)my_off & 15u;
-    uint32_t w0[10];
-    window<10>(imgs + lane * kRow, s, w0);
-    bool wide;
-    {
-        const uint32_t my_b = plan_round_b(a, s, my_off, my_len, t * 64u + lane < a.n, false, need_max, w0, wide);
-        issue_round_b2(a, t, lane, st.qa0, my_b, rb);
-    }
-    issue_round_a_pipe2<DW>(a, lane, dn, st, wide, need_max);
-    load_desc_pipe<DW>(a, t + 2 * step, t + 2 * step < t_end, lane, dn);
-    pad_stores<REC, FILTER>();
-    stage_round_b2(rb, imgs, lane);
-    wave_lds_sync();
-    window<10>(imgs + lane * kRow, s, w0);
-
-    for (;;) {
-        uint32_t* img = imgs + cur * kImg;
-        uint32_t* nimg = imgs + (cur ^ 1u) * kImg;
-        const uint32_t tn = t + step;
-        const bool more = tn < t_end;
-        // 1. round A of t + step into the other image; plan + issue its round B
-        stage_to_lds<-1>(st, nimg, lane);
-        wave_lds_sync();
-        const uint64_t n_off = st.off;
-        const uint32_t n_len = st.len;
-        const uint32_t ns_ = (uint32_t)n_off & 15u;
-        bool wide2;
-        {
-            uint32_t w1[10];
-            window<10>(nimg + lane * kRow, ns_, w1);
-            const uint32_t my_b = plan_round_b(a, ns_, n_off, n_len, more && tn * 64u + lane < a.n, st.wide, need_max, w1,
-                                               wide2);
-            issue_round_b2(a, tn, lane, st.qa0, more ? my_b : 0u, rb);
-        }
-        // 2. round A of t + 2 step, descriptors of t + 3 step
-        issue_round_a_pipe2<DW>(a, lane, dn, st, wide2, need_max);
-        load_desc_pipe<DW>(a, tn + 2 * step, tn + 2 * step < t_end, lane, dn);
-
-        // 3. tile t: parse, tiled record stores, filter
-        const uint32_t p0 = t * 64u;
-        const uint32_t my = p0 + lane;
-        const bool live = my < a.n;
-        const uint32_t len = live ? my_len : 0u;
-        const uint32_t* row = img + lane * kRow;
-        if (REC == kRecTiled) {
-            Parsed p;
-            uint32_t nsl = parse_packet<true>(row, s, len, w0, p);
-            if (!live) {
-                nsl = 2u;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) p.r[k] = 0u;
-            }
-            const bool rec_in = BT_IN(&g_bounds_main, kSiteRecord, t, (a.n_cap + 63u) / 64u);
-            const auto r = rsrc_of(a.records + (uint64_t)t * (BT_REC_SLABS * 64 * 16), rec_in ? BT_REC_SLABS * 64 * 16 : 0u);
-            const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-            for (uint32_t k = 0; k < BT_REC_SLABS; ++k) {
-                const uint64_t mk = __ballot(k < nsl);
-                const uint32_t off = k < 2u ? (k * 64u + lane) * 16u
-                                   : k < nsl ? (k * 64u + (uint32_t)__popcll(mk & below)) * 16u : kOob;
-                st_b128<true>(r, off, make_uint4(p.r[4 * k], p.r[4 * k + 1], p.r[4 * k + 2], p.r[4 * k + 3]));
-            }
-        }
-        if (FILTER) {
-            uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, nullptr, img + lane * kRow, my_off, len, w0, live, slot);
-            const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
-            const uint32_t cnt = min(64u, a.n - p0);
-            const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
-            const bool v_in = BT_IN(&g_bounds_main, kSiteVerdict, t, a.ntiles);
-            const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict && v_in ? 8u : 0u);
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
-        }
-        wave_lds_sync();   // tile t's image reads are done: the next iteration stages into it
-        if (!more) break;
-        // 4. round B of t + step
-        stage_round_b2(rb, nimg, lane);
-        wave_lds_sync();
-        s = ns_;
-        window<10>(nimg + lane * kRow, s, w0);
-        my_off = n_off;
-        my_len = n_len;
-        cur ^= 1u;
-        t = tn;
-    }
-}
-
 // ---- ordered compaction of passing packet indices ---------------------------------
 // K2: chunk_sums[c] = the passing packets of chunk c (kChunkTiles = 256 tiles, one per
 // thread): the popcounts of the tiles' verdict words.
@@ -1540,21 +1315,6 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
             // (profiles/r02/ab/pipe_grid.txt; before that change the residency was level or
             // better).
             const int cap2 = 2 * cu_count();
-            if constexpr (F != 2) {
-                static const bool pipe2 = [] {   // BT_PIPE2=1: round B one tile ahead (A/B)
-                    const char* e = getenv("BT_PIPE2");
-                    return e && *e && *e != '0';
-                }();
-                if (pipe2) {
-                    if (a.desc_words == 1)
-                        go(bt_parse_filter_pipe2<REC, F, 1>,
-                           grid > 0 ? 0 : std::min(cap2, resident_grid<bt_parse_filter_pipe2<REC, F, 1>>(dyn)));
-                    else
-                        go(bt_parse_filter_pipe2<REC, F, 2>,
-                           grid > 0 ? 0 : std::min(cap2, resident_grid<bt_parse_filter_pipe2<REC, F, 2>>(dyn)));
-                    return;
-                }
-            }
             if (a.desc_words == 1)
                 go(bt_parse_filter_pipe<REC, F, 1>,
                    grid > 0 ? 0 : std::min(cap2, resident_grid<bt_parse_filter_pipe<REC, F, 1>>(dyn)));
