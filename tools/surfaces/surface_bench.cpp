@@ -2,7 +2,7 @@
 // to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
 // integrator calls").
 //
-//   surface_bench [all|filter|ref|mt|parser|sizes|single|group|plugin] [--packets N] [--seconds S] [--threads T]
+//   surface_bench [all|filter|ref|mt|parser|sizes|single|group|plugin|plugin-hot] [--packets N] [--seconds S] [--threads T]
 //                 [--plugin SO] [--chunks 16384,65536] [--members 1,2,4]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
@@ -22,6 +22,8 @@
 //   single    one packet per call (applyFilters(const Packet&), parsePacket(slice, name)) and small
 //             classify() batches, host branch against device branch: bench_single below;
 //   group     one GpuPacketFilter over a device group of 1 / 2 / 4 members: bench_group below;
+//   plugin-hot  the plugin fed by producers that copy each frame into a fresh buffer just
+//             before onPacket (a capture backend's just-received frames);
 //   plugin    libgpu_parse_filter_plugin.so through createPlugin(): onPacket from 1 and from
 //             T threads (PluginManager::processPacket's per-packet call), until the verdict
 //             sink has seen every packet.
@@ -529,7 +531,12 @@ void bench_group(const Capture& c, int threads, double seconds, const std::vecto
     }
 }
 
-void bench_plugin(const Capture& c, int threads, double seconds, const char* so) {
+// hot: each producer copies the frame into a fresh heap buffer right before onPacket, as a
+// capture backend hands over a just-received frame (the reference's AF_PacketBackend: recv()
+// + a heap copy per packet, src/AF_PacketBackend.cpp:318-363; GpuAfPacketBackend copies each
+// frame into its own Packet the same way): the frame's bytes are in the producer's cache when
+// the plugin sees them, which is what BEATRICE_GPU_PACK (copying the prefix at onPacket) needs.
+void bench_plugin(const Capture& c, int threads, double seconds, const char* so, bool hot = false) {
     void* h = dlopen(so, RTLD_LAZY);
     if (!h) {
         std::fprintf(stderr, "dlopen %s: %s\n", so, dlerror());
@@ -546,6 +553,17 @@ void bench_plugin(const Capture& c, int threads, double seconds, const char* so)
     set_sink(p, [](void* u, const gpu_verdict_batch* b) { *static_cast<std::atomic<uint64_t>*>(u) += b->n; }, &seen);
     auto feed = [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
+            if (hot) {
+                const size_t len = c.packets[i].length();
+                std::shared_ptr<uint8_t[]> b(new uint8_t[len]);
+                std::memcpy(b.get(), c.packets[i].data(), len);
+                Packet pk(std::shared_ptr<const uint8_t[]>(std::move(b)), len);
+                try {
+                    p->onPacket(pk);
+                } catch (const std::exception&) {
+                }
+                continue;
+            }
             Packet pk = c.packets[i];
             try {
                 p->onPacket(pk);   // PluginManager::processPacket (src/PluginManager.cpp:158-171)
@@ -582,9 +600,11 @@ void bench_plugin(const Capture& c, int threads, double seconds, const char* so)
     while (seen < fed) std::this_thread::yield();
     const auto t1 = Clock::now();
     char extra[200];
-    std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"fed\": %llu, \"batch\": %s",
-                  secs(t0, t_fed), secs(t0, t1), (unsigned long long)fed.load(), getenv("BEATRICE_GPU_BATCH"));
-    line("plugin onPacket -> verdict sink", c, threads, fed / secs(t0, t1), extra);
+    std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"fed\": %llu, \"batch\": %s, "
+                  "\"hot_frames\": %s, \"pack\": \"%s\"", secs(t0, t_fed), secs(t0, t1), (unsigned long long)fed.load(),
+                  getenv("BEATRICE_GPU_BATCH"), hot ? "true" : "false", getenv("BEATRICE_GPU_PACK") ? getenv("BEATRICE_GPU_PACK") : "0");
+    line(hot ? "plugin onPacket (hot frames: heap copy per packet) -> verdict sink" : "plugin onPacket -> verdict sink", c,
+         threads, fed / secs(t0, t1), extra);
     p->onStop();
     set_sink(p, nullptr, nullptr);
     delete p;
@@ -644,6 +664,11 @@ int main(int argc, char** argv) {
         if (what == "all" || what == "sizes") bench_call_sizes(c, seconds);
         if (what == "all" || what == "single") bench_single(c, seconds);
         if (what == "all" || what == "group") bench_group(c, threads, seconds, members);
+        if (what == "plugin-hot") {   // 1 / 8 / 16 producers writing each frame right before onPacket
+            bench_plugin(c, 1, seconds, so, true);
+            if (threads >= 8) bench_plugin(c, 8, seconds, so, true);
+            bench_plugin(c, threads, seconds, so, true);
+        }
         if (what == "all" || what == "plugin") {
             bench_plugin(c, 1, seconds, so);
             if (threads >= 4) bench_plugin(c, threads / 2, seconds, so);   // producers leave CPUs to the plugin
