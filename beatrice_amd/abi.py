@@ -176,6 +176,7 @@ EXPORTS = [
     "bt_group_split_cost", "bt_group_cost", "bt_group_thread_budget", "bt_group_host_register",
     "bt_group_host_unregister", "bt_group_parse_filter_mapped", "bt_context_placement", "bt_node_cpus",
     "bt_usable_cpus", "bt_extract_host", "bt_filter_dfa_pool", "bt_group_split_plan",
+    "bt_group_host_parallel",
 ]
 
 DEST_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)   # bt_format_records_to's dest
@@ -263,6 +264,7 @@ def lib() -> ctypes.CDLL:
         "bt_group_split": (ctypes.c_int, [vp, u32, u32, vp]),
         "bt_group_split_cost": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(SplitCost), vp]),
         "bt_group_split_plan": (ctypes.c_int, [vp, u32, u32, ctypes.POINTER(SplitCost), vp]),
+        "bt_group_host_parallel": (ctypes.c_int, [vp, vp, vp]),
         "bt_group_cost": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, ctypes.POINTER(SplitCost)]),
         "bt_group_thread_budget": (ctypes.c_int, [u32, u32, u32, ctypes.POINTER(u32)]),
         "bt_group_host_register": (ctypes.c_int, [vp, vp, u64]),

@@ -543,6 +543,22 @@ int bt_group_parse_filter_ptrs(bt_group* g, const uint8_t* const* frames, const 
     }
 }
 
+int bt_group_host_parallel(bt_group* g, void (*fn)(void*, uint32_t, uint32_t), void* user) {
+    if (!g || !fn) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
+    try {
+        const uint32_t m = (uint32_t)g->members.size();
+        std::vector<uint32_t> base(m + 1, 0);
+        for (uint32_t k = 0; k < m; ++k) base[k + 1] = base[k] + bt::pool_size(g->members[k]);
+        const uint32_t total = base[m];
+        return run_members(g, [&](uint32_t k) -> int {
+            bt::host_parallel(g->members[k], [&](unsigned w, unsigned) { fn(user, base[k] + w, total); });
+            return BT_OK;
+        });
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_host_parallel: %s", e.what());
+    }
+}
+
 int bt_group_host_register(bt_group* g, void* host, uint64_t bytes) {
     if (!g || !host || !bytes) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / empty range");
     try {

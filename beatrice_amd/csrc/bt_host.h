@@ -40,5 +40,7 @@ int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3
 // Runs fn(worker, n_workers) on every worker of ctx's host pool (the caller is
 // worker 0) and waits; with ctx == NULL it runs fn(0, 1) inline.
 void host_parallel(bt_ctx* ctx, const std::function<void(unsigned, unsigned)>& fn);
+// The size of ctx's host pool (created on first use).
+unsigned pool_size(bt_ctx* ctx);
 
 }  // namespace bt

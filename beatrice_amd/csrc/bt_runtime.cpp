@@ -301,6 +301,8 @@ HostPool& pool_of(bt_ctx* c) {
     return *c->pool;
 }
 
+unsigned pool_size(bt_ctx* ctx) { return pool_of(ctx).size(); }
+
 void host_parallel(bt_ctx* ctx, const std::function<void(unsigned, unsigned)>& fn) {
     if (!ctx) {
         fn(0, 1);

@@ -284,14 +284,15 @@ uint32_t GpuPacketFilter::resolveHost(const Packet& p, uint32_t first) {
 
 namespace {
 
-// fn(lo, hi) over [0, n) split across the context's host threads (bt_host_parallel).
+// fn(lo, hi) over [0, n) split across the group's host threads (bt_group_host_parallel: every
+// member's pool, so a group's whole host budget works on the batch's results).
 template <class Fn>
-void parallel_ranges(bt_ctx* ctx, size_t n, Fn&& fn) {
+void parallel_ranges(bt_group* group, size_t n, Fn&& fn) {
     struct U {
         Fn* fn;
         size_t n;
     } u{&fn, n};
-    bt_host_parallel(ctx, [](void* p, uint32_t w, uint32_t T) {
+    bt_group_host_parallel(group, [](void* p, uint32_t w, uint32_t T) {
         auto* x = static_cast<U*>(p);
         const size_t lo = x->n * w / T, hi = x->n * (w + 1) / T;
         if (lo < hi) (*x->fn)(lo, hi);
@@ -311,10 +312,10 @@ void advise_huge(void* p, size_t bytes) {
 // Faults the (still unconstructed) storage in on the host threads, one write per 4 KiB
 // page, so the serial default construction that follows runs on resident memory instead
 // of taking every page fault (and the zeroing behind it) on the calling thread.
-void prefault(bt_ctx* ctx, void* p, size_t bytes) {
+void prefault(bt_group* group, void* p, size_t bytes) {
     if (bytes < (size_t(16) << 20)) return;
     auto* b = static_cast<volatile uint8_t*>(p);
-    parallel_ranges(ctx, (bytes + 4095) / 4096, [&](size_t lo, size_t hi) {
+    parallel_ranges(group, (bytes + 4095) / 4096, [&](size_t lo, size_t hi) {
         for (size_t k = lo; k < hi; ++k) b[k * 4096] = 0;
     });
 }
@@ -336,7 +337,7 @@ void GpuPacketFilter::forRanges(size_t n, Fn&& fn) {
     if (n < kInlineBelow || inFlight_.load(std::memory_order_relaxed) > 1) {
         if (n) fn(size_t(0), n);
     } else {
-        parallel_ranges(ctx_, n, [&](size_t lo, size_t hi) { fn(lo, hi); });
+        parallel_ranges(group_, n, [&](size_t lo, size_t hi) { fn(lo, hi); });
     }
 }
 
@@ -454,7 +455,7 @@ bool GpuPacketFilter::scanParallel(size_t n, const uint8_t* decide, std::vector<
             }
         }
     };
-    if (bt_host_parallel(ctx_, run, &u) != BT_OK) return false;
+    if (bt_group_host_parallel(group_, run, &u) != BT_OK) return false;
     for (const Part& p : parts)
         if (p.host) return false;
     t.rejected.assign(slots, 0);
@@ -566,7 +567,7 @@ std::vector<GpuPacketFilter::FilterResult> GpuPacketFilter::applyFilters(const s
     // result either way, its strings are copied rather than concatenated per packet.
     results.reserve(t.stop);
     advise_huge(results.data(), t.stop * sizeof(FilterResult));
-    if (inFlight_.load(std::memory_order_relaxed) == 1) prefault(ctx_, results.data(), t.stop * sizeof(FilterResult));
+    if (inFlight_.load(std::memory_order_relaxed) == 1) prefault(group_, results.data(), t.stop * sizeof(FilterResult));
     results.resize(t.stop);
     forRanges(t.stop, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {

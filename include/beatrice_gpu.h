@@ -567,6 +567,12 @@ int      bt_group_cost(bt_group* group, int mapped, int records, int filters, ui
  * member usable / members, at least 1 and at most 8 (one context alone: min(8, usable), the
  * single-context default). Host only; bt_group_create applies it. */
 int      bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member);
+/* bt_host_parallel over the whole group's host threads: fn(user, w, workers) runs once for
+ * every w in [0, workers), workers = the members' pool sizes summed (member k's pool, on its
+ * NUMA node, takes a contiguous range of w); returns when all have. For host-side work on a
+ * batch's results (a filter's decision scan, its FilterResults), so that a group spends its
+ * whole budget there rather than member 0's share of it. */
+int      bt_group_host_parallel(bt_group* group, void (*fn)(void* user, uint32_t worker, uint32_t workers), void* user);
 
 /* Zero-copy over the group (AF_XDP UMEM, TPACKET_V3 ring, output arrays): page-lock a host
  * range once (portable, mapped) and map it into every member's device; each member reads

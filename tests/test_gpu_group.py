@@ -301,3 +301,23 @@ def test_group_placement_and_budget():
         assert grp.cost(False, True, True, 8) == (112, 16, 105)
     finally:
         grp.close()
+
+
+def test_group_host_parallel_covers_every_member_thread():
+    """bt_group_host_parallel: each worker index of the group's whole budget runs once."""
+    import ctypes
+    grp = _group(3, host_threads=12)
+    try:
+        seen = []
+        total = []
+        cb_t = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32)
+
+        def cb(_u, w, T):
+            seen.append(w)
+            total.append(T)
+        f = cb_t(cb)
+        assert abi.lib().bt_group_host_parallel(grp.h, ctypes.cast(f, ctypes.c_void_p), None) == 0
+        assert len(set(total)) == 1 and total[0] == 3 * abi.group_thread_budget(3, abi.usable_cpus(), 12)
+        assert sorted(seen) == list(range(total[0]))
+    finally:
+        grp.close()

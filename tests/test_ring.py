@@ -167,6 +167,90 @@ def test_live_ring_on_loopback():
         s.close()
 
 
+@pytest.mark.skipif(not _can_raw(), reason="no CAP_NET_RAW: cannot open an AF_PACKET ring")
+@pytest.mark.parametrize("rings", [2, 3])
+def test_fanout_hash_rings_split_by_flow(rings):
+    """Per-GPU ring sharding: `rings` TPACKET_V3 rings on lo in one
+    PACKET_FANOUT_HASH group (TpacketV3Ring::Options::fanoutGroup, one ring per GPU worker).
+    The c1 golden frames go out as UDP payloads over 40 flows (distinct source ports); every
+    frame lands in exactly one ring and every flow in one ring, and the walker reads each ring
+    as bt_ring_walk_tpv3 does. Only each datagram's receive copy (sll_pkttype PACKET_HOST) is
+    counted: lo also hands the rings its transmit copy, whose hash is the sending socket's random
+    tx hash, where a NIC's receive ring sees the receive copy alone."""
+    import random
+    from conftest import load_golden
+    g, _ = load_golden("c1")
+    frames = [bytes(g["data"][o:o + n]) for o, n in zip(synth.desc_off(g["desc"]), synth.desc_len(g["desc"]))][:200]
+    bs, nb = 1 << 16, 16
+    group = random.randint(1, 0xFFFF)
+    socks, maps = [], []
+    try:
+        for _ in range(rings):
+            s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3))
+            s.setsockopt(263, 10, 2)                                       # PACKET_VERSION = TPACKET_V3
+            s.setsockopt(263, 5, struct.pack("7I", bs, nb, 2048, bs * nb // 2048, 5, 0, 0))   # PACKET_RX_RING
+            s.bind(("lo", 3))
+            s.setsockopt(263, 18, group | (0 << 16))                       # PACKET_FANOUT, PACKET_FANOUT_HASH
+            socks.append(s)
+            maps.append(mmap.mmap(s.fileno(), bs * nb))
+        sinks = []   # listeners, so that no ICMP port-unreachable (quoting the payload) comes back
+        for p in range(7):
+            k = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            k.bind(("127.0.0.1", 0))
+            sinks.append(k)
+        ports = [k.getsockname()[1] for k in sinks]
+        senders = []
+        for f in range(40):
+            u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            u.bind(("127.0.0.1", 0))
+            senders.append(u)
+        sent = {}
+        for i, fr in enumerate(frames):
+            f = i % 40
+            mark = b"bt-fan-%03d-%02d|" % (i, f)
+            senders[f].sendto(mark + fr, ("127.0.0.1", ports[f % 7]))
+            sent[mark] = f
+        for u in senders + sinks:
+            u.close()
+        time.sleep(0.2)
+        where = {}   # mark -> set of rings
+        for r, m in enumerate(maps):
+            ring = np.frombuffer(m, dtype=np.uint8)
+            desc, taken = abi.ring_walk_tpv3(ring, bs, nb)
+            assert np.array_equal(desc, ru.walk_tpv3(ring, bs, nb)[0])
+            buf = memoryview(m)
+            j = 0
+            for b in range(taken):   # each frame's sll_pkttype: tpacket3_hdr (48 B), then sockaddr_ll
+                status, npk, off = struct.unpack_from("<III", buf, b * bs + 8)
+                for _ in range(npk):
+                    nxt = struct.unpack_from("<I", buf, b * bs + off)[0]
+                    host = buf[b * bs + off + 48 + 10] == 0   # PACKET_HOST
+                    o, n = int(synth.desc_off(desc[j:j + 1])[0]), int(synth.desc_len(desc[j:j + 1])[0])
+                    fr = bytes(ring[o:o + n])
+                    k = fr.find(b"bt-fan-")
+                    if host and k >= 0 and n > 23 and fr[23] == 17:
+                        where.setdefault(fr[k:k + 14], set()).add(r)
+                    off += nxt
+                    j += 1
+            assert j == len(desc)
+            del buf
+            abi.ring_release_tpv3(ring, bs, nb, 0, taken)
+            del ring
+        missing = [m for m in sent if m not in where]
+        assert not missing, f"{len(missing)} frames captured by no ring"
+        assert all(len(v) == 1 for v in where.values()), "a frame landed in two rings"
+        flow_rings = {}
+        for m, f in sent.items():
+            flow_rings.setdefault(f, set()).update(where[m])
+        assert all(len(v) == 1 for v in flow_rings.values()), "a flow was split across rings"
+        assert len({next(iter(v)) for v in flow_rings.values()}) > 1, "every flow hashed to one ring"
+    finally:
+        for m in maps:
+            m.close()
+        for s in socks:
+            s.close()
+
+
 CAPTURE_BIN = os.path.join(os.path.dirname(GOLDEN), "cpp", "test_capture")
 
 
