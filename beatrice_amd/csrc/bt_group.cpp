@@ -360,9 +360,21 @@ int bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* b
     return bt_group_split_cost(lens, n, parts, &kShardCost, bounds);
 }
 
+static int split_cost_exact(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
+                            uint32_t* bounds);
+
 int bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
                         uint32_t* bounds) {
     if (!bounds || !parts || !cost || (n && !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / zero parts");
+    try {
+        return split_cost_exact(lens, n, parts, cost, bounds);
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_INTERNAL, "bt_group_split_cost: %s", e.what());
+    }
+}
+
+static int split_cost_exact(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
+                            uint32_t* bounds) {
     bounds[0] = 0;
     if (parts == 1 || n == 0) {
         for (uint32_t k = 1; k <= parts; ++k) bounds[k] = n;
@@ -411,8 +423,18 @@ int bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested
     return BT_OK;
 }
 
+static int group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out);
+
 int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out) {
     if (!out || !devices || !n_devices) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / no devices");
+    try {
+        return group_create(devices, n_devices, opts, out);
+    } catch (const std::exception& e) {
+        return bt::set_error(BT_E_RESOURCE, "bt_group_create: %s", e.what());
+    }
+}
+
+static int group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out) {
     *out = nullptr;
     for (uint32_t i = 0; i < n_devices; ++i)
         for (uint32_t j = 0; j < i; ++j)
