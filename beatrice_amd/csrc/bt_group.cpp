@@ -24,7 +24,6 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <exception>
 #include <functional>
 #include <memory>
@@ -35,90 +34,14 @@
 #include <vector>
 
 #include "bt_host.h"
+#include "bt_host_pool.h"
 
 namespace {
 
 constexpr uint32_t kTile = 64;
 constexpr uint32_t kMaxPool = 16;   // a context's host pool has at most 16 workers
 
-// One worker thread per member after the first, kept for the group's life, each with its own
-// FIFO of calls: member k's part of a call runs on thread k (member 0's on the caller), so a
-// call creates no thread, and calls from several threads queue per member instead of waiting
-// for each other's whole batch (each member still runs one call at a time: its context
-// serialises them).
-class MemberThreads {
-public:
-    MemberThreads(uint32_t members, const std::vector<const cpu_set_t*>& pins) : q_(members) {
-        for (uint32_t k = 1; k < members; ++k) {
-            if (pins[k]) {
-                q_[k].pin = *pins[k];
-                q_[k].pinned = true;
-            }
-            q_[k].th = std::thread([this, k] { loop(k); });
-        }
-    }
-    ~MemberThreads() {
-        for (size_t k = 1; k < q_.size(); ++k) {
-            {
-                std::lock_guard<std::mutex> lk(q_[k].m);
-                q_[k].stop = true;
-            }
-            q_[k].cv.notify_one();
-            q_[k].th.join();
-        }
-    }
-    // fn(k) for every member k, concurrently; returns when all have. fn must not throw.
-    void run(const std::function<void(uint32_t)>& fn) {
-        Call call;
-        call.fn = &fn;
-        call.pending = (uint32_t)q_.size() - 1;
-        for (size_t k = 1; k < q_.size(); ++k) {
-            {
-                std::lock_guard<std::mutex> lk(q_[k].m);
-                q_[k].jobs.push_back(&call);
-            }
-            q_[k].cv.notify_one();
-        }
-        fn(0);
-        std::unique_lock<std::mutex> lk(call.m);
-        call.cv.wait(lk, [&] { return call.pending == 0; });
-    }
-
-private:
-    struct Call {
-        const std::function<void(uint32_t)>* fn = nullptr;
-        std::mutex m;
-        std::condition_variable cv;
-        uint32_t pending = 0;
-    };
-    struct Queue {
-        std::mutex m;
-        std::condition_variable cv;
-        std::deque<Call*> jobs;
-        bool stop = false;
-        bool pinned = false;
-        cpu_set_t pin{};
-        std::thread th;
-    };
-    void loop(uint32_t k) {
-        Queue& q = q_[k];
-        if (q.pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(q.pin), &q.pin);
-        for (;;) {
-            Call* c;
-            {
-                std::unique_lock<std::mutex> lk(q.m);
-                q.cv.wait(lk, [&] { return q.stop || !q.jobs.empty(); });
-                if (q.jobs.empty()) return;   // stop, and nothing left
-                c = q.jobs.front();
-                q.jobs.pop_front();
-            }
-            (*c->fn)(k);
-            std::lock_guard<std::mutex> lk(c->m);
-            if (--c->pending == 0) c->cv.notify_one();
-        }
-    }
-    std::vector<Queue> q_;
-};
+using bt::MemberThreads;   // bt_host_pool.h
 
 // A host range registered with every member (bt_group_host_register).
 struct Region {

@@ -1,6 +1,6 @@
-// bt_host_pool.h — the context's host thread pool (beatrice_amd/csrc/bt_runtime.cpp), in a
-// header of its own so tests/cpp/test_host_pool.cpp can stress it under ThreadSanitizer on the
-// CPU. Host code only.
+// bt_host_pool.h — the context's host thread pool (beatrice_amd/csrc/bt_runtime.cpp) and a
+// group's member threads (bt_group.cpp), in a header of their own so
+// tests/cpp/test_host_pool.cpp can stress them under ThreadSanitizer on the CPU. Host code only.
 #pragma once
 
 #include <pthread.h>
@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -123,6 +124,86 @@ private:
     cpu_set_t pin_{};
     uint64_t gen_ = 0;
     bool stop_ = false;
+};
+
+// The group's member threads (beatrice_amd/csrc/bt_group.cpp).
+// One worker thread per member after the first, kept for the group's life, each with its own
+// FIFO of calls: member k's part of a call runs on thread k (member 0's on the caller), so a
+// call creates no thread, and calls from several threads queue per member instead of waiting
+// for each other's whole batch (each member still runs one call at a time: its context
+// serialises them).
+class MemberThreads {
+public:
+    MemberThreads(uint32_t members, const std::vector<const cpu_set_t*>& pins) : q_(members) {
+        for (uint32_t k = 1; k < members; ++k) {
+            if (pins[k]) {
+                q_[k].pin = *pins[k];
+                q_[k].pinned = true;
+            }
+            q_[k].th = std::thread([this, k] { loop(k); });
+        }
+    }
+    ~MemberThreads() {
+        for (size_t k = 1; k < q_.size(); ++k) {
+            {
+                std::lock_guard<std::mutex> lk(q_[k].m);
+                q_[k].stop = true;
+            }
+            q_[k].cv.notify_one();
+            q_[k].th.join();
+        }
+    }
+    // fn(k) for every member k, concurrently; returns when all have. fn must not throw.
+    void run(const std::function<void(uint32_t)>& fn) {
+        Call call;
+        call.fn = &fn;
+        call.pending = (uint32_t)q_.size() - 1;
+        for (size_t k = 1; k < q_.size(); ++k) {
+            {
+                std::lock_guard<std::mutex> lk(q_[k].m);
+                q_[k].jobs.push_back(&call);
+            }
+            q_[k].cv.notify_one();
+        }
+        fn(0);
+        std::unique_lock<std::mutex> lk(call.m);
+        call.cv.wait(lk, [&] { return call.pending == 0; });
+    }
+
+private:
+    struct Call {
+        const std::function<void(uint32_t)>* fn = nullptr;
+        std::mutex m;
+        std::condition_variable cv;
+        uint32_t pending = 0;
+    };
+    struct Queue {
+        std::mutex m;
+        std::condition_variable cv;
+        std::deque<Call*> jobs;
+        bool stop = false;
+        bool pinned = false;
+        cpu_set_t pin{};
+        std::thread th;
+    };
+    void loop(uint32_t k) {
+        Queue& q = q_[k];
+        if (q.pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(q.pin), &q.pin);
+        for (;;) {
+            Call* c;
+            {
+                std::unique_lock<std::mutex> lk(q.m);
+                q.cv.wait(lk, [&] { return q.stop || !q.jobs.empty(); });
+                if (q.jobs.empty()) return;   // stop, and nothing left
+                c = q.jobs.front();
+                q.jobs.pop_front();
+            }
+            (*c->fn)(k);
+            std::lock_guard<std::mutex> lk(c->m);
+            if (--c->pending == 0) c->cv.notify_one();
+        }
+    }
+    std::vector<Queue> q_;
 };
 
 }  // namespace bt

@@ -5,7 +5,8 @@
 //   * runs from several caller threads at once (the pool serialises them);
 //   * slow indices (a worker sleeping inside fn) and workers that wake late (runs of
 //     microseconds back to back) never let an index run twice or a run return early;
-//   * destruction with idle workers.
+//   * destruction with idle workers;
+//   * the group's MemberThreads: concurrent callers, each call's fn(k) once per member.
 // Prints "ALL OK" and exits 0, or names the first failure.
 #include <atomic>
 #include <chrono>
@@ -48,10 +49,40 @@ static int check(unsigned T, int runs) {
     return 0;
 }
 
+// The group's member threads: run(fn) from several callers at once, each call's fn(k) exactly
+// once for every member k, calls queued per member in arrival order, destruction while idle.
+static int check_members(uint32_t m, int calls) {
+    std::vector<const cpu_set_t*> pins(m, nullptr);
+    bt::MemberThreads mt(m, pins);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> callers;
+    for (int c = 0; c < 6; ++c)
+        callers.emplace_back([&, c] {
+            for (int r = 0; r < calls; ++r) {
+                std::vector<int> h(m, 0);   // written by the member threads, read after run()
+                std::atomic<int> in{0};
+                mt.run([&](uint32_t k) {
+                    h[k]++;
+                    in.fetch_add(1);
+                    if ((r + c + (int)k) % 61 == 0) std::this_thread::sleep_for(std::chrono::microseconds(30));
+                });
+                if (in.load() != (int)m) bad++;
+                for (uint32_t k = 0; k < m; ++k)
+                    if (h[k] != 1) bad++;
+            }
+        });
+    for (auto& t : callers) t.join();
+    if (bad) return std::printf("FAIL members=%u: %d bad calls\n", m, bad.load()), 1;
+    std::printf("ok   members=%u: %d calls from 6 threads\n", m, 6 * calls);
+    return 0;
+}
+
 int main() {
     int fails = 0;
     for (unsigned T : {1u, 2u, 3u, 8u, 16u}) fails += check(T, 4000);
+    for (uint32_t m : {2u, 3u, 8u}) fails += check_members(m, 1500);
     { bt::HostPool idle(8); }   // destroyed with every worker waiting
+    { bt::MemberThreads idle(4, std::vector<const cpu_set_t*>(4, nullptr)); }
     std::printf(fails ? "FAILED\n" : "ALL OK\n");
     return fails ? 1 : 0;
 }
