@@ -75,6 +75,8 @@ OPT_WIDE_NEVER = 0x400
 OPT_WIDE_ALWAYS = 0x800
 OPT_PIPELINE = 0x2000
 OPT_GROUP_SHARED_DEVICE = 0x4000
+OPT_NO_LEAN_PCIE = 0x8000
+OPT_MAPPED_GATHER_SPARSE = 0x10000
 TIME_KERNEL_EVENTS = 0x1
 TIME_PIPELINED = 0x2
 

@@ -299,6 +299,11 @@ typedef struct bt_opts {
 #define BT_OPT_PIPELINE 0x2000u    /* bt_time_device: steps as bt_parse_filter_device_async */
 #define BT_OPT_GROUP_SHARED_DEVICE 0x4000u /* bt_group_create: allow a device listed twice (tests) */
 #define BT_OPT_NO_LEAN_PCIE 0x8000u /* frames in host memory: read whole 64-B windows (A/B only) */
+#define BT_OPT_MAPPED_GATHER_SPARSE 0x10000u /* bt_group_parse_filter_mapped, filter-only calls over
+                                      bt_pkt_desc: a member whose frames lie far apart (sampled
+                                      mean spacing >= BT_MAPPED_GATHER_ABOVE, default 512 B)
+                                      gathers their prefixes on its host threads instead of
+                                      reading each frame's window over PCIe */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */

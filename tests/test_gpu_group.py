@@ -321,3 +321,23 @@ def test_group_host_parallel_covers_every_member_thread():
         assert sorted(seen) == list(range(total[0]))
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("members", [1, 2])
+def test_group_mapped_sparse_frames_gathered_on_host(members, monkeypatch):
+    """BT_OPT_MAPPED_GATHER_SPARSE: filter-only mapped batches whose frames lie far apart (C4,
+    ~870 B) take each member's host gather, dense ones (C2) stay in place; the outputs are
+    the same either way. BT_MAPPED_GATHER_ABOVE is read once per process, so the test uses the
+    default threshold (512 B)."""
+    for cfg, n in ((synth.C4, 30011), (synth.C2, 20000)):
+        data, desc = synth.capture(cfg, n, seed=0x33)
+        grp = _group(members, flags=abi.OPT_MAPPED_GATHER_SPARSE)
+        try:
+            grp.compile(C3_SET)
+            out = _run_mapped(grp, data, desc, n, records=False)
+            nov = _run_mapped(grp, data, desc, n, records=False, verdict=False)
+        finally:
+            grp.close()
+        _, dec, _ = ol.oracle_run(data, desc, n, C3_SET)
+        _check_filter(out, dec, n)
+        _check_filter(nov, dec, n)

@@ -78,6 +78,7 @@ if a.group:
     grp.compile(FILTERS)
     n = a.packets
     where = {"members": m, "devices": devices, "shared_device": shared, "usable_cpus": abi.usable_cpus(),
+             "flags": a.flags,
              "placement": [grp.placement(k) for k in range(m)], "data_nodes": page_nodes(data),
              "numa_pin": os.environ.get("BT_NUMA_PIN", "1"), "shared_serial": os.environ.get("BT_GROUP_SHARED_SERIAL", "0")}
 
