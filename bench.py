@@ -551,6 +551,58 @@ def cpu_baseline(sample, wl, seconds, cpus):
                       f"instances, disjoint shards"}
 
 
+def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
+    """The product's multi-GPU ingest, in one process: a bt_group over the job's n_dev devices
+    reads one batch of frames in registered host memory (an AF_XDP UMEM / a capture ring's
+    shape: frames back to back) in place, every device its range over its own PCIe link
+    (bt_group_host_register + bt_group_parse_filter_mapped), C3's 5-tuple filter, decisions and
+    verdict words written back into registered host memory. PCIe-inclusive, strong scaling (one
+    batch split n_dev ways), never the line's `value`. Rank 0 runs it after every rank's
+    device-resident timing, the other ranks waiting at a barrier."""
+    import time as _time
+    visible = abi.device_count()
+    if visible < n_dev:
+        return {"skipped": f"rank 0 sees {visible} device(s), the job has {n_dev}"}
+    devs = list(range(n_dev))
+    out = {"workload": "zero-copy ingest, one process, bt_group over the job's devices: frames in registered "
+                       "host memory read in place over each device's PCIe link (bt_group_parse_filter_mapped), "
+                       "C3's 5-tuple filter, decisions + verdict words back into host memory",
+           "n_devices": n_dev, "packets": packets, "scaling": "strong", "pcie_inclusive": True, "unit": "Mpps"}
+    for name, cfg in (("c2", synth.C2), ("c3", synth.C3)):
+        data, desc = synth.capture(cfg, packets)
+        grp = abi.Group(devs)
+        held = []
+        try:
+            grp.compile(C3_FILTERS)
+            tiles = (packets + 63) // 64
+            dec = np.zeros(tiles * 64, np.uint8)
+            ver = np.zeros(tiles, np.uint64)
+            for a in (data, desc, dec, ver):
+                grp.register(a)
+                held.append(a)
+            batch = abi.Batch(data.ctypes.data, desc.ctypes.data, 0, packets, data.nbytes, abi.DESC_PACKED, 0)
+            outs = abi.Outputs(None, packets, ver.ctypes.data, dec.ctypes.data, None, None)
+            grp.run_mapped(batch, outs)   # warm: first touches of the mapping on every device
+            times = []
+            for _ in range(reps):
+                t0 = _time.perf_counter()
+                grp.run_mapped(batch, outs)
+                times.append(_time.perf_counter() - t0)
+            bits = np.unpackbits(ver.view(np.uint8), bitorder="little")[:packets].astype(bool)
+            consistent = bool(np.array_equal(bits, (dec[:packets] >> 6) == 0))
+            med = sorted(times)[len(times) // 2]
+            out[name] = {"value": round(packets / med / 1e6, 1), "best": round(packets / min(times) / 1e6, 1),
+                         "ms_per_call": round(med * 1e3, 3), "pass_fraction": round(float(bits.mean()), 4),
+                         "verdicts_match_decisions": consistent,
+                         "placement": [grp.placement(k) for k in range(n_dev)]}
+        finally:
+            for a in held:
+                grp.unregister(a)
+            grp.close()
+        del data, desc
+    return out
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -640,6 +692,8 @@ def main():
     ap.add_argument("--strong", action="store_true", help="the headline as strong scaling (C5's other half)")
     ap.add_argument("--outputs", default=None,
                     help="A/B only: comma list of the headline's outputs (records,decide,verdict,pass_idx)")
+    ap.add_argument("--group-ingest-packets", type=int, default=1 << 24,
+                    help="packets of the in-process group zero-copy ingest entry (0 = skip it)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -712,6 +766,18 @@ def main():
                         "threads": wide["cores"], "value": wide["value"], "unit": wide["unit"]}
             else:
                 results[key]["cpu_baseline"] = None
+
+    # the product's multi-GPU ingest (one process, every device of the job), after every rank's
+    # device-resident timing: the other ranks wait at a barrier meanwhile
+    if dist is not None:
+        dist.barrier()
+    if rank == 0 and args.group_ingest_packets > 0 and args.configs != "none":
+        try:
+            results["zero_copy_group"] = measure_group_ingest(world, args.group_ingest_packets)
+        except Exception as e:   # reported, never fatal to the line
+            results["zero_copy_group"] = {"error": str(e)[:300]}
+    if dist is not None:
+        dist.barrier()
 
     if rank == 0:
         h = results.pop("__head__")
