@@ -118,7 +118,7 @@ def test_rocprof_stats_agree_with_bench_events(cfg):
 
 
 R02 = os.path.join(ROOT, "profiles", "r02")
-ROUNDS = ["r02", "r03"]   # the closing files of each round since the bench took its current form
+ROUNDS = ["r02", "r03", "r04"]   # the closing files of each round since the bench took its current form
 
 
 def _check_entry(e, n_gpus=1):
@@ -145,7 +145,9 @@ def test_default_line_covers_every_config(rnd):
     assert d["n_gpus"] == 1 and "parse + PacketFilter" in d["config"]["workload"] and "64B" in d["config"]["workload"]
     _check_entry(d)
     assert d["cpu_baseline"]["kind"] == "reference" and d["cpu_baseline"]["cores"] >= 1
+    group = d["configs"].pop("zero_copy_group", None)   # round 4 on: the in-process group ingest entry
     assert set(d["configs"]) == {"c2", "c3", "c4", "c1"}
+    assert group is not None or rnd in ("r02", "r03")
     for k, e in d["configs"].items():
         _check_entry(e)
         assert e["cpu_baseline"] and e["cpu_baseline"]["value"] > 0, k
@@ -162,7 +164,7 @@ def test_default_line_timing_form(rnd):
     on every main kernel) whose mean is the roofline's kernel_ms and whose steps run as
     fast as the timed ones (the warm-up leads straight into the timed region)."""
     d = _line(os.path.join(ROOT, "profiles", rnd, "bench_default.json"))
-    entries = [("c2f", d)] + list(d["configs"].items())
+    entries = [("c2f", d)] + [(k, e) for k, e in d["configs"].items() if k != "zero_copy_group"]
     for k, e in entries:
         t, r = e["timing"], e["roofline"]
         assert t["kernel_events_in_timed_region"] is False, k
@@ -181,7 +183,7 @@ def test_default_line_timing_form(rnd):
 def test_two_rank_line_has_per_rank_entries(rnd):
     d = _line(os.path.join(ROOT, "profiles", rnd, "bench_2rank_one_gpu.json"))
     assert d["n_gpus"] == 2 and len(d["per_rank"]) == 2
-    assert set(d["configs"]) == {"c3", "c3_strong"}
+    assert set(d["configs"]) - {"zero_copy_group"} == {"c3", "c3_strong"}
     assert d["configs"]["c3"]["scaling"] == "weak" and d["configs"]["c3_strong"]["scaling"] == "strong"
     s = d["configs"]["c3_strong"]
     assert sum(r["packets"] for r in s["per_rank"]) == s["packets_total"] == 1 << 24
@@ -206,6 +208,25 @@ def test_round_rocprof_stats_agree_with_bench_events(rnd, cfg):
     assert len(rows) == 1
     assert under["roofline"]["kernel"] in rows[0]["Name"]
     assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(under["roofline"]["kernel_ms"], rel=0.05)
+
+
+def test_group_ingest_entry():
+    """Round 4's `configs.zero_copy_group`: the one-process bt_group over the job's devices reading
+    frames in registered host memory in place. At N=1 it ran (one member); on the one-GPU box's
+    rank rehearsals it says why it was skipped instead of measuring one device as N."""
+    d = _line(os.path.join(ROOT, "profiles", "r04", "bench_default.json"))
+    g = d["configs"]["zero_copy_group"]
+    assert g["n_devices"] == 1 and g["scaling"] == "strong" and g["pcie_inclusive"] is True
+    for cap in ("c2", "c3"):
+        e = g[cap]
+        assert e["verdicts_match_decisions"] is True and 0 < e["pass_fraction"] < 1
+        assert e["value"] == pytest.approx(g["packets"] / (e["ms_per_call"] * 1e-3) / 1e6, rel=2e-3)
+        assert len(e["placement"]) == 1
+    # PCIe-inclusive: never the line's value, and far below the device-resident rate
+    assert g["c2"]["value"] < d["value"] / 10
+    for n in (2, 4):
+        r = _line(os.path.join(ROOT, "profiles", "r04", f"bench_{n}rank_one_gpu.json"))
+        assert "skipped" in r["configs"]["zero_copy_group"]
 
 
 def test_committed_traffic_is_keyed_to_these_kernels():

@@ -19,4 +19,9 @@ for path in sys.argv[1:]:
     print(f"{path}: n_gpus {d.get('n_gpus')} {d['config'].get('devices_distinct', '')}")
     one("head", d)
     for k, e in (d.get("configs") or {}).items():
-        one(k, e)
+        if "value" in e:
+            one(k, e)
+        else:   # the group ingest entry: one value per capture, or why it was skipped
+            print(f"{path} {k}: " + ", ".join(f"{c} {v['value']} Mpps" for c, v in e.items()
+                                               if isinstance(v, dict) and "value" in v)
+                  + (e.get("skipped") or e.get("error") or ""))
