@@ -258,7 +258,10 @@ public:
 private:
     using Clock = std::chrono::steady_clock;
     static constexpr size_t kShards = 32;
-    struct Shard {
+    // One shard per 128 B (two lines, the adjacent-line prefetch pair): a shard's lock and
+    // vector ends are written on every onPacket, and neighbouring shards in one line made
+    // every append a cache-line transfer between two producer threads.
+    struct alignas(128) Shard {
         std::mutex mu;
         HeldBatch pending;
         std::atomic<int64_t> first{0};   // arrival of the pending batch's first packet (ticks)
@@ -408,6 +411,9 @@ private:
                 q.batch.clear();
                 drop.clear();
                 lk.lock();
+                // (handing the cleared vectors to clean_ here, capacity kept, was measured: no
+                // gain at 8 / 16 producers and one producer 40 % slower, writing into lines the
+                // classifier's core last held; profiles/r04/surfaces/ab_plugin_shard_align.jsonl)
             }
             done_cv_.notify_all();
         }

@@ -52,6 +52,8 @@
 #include "beatrice/PacketFilter.hpp"
 #include "beatrice_gpu_plugin.h"
 
+#include <sys/resource.h>
+
 extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
 extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
 
@@ -536,6 +538,18 @@ void bench_group(const Capture& c, int threads, double seconds, const std::vecto
 // + a heap copy per packet, src/AF_PacketBackend.cpp:318-363; GpuAfPacketBackend copies each
 // frame into its own Packet the same way): the frame's bytes are in the producer's cache when
 // the plugin sees them, which is what BEATRICE_GPU_PACK (copying the prefix at onPacket) needs.
+// the job cgroup's throttled time (cgroup v2 cpu.stat), -1 when not readable
+long long cgroup_throttled_usec() {
+    FILE* f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+    if (!f) return -1;
+    char key[64];
+    long long v, out = -1;
+    while (std::fscanf(f, "%63s %lld", key, &v) == 2)
+        if (!std::strcmp(key, "throttled_usec")) out = v;
+    std::fclose(f);
+    return out;
+}
+
 void bench_plugin(const Capture& c, int threads, double seconds, const char* so, bool hot = false) {
     void* h = dlopen(so, RTLD_LAZY);
     if (!h) {
@@ -579,6 +593,9 @@ void bench_plugin(const Capture& c, int threads, double seconds, const char* so,
     // shards have grown, the device pass is warm), then the last partial batches are flushed
     std::atomic<uint64_t> fed{0};
     std::atomic<bool> stop{false};
+    struct rusage ru0, ru1;
+    getrusage(RUSAGE_SELF, &ru0);
+    const long long thr0 = cgroup_throttled_usec();
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
@@ -599,10 +616,17 @@ void bench_plugin(const Capture& c, int threads, double seconds, const char* so,
     flush(p);
     while (seen < fed) std::this_thread::yield();
     const auto t1 = Clock::now();
-    char extra[200];
+    getrusage(RUSAGE_SELF, &ru1);
+    const long long thr1 = cgroup_throttled_usec();
+    auto tv = [](const timeval& a) { return a.tv_sec + a.tv_usec * 1e-6; };
+    const double cpu_s = tv(ru1.ru_utime) - tv(ru0.ru_utime) + tv(ru1.ru_stime) - tv(ru0.ru_stime);
+    char extra[400];
     std::snprintf(extra, sizeof(extra), "\"onPacket_s\": %.4f, \"seconds\": %.4f, \"fed\": %llu, \"batch\": %s, "
-                  "\"hot_frames\": %s, \"pack\": \"%s\"", secs(t0, t_fed), secs(t0, t1), (unsigned long long)fed.load(),
-                  getenv("BEATRICE_GPU_BATCH"), hot ? "true" : "false", getenv("BEATRICE_GPU_PACK") ? getenv("BEATRICE_GPU_PACK") : "0");
+                  "\"hot_frames\": %s, \"pack\": \"%s\", \"cpu_s\": %.3f, \"sys_s\": %.3f, \"minflt\": %ld, "
+                  "\"cgroup_throttled_ms\": %.1f, \"plugin\": \"%s\"", secs(t0, t_fed), secs(t0, t1), (unsigned long long)fed.load(),
+                  getenv("BEATRICE_GPU_BATCH"), hot ? "true" : "false", getenv("BEATRICE_GPU_PACK") ? getenv("BEATRICE_GPU_PACK") : "0",
+                  cpu_s, tv(ru1.ru_stime) - tv(ru0.ru_stime), ru1.ru_minflt - ru0.ru_minflt,
+                  thr0 >= 0 && thr1 >= 0 ? (thr1 - thr0) / 1e3 : -1.0, so);
     line(hot ? "plugin onPacket (hot frames: heap copy per packet) -> verdict sink" : "plugin onPacket -> verdict sink", c,
          threads, fed / secs(t0, t1), extra);
     p->onStop();
