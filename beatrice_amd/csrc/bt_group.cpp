@@ -21,6 +21,7 @@
 #include <pthread.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -613,9 +614,14 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
                     return bt::set_error(BT_E_INTERNAL, "hipHostRegister (scratch): %s",
                                          hipGetErrorString(hipGetLastError()));
                 }
+                if (int rc = alias_all(g, p, &g->scratch_dev)) {   // no half-made scratch for later calls
+                    (void)hipHostUnregister(p);
+                    free(p);
+                    g->scratch_dev.clear();
+                    return rc;
+                }
                 g->scratch = static_cast<uint64_t*>(p);
                 g->scratch_words = bytes / 8;
-                if (int rc = alias_all(g, p, &g->scratch_dev)) return rc;
             }
             ver = g->scratch;
             ver_dev = g->scratch_dev;
@@ -689,13 +695,29 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
             }
             return sum >= gather_above * samples;
         };
+        // the host gather reads each frame at base + off directly: only when every frame of the
+        // range lies inside the batch's bytes (the kernels clamp reads at `bytes` instead)
+        auto in_bounds = [&](bt_ctx* c, uint32_t lo, uint32_t hi) {
+            const uint64_t* d = static_cast<const uint64_t*>(b->desc);
+            std::atomic<bool> ok{true};
+            bt::host_parallel(c, [&](unsigned w, unsigned T) {
+                const uint32_t a = lo + (uint32_t)((uint64_t)(hi - lo) * w / T);
+                const uint32_t e = lo + (uint32_t)((uint64_t)(hi - lo) * (w + 1) / T);
+                for (uint32_t i = a; i < e; ++i)
+                    if (BT_DESC_OFF(d[i]) + BT_DESC_LEN(d[i]) > b->bytes) {
+                        ok.store(false, std::memory_order_relaxed);
+                        return;
+                    }
+            });
+            return ok.load();
+        };
         // phase 1: every member's kernels over its range, then its pass count (per pool worker)
         std::vector<std::vector<uint32_t>> cnt(m);
         int rc = run_members(g, [&](uint32_t k) -> int {
             const uint32_t lo = r[k].lo, hi = r[k].hi;
             if (lo == hi) return BT_OK;
             bt_ctx* c = g->members[k];
-            if (may_gather && sparse(lo, hi)) {   // host addresses: the frames, the outputs' host side
+            if (may_gather && sparse(lo, hi) && in_bounds(c, lo, hi)) {   // host addresses: frames, outputs
                 if (int e = bt_parse_filter(c, b->base, static_cast<const bt_pkt_desc*>(b->desc) + lo, hi - lo, nullptr,
                                             ver ? ver + lo / kTile : nullptr, o->decide ? o->decide + lo : nullptr,
                                             nullptr, nullptr))

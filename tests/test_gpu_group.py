@@ -99,7 +99,8 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True, verdict=True, pass_list=True):
+def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True, verdict=True, pass_list=True,
+                nbytes=None):
     """Registers the batch and the device-written outputs with the group, runs the mapped call,
     unregisters. Returns the outputs (records still in the tiled device layout)."""
     tiles = max(1, (n + 63) // 64)
@@ -112,7 +113,7 @@ def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True,
     for a in held:
         grp.register(a)
     try:
-        batch = abi.Batch(_ptr(base), _ptr(desc), stride, n, base.nbytes, fmt, 0)
+        batch = abi.Batch(_ptr(base), _ptr(desc), stride, n, base.nbytes if nbytes is None else nbytes, fmt, 0)
         outs = abi.Outputs(_ptr(h_rec), n, _ptr(h_ver), _ptr(h_dec), _ptr(pidx) if pass_list else None,
                            npass.ctypes.data)
         grp.run_mapped(batch, outs)
@@ -341,3 +342,27 @@ def test_group_mapped_sparse_frames_gathered_on_host(members, monkeypatch):
         _, dec, _ = ol.oracle_run(data, desc, n, C3_SET)
         _check_filter(out, dec, n)
         _check_filter(nov, dec, n)
+
+
+@pytest.mark.parametrize("members", [1, 2])
+def test_group_mapped_sparse_gather_keeps_the_bytes_bound(members):
+    """A frame that runs past batch.bytes: the host gather would read it at base + off
+    directly, so the member whose range holds it stays on the kernels (which clamp reads at
+    `bytes`); the outputs equal the same batch without the option."""
+    n = 30011
+    data, desc = synth.capture(synth.C4, n, seed=0x34)
+    last = int(synth.desc_off(desc)[-1])
+    nbytes = last + 20   # the last frame's window crosses the end of the batch
+    outs = []
+    for flags in (abi.OPT_MAPPED_GATHER_SPARSE, 0):
+        grp = _group(members, flags=flags)
+        try:
+            grp.compile(C3_SET)
+            outs.append(_run_mapped(grp, data, desc, n, records=False, nbytes=nbytes))
+        finally:
+            grp.close()
+    a, b = outs
+    assert np.array_equal(a["decide"], b["decide"]) and np.array_equal(a["verdict"], b["verdict"])
+    assert np.array_equal(a["pass_idx"], b["pass_idx"])
+    _, dec, _ = ol.oracle_run(data, desc, n - 1, C3_SET)   # every frame inside the bytes: the oracle's
+    assert np.array_equal(a["decide"][:n - 1], dec)
