@@ -593,6 +593,30 @@ void pipeline_run(bt_ctx* c, uint32_t cnt, Fn&& fn) {
     }
 }
 
+// One frame's staged prefix: m bytes of src to dst (16-B aligned, its slot rounded up to 16).
+// With `nt`, whole 16-B chunks go out as non-temporal stores (no read-for-ownership of the
+// staging lines, which only the DMA engine reads next); the tail chunk is assembled from the
+// frame's last bytes, never read past them. The caller fences (sfence) before the copy's
+// consumer runs.
+typedef long long v2i64 __attribute__((vector_size(16)));
+inline void stage_prefix(uint8_t* dst, const uint8_t* src, uint32_t m, bool nt) {
+    if (!nt) {
+        std::memcpy(dst, src, m);
+        return;
+    }
+    uint32_t k = 0;
+    for (; k + 16 <= m; k += 16) {
+        v2i64 x;
+        std::memcpy(&x, src + k, 16);
+        __builtin_nontemporal_store(x, reinterpret_cast<v2i64*>(dst + k));
+    }
+    if (k < m) {
+        v2i64 x{};
+        std::memcpy(&x, src + k, m - k);
+        __builtin_nontemporal_store(x, reinterpret_cast<v2i64*>(dst + k));
+    }
+}
+
 // Copies one finished chunk from pinned staging into the caller's buffers.
 void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint8_t* decide) {
     const uint32_t chunk = c->chunk;
@@ -1060,6 +1084,13 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
     // the payload window's too (bytes past the staged prefix would be the next frame's)
     const uint32_t slot = stage_bytes(c, records != nullptr);
     static const bool prefetch = getenv("BT_NO_GATHER_PREFETCH") == nullptr;   // A/B knobs
+    // non-temporal staging stores (BT_GATHER_NT=0: plain copies). Same-box A/B, 5 pairs over
+    // two boxes (profiles/r04/e2e/ab_gather_nt*.jsonl): C2 verdicts +2..+34 % in every pair,
+    // C4 +8 % on average, C3 level
+    static const bool nt = [] {
+        const char* e = getenv("BT_GATHER_NT");
+        return !e || atoi(e) != 0;
+    }();
     static const uint32_t kGatherAhead = [] {
         const char* e = getenv("BT_GATHER_AHEAD");
         return e && atoi(e) > 0 ? (uint32_t)atoi(e) : kGatherAheadDefault;
@@ -1104,10 +1135,11 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                     uint32_t len = 0;
                     const uint8_t* f = frame(base_i + i, &len);
                     const uint32_t m = std::min(len, slot);
-                    if (m) std::memcpy(pre + p, f, m);
+                    if (m) stage_prefix(pre + p, f, m, nt);
                     d[i] = BT_DESC(p, len);
                     p += (m + 15) & ~15u;
                 }
+                if (nt) __builtin_ia32_sfence();   // the prefixes are visible before the H2D copy
             });
             const uint64_t pos = part[T];
             const size_t pre_bytes = (pos + 15) & ~15ull;
