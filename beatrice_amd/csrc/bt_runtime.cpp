@@ -625,12 +625,27 @@ void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint
     const uint64_t* ver = reinterpret_cast<const uint64_t*>(dec + chunk);
     const unsigned T = c->pool->size();
     const uint32_t lo = s.lo, cnt = s.cnt;
+    static const bool drain_nt = [] {   // A/B knob: BT_DRAIN_NT=1 streams the records out
+        const char* e = getenv("BT_DRAIN_NT");
+        return e && atoi(e) != 0;
+    }();
     pipeline_run(c, cnt, [&](unsigned w) {   // split on 64-packet boundaries
         const uint32_t tiles = (cnt + 63) / 64;
         const uint32_t t0 = (uint32_t)((uint64_t)tiles * w / T), t1 = (uint32_t)((uint64_t)tiles * (w + 1) / T);
         const uint32_t a = t0 * 64, b = std::min(cnt, t1 * 64);
         if (a >= b) return;
-        if (records) std::memcpy(records + lo + a, rec + (size_t)a * BT_REC_BYTES, (size_t)(b - a) * BT_REC_BYTES);
+        if (records) {
+            uint8_t* dst = reinterpret_cast<uint8_t*>(records + lo + a);
+            const uint8_t* src = rec + (size_t)a * BT_REC_BYTES;
+            const size_t bytes = (size_t)(b - a) * BT_REC_BYTES;   // a multiple of 16
+            if (drain_nt && ((uintptr_t)dst & 15u) == 0) {   // the caller's records: not read back here
+                for (size_t k = 0; k < bytes; k += 16)
+                    __builtin_nontemporal_store(*reinterpret_cast<const v2i64*>(src + k), reinterpret_cast<v2i64*>(dst + k));
+                __builtin_ia32_sfence();
+            } else {
+                std::memcpy(dst, src, bytes);
+            }
+        }
         if (decide) std::memcpy(decide + lo + a, dec + a, b - a);
         if (verdict) std::memcpy(verdict + (lo + a) / 64, ver + a / 64, (size_t)(t1 - t0) * 8);
     });
