@@ -595,6 +595,19 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
                          "ms_per_call": round(med * 1e3, 3), "pass_fraction": round(float(bits.mean()), 4),
                          "verdicts_match_decisions": consistent,
                          "placement": [grp.placement(k) for k in range(n_dev)]}
+            if name == "c3":   # the same frames through the members' host gathers (bt_group_parse_filter)
+                grp.run_host(data, desc, records=False)
+                ht = []
+                for _ in range(reps):
+                    t0 = _time.perf_counter()
+                    h = grp.run_host(data, desc, records=False)
+                    ht.append(_time.perf_counter() - t0)
+                hm = sorted(ht)[len(ht) // 2]
+                out["c3_host_gather"] = {
+                    "value": round(packets / hm / 1e6, 1), "best": round(packets / min(ht) / 1e6, 1),
+                    "ms_per_call": round(hm * 1e3, 3), "decisions_match_zero_copy": bool(np.array_equal(h["decide"], dec[:packets])),
+                    "workload": "C3 frames in ordinary host memory: each member gathers its range's 48-B prefixes on "
+                                "its NUMA-pinned host threads into pinned staging, H2D, kernels, verdicts back"}
         finally:
             for a in held:
                 grp.unregister(a)
