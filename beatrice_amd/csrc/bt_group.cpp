@@ -70,6 +70,14 @@ struct bt_group {
     uint64_t* scratch = nullptr;
     size_t scratch_words = 0;
     std::vector<uint8_t*> scratch_dev;
+    // host batches: a call that finds another one in flight runs whole on the least busy
+    // member (up to route_below packets; BT_GROUP_ROUTE_BELOW, 0 = always split) instead of
+    // splitting, so concurrent callers spread over the members (and the lanes of a device
+    // listed twice) rather than each paying every member's per-call cost; a lone call splits
+    std::atomic<uint32_t> calls{0};
+    std::unique_ptr<std::atomic<uint32_t>[]> busy;   // per member: call parts running on it
+    std::atomic<uint32_t> rr{0};
+    uint32_t route_below = 0;
 };
 
 namespace {
@@ -182,11 +190,30 @@ int run_members(bt_group* g, Fn fn) {
     return BT_OK;
 }
 
+// Holds a counter up for a scope.
+struct Hold {
+    std::atomic<uint32_t>& a;
+    explicit Hold(std::atomic<uint32_t>& x) : a(x) { a.fetch_add(1, std::memory_order_acq_rel); }
+    ~Hold() { a.fetch_sub(1, std::memory_order_acq_rel); }
+};
+
 // One host batch over the group: frames(ctx, lo, cnt, ...) runs packets [lo, lo + cnt).
 template <class LenAt, class Frames>
 int group_batch(bt_group* g, uint32_t n, LenAt len, Frames frames, bt_rec* records, uint64_t* verdict,
                 uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
     const uint32_t m = (uint32_t)g->members.size();
+    const uint32_t others = g->calls.load(std::memory_order_acquire);
+    Hold in_flight(g->calls);
+    if (m > 1 && others > 0 && n <= g->route_below) {   // concurrent callers: whole calls, spread
+        const uint32_t start = g->rr.fetch_add(1, std::memory_order_relaxed) % m;
+        uint32_t k = start, least = UINT32_MAX;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t c = (start + j) % m, v = g->busy[c].load(std::memory_order_relaxed);
+            if (v < least) least = v, k = c;
+        }
+        Hold on(g->busy[k]);
+        return frames(g->members[k], 0, n, records, verdict, decide, pass_idx, n_pass);
+    }
     const bool want_filter = verdict || decide || pass_idx || n_pass;
     bt_split_cost cost{};
     (void)bt_group_cost(g, 0, records != nullptr, want_filter, 8, &cost);
@@ -198,6 +225,7 @@ int group_batch(bt_group* g, uint32_t n, LenAt len, Frames frames, bt_rec* recor
     int rc = run_members(g, [&](uint32_t k) -> int {
         const uint32_t lo = r[k].lo, cnt = r[k].hi - r[k].lo;
         if (!cnt) return BT_OK;
+        Hold on(g->busy[k]);
         return frames(g->members[k], lo, cnt, records ? records + lo : nullptr, verdict ? verdict + lo / kTile : nullptr,
                       decide ? decide + lo : nullptr, pass_idx ? pass_idx + lo : nullptr,
                       want_pass ? &npass[k] : nullptr);
@@ -398,6 +426,10 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         }
         const char* e = getenv("BT_GROUP_SHARED_SERIAL");
         g->serial_shared = e && atoi(e) != 0;
+        const char* rb = getenv("BT_GROUP_ROUTE_BELOW");
+        g->route_below = rb ? (uint32_t)strtoul(rb, nullptr, 10) : (1u << 20);
+        g->busy = std::make_unique<std::atomic<uint32_t>[]>(n_devices);
+        for (uint32_t i = 0; i < n_devices; ++i) g->busy[i].store(0, std::memory_order_relaxed);
     }
     if (n_devices > 1) {
         std::vector<const cpu_set_t*> pins;

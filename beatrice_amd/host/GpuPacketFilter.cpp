@@ -104,7 +104,14 @@ void GpuPacketFilter::open(const std::vector<int>& devices, const bt_opts* opts)
         throw std::runtime_error("GpuPacketFilter: libbeatrice_gpu.so has C-ABI version " +
                                  std::to_string(bt_abi_version()) + ", this adapter needs " +
                                  std::to_string(BT_ABI_VERSION));
-    if (bt_group_create(devices.data(), (uint32_t)devices.size(), opts, &group_) != BT_OK)
+    // a device listed more than once is that many lanes on it (contexts with their own staging,
+    // streams and host threads): concurrent callers' device passes then overlap on the device
+    bt_opts o{};
+    if (opts) o = *opts;
+    for (size_t i = 0; i < devices.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (devices[i] == devices[j]) o.flags |= BT_OPT_GROUP_SHARED_DEVICE;
+    if (bt_group_create(devices.data(), (uint32_t)devices.size(), &o, &group_) != BT_OK)
         throw std::runtime_error(std::string("GpuPacketFilter: ") + bt_last_error());
     ctx_ = bt_group_member(group_, 0);
 }

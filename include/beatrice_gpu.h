@@ -297,7 +297,12 @@ typedef struct bt_opts {
 #define BT_OPT_WIDE_NEVER 0x400u   /* descriptor mode: always two-round loads (A/B only)   */
 #define BT_OPT_WIDE_ALWAYS 0x800u  /* descriptor mode: always wide round A (A/B only)      */
 #define BT_OPT_PIPELINE 0x2000u    /* bt_time_device: steps as bt_parse_filter_device_async */
-#define BT_OPT_GROUP_SHARED_DEVICE 0x4000u /* bt_group_create: allow a device listed twice (tests) */
+#define BT_OPT_GROUP_SHARED_DEVICE 0x4000u /* bt_group_create: allow a device listed more than once:
+                                      that many lanes (contexts) on it; concurrent host batches
+                                      then run whole on the least busy member (groups route a
+                                      call that finds another in flight, up to
+                                      BT_GROUP_ROUTE_BELOW packets, default 1M, instead of
+                                      splitting it) */
 #define BT_OPT_NO_LEAN_PCIE 0x8000u /* frames in host memory: read whole 64-B windows (A/B only) */
 #define BT_OPT_MAPPED_GATHER_SPARSE 0x10000u /* bt_group_parse_filter_mapped, filter-only calls over
                                       bt_pkt_desc: a member whose frames lie far apart (sampled

@@ -366,3 +366,37 @@ def test_group_mapped_sparse_gather_keeps_the_bytes_bound(members):
     assert np.array_equal(a["pass_idx"], b["pass_idx"])
     _, dec, _ = ol.oracle_run(data, desc, n - 1, C3_SET)   # every frame inside the bytes: the oracle's
     assert np.array_equal(a["decide"][:n - 1], dec)
+
+
+def test_group_concurrent_callers_routed_whole():
+    """Host batches from several threads at once: a call that finds another in flight runs
+    whole on the least busy member (a device listed twice = two lanes on it) instead of being
+    split; every caller's outputs still equal the oracle's."""
+    import threading
+    caps = [synth.capture(synth.C3, 20000 + 640 * k, seed=0x70 + k) for k in range(6)]
+    exp = [ol.oracle_run(d, q, len(q), C3_SET) for d, q in caps]
+    grp = _group(2)
+    errors = []
+    try:
+        grp.compile(C3_SET)
+
+        def caller(k):
+            try:
+                d, q = caps[k]
+                for _ in range(4):
+                    out = grp.run_host(d, q, records=(k % 2 == 0))
+                    rec, dec, npass = exp[k]
+                    assert np.array_equal(out["decide"], dec) and out["n_pass"] == npass
+                    if k % 2 == 0:
+                        assert np.array_equal(out["records"], rec)
+            except Exception as e:   # reported from the main thread
+                errors.append((k, repr(e)))
+        th = [threading.Thread(target=caller, args=(k,)) for k in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in th), "a caller hung"
+    finally:
+        grp.close()
+    assert not errors, errors
