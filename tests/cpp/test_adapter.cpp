@@ -191,9 +191,12 @@ static bool filter_case(const char* label, const Capture& cap, const std::vector
 // Several threads calling one GpuPacketFilter at once (each on its own shard, in chunks),
 // while another thread keeps re-enabling a filter (a recompile between their calls): every
 // result and the summed stats equal the reference's over the whole capture.
-static bool concurrent_case(const char* label, const Capture& cap, const std::vector<Spec>& specs, int threads) {
+// lanes > 1: device 0 listed that many times (concurrent calls routed whole to the least busy
+// lane); chunk0: the first thread's call size (small calls take the host branch, §1)
+static bool concurrent_case(const char* label, const Capture& cap, const std::vector<Spec>& specs, int threads,
+                            int lanes = 1, size_t chunk0 = 700) {
     PacketFilter ref;
-    GpuPacketFilter gpu(0);
+    GpuPacketFilter gpu(std::vector<int>(lanes, 0));
     install(ref, specs);
     install(gpu, specs);
     const std::vector<PacketFilter::FilterResult> want = ref.applyFilters(cap.packets);
@@ -211,7 +214,7 @@ static bool concurrent_case(const char* label, const Capture& cap, const std::ve
     for (int t = 0; t < threads; ++t)
         th.emplace_back([&, t] {
             const size_t lo = cap.packets.size() * t / threads, hi = cap.packets.size() * (t + 1) / threads;
-            size_t chunk = 700 + 311 * (size_t)t;
+            size_t chunk = chunk0 + 311 * (size_t)t;
             for (size_t at = lo; at < hi; at += chunk) {
                 const std::vector<Packet> part(cap.packets.begin() + at, cap.packets.begin() + std::min(hi, at + chunk));
                 try {
@@ -251,8 +254,8 @@ static bool concurrent_case(const char* label, const Capture& cap, const std::ve
           "%s: stats processed %lu (want %lu) passed %lu (want %lu)", label, (unsigned long)sb.packetsProcessed,
           (unsigned long)(sa.packetsProcessed + twice), (unsigned long)sb.packetsPassed,
           (unsigned long)(sa.packetsPassed + twice_passed));
-    std::printf("ok   concurrent %-19s %zu packets on %d threads + a recompiling thread, %lu passed\n", label,
-                cap.packets.size(), threads, (unsigned long)sa.packetsPassed);
+    std::printf("ok   concurrent %-19s %zu packets on %d threads (%d lane(s), calls of %zu+) + a recompiling thread, "
+                "%lu passed\n", label, cap.packets.size(), threads, lanes, chunk0, (unsigned long)sa.packetsPassed);
     return true;
 }
 
@@ -924,6 +927,12 @@ int main(int argc, char** argv) {
     }
     ok &= concurrent_case("c3/headline", c3, headline, 8);
     ok &= concurrent_case("fuzz/payload+custom", fz, host_side, 6);
+    // device-branch calls (>= 4096 packets) from 8 threads over two lanes on one device
+    {
+        Capture c3b = capture(3, 160000, 0x5EED0035), fzb = capture(9, 120000, 0x5EED0036);
+        ok &= concurrent_case("c3/headline/lanes", c3b, headline, 8, 2, 4096);
+        ok &= concurrent_case("fuzz/host-side/lanes", fzb, host_side, 6, 2, 4096);
+    }
     ok &= parser_case("c3", c3);
     ok &= parser_case("c4", c4);
     ok &= parser_case("fuzz", fz);
