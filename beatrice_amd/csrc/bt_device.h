@@ -53,12 +53,17 @@ struct MainArgs {
     uint32_t dfa_bytes;        // 0: the program has no BT_K_PAYLOAD slot
     uint32_t prefixes;         // BT_BATCH_PREFIXES: base holds header prefixes only
     uint32_t lean;             // descriptor mode: bytes of a frame round A reads at most (0xFFFF:
-                               // its first 64-B window); 46 for host-resident frames (kLeanPcie)
+                               // its first 64-B window); 38 for host-resident frames (kLeanPcie)
+    uint32_t lean_lo;          // ... and the first of them it needs: round A skips the 16-B chunks
+                               // that end at or before it (0; 12 for lean calls: nothing in a
+                               // filter-only call reads the MAC addresses)
 };
-// Frames read over PCIe (registered host memory) by a filter-only call: round A reads
-// the first 46 B of a frame (every filter gate and the detector's 38 B) instead of the
-// whole 64-B window (DESIGN.md §9.2 has the A/B).
-constexpr uint32_t kLeanPcie = 46;
+// Frames read over PCIe (registered host memory) by a filter-only call: round A reads only
+// the 16-B chunks holding bytes 12..37 of a frame (every filter gate and the detector column)
+// instead of the whole 64-B window (DESIGN.md §9.2 has the A/Bs: round 3's first 46 B, round
+// 4's [12, 38): C4 +3..7 %, the others level).
+constexpr uint32_t kLeanPcie = 38;
+constexpr uint32_t kLeanLo = 12;
 
 constexpr uint32_t kDfaPoolMax = 16384;   // bytes of DFA tables per program (LDS budget)
 

@@ -583,7 +583,8 @@ __device__ __forceinline__ void issue_loads(const MainArgs& a, uint32_t t, uint3
             // bytes from a0 this round may read: the frame; when wide, only up to the end
             // of a0's 128-B line (round B takes the next line, and only what is needed)
             const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + min(ql, a.lean);
-            const bool ok = live_q && (16u * c < a_end) && (addr + 16u <= a.bytes);
+            const uint32_t a_lo = wide ? 0u : sq + a.lean_lo;   // chunks ending at or before it: unread
+            const bool ok = live_q && (16u * c < a_end) && (16u * c + 16u > a_lo) && (addr + 16u <= a.bytes);
             st.v[j] = ok ? ld16(a.base + addr, ntl) : make_uint4(0, 0, 0, 0);
             if (wide) {   // chunks 4..7 of the same line
                 const bool okb = live_q && (16u * (c + 4u) < a_end) && (addr + 64u + 16u <= a.bytes);
@@ -1007,7 +1008,8 @@ __device__ __forceinline__ void issue_round_a_pipe(const MainArgs& a, uint32_t l
         st.qa0[j] = a0;
         // bitwise & keeps the conditions branch-free (&& made exec-mask branches)
         const uint32_t a_end = wide ? round_a_end_wide(a0, sq, ql, need_max) : sq + min(ql, a.lean);
-        const bool ok = (16u * c < a_end) & (addr + 16u <= a.bytes);
+        const uint32_t a_lo = wide ? 0u : sq + a.lean_lo;   // chunks ending at or before it: unread
+        const bool ok = (16u * c < a_end) & (16u * c + 16u > a_lo) & (addr + 16u <= a.bytes);
         st.v[j] = ld16(ok ? a.base + addr : zero, ntl);
         if (wide) {
             const bool okb = (16u * (c + 4u) < a_end) & (addr + 64u + 16u <= a.bytes);

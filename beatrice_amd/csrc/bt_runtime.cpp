@@ -470,10 +470,12 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     if (w && !o->verdict) { int rc = ws_touch(c, w, st); if (rc) return rc; }   // the main kernel writes w->verdict
     a.blocked = (c->opts.flags & BT_OPT_TILE_BLOCKED) ? 1u : 0u;
     // Lean round A for frames read over PCIe, filter-only calls: the filters and the
-    // detector read <= 38 B, so a 46-B first round reads 25 % fewer bytes per frame (A/B,
-    // profiles/r03/e2e/lean_ab.jsonl: zero-copy verdicts C3 +17 %, C4 +4..10 %, C2 +2..4 %;
-    // TPACKET_V3 ring C2 / C4 level, C3 -8 %). Calls that also parse would need a second
-    // round for almost every tile (the walk reads to L3 + 40 B) and lost 28-39 %: not lean.
+    // detector read bytes 12..37, so round A reads only the 16-B chunks holding them (A/Bs:
+    // round 3's 46-B first round against the 64-B window, profiles/r03/e2e/lean_ab.jsonl:
+    // zero-copy verdicts C3 +17 %, C4 +4..10 %, C2 +2..4 %; round 4's [12, 38) against
+    // [0, 46), profiles/r04/e2e/ab_lean_lo.jsonl: C4 zero-copy and ring +3..7 %, C2 / C3
+    // level). Calls that also parse would need a second round for almost every tile (the
+    // walk reads to L3 + 40 B) and lost 28-39 %: not lean.
     a.lean = 0xFFFFu;
     const bool lean = b->desc && !o->records && !(c->opts.flags & BT_OPT_NO_LEAN_PCIE) && host_resident(c, b->base);
     a.dfa = c->dfa_dev[c->dfa_cur];
@@ -489,8 +491,18 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
     if (c->opts.flags & BT_OPT_WIDE_ALWAYS) a.nt |= 8u;
+    a.lean_lo = 0;
     if (lean && !(a.nt & 8u)) {   // frames over PCIe: lean round A, never the wide 128-B mode
-        a.lean = kLeanPcie;
+        static const uint32_t lean_end = [] {   // A/B knobs: BT_LEAN_END, BT_LEAN_LO
+            const char* e = getenv("BT_LEAN_END");
+            return e && atoi(e) >= (int)kNeedFilter ? (uint32_t)atoi(e) : kLeanPcie;
+        }();
+        static const uint32_t lean_lo = [] {
+            const char* e = getenv("BT_LEAN_LO");
+            return e && atoi(e) >= 0 && atoi(e) <= 12 ? (uint32_t)atoi(e) : kLeanLo;
+        }();
+        a.lean = lean_end;
+        a.lean_lo = lean_lo;
         a.nt |= 4u;
     }
     int rec = kRecNone;
