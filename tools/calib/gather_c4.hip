@@ -17,7 +17,7 @@
 //              opaque zero from it, as the walk's EtherTypes / IHL decide round B).
 // Each prints ms per launch (median of 15) and the algorithmic rate; bt_parse_filter_pipe's
 // C4 main kernel is bench.py --config c4's roofline.kernel_ms. The same box runs both
-// (tools/gpu_r04g.sh).
+// (tools/gpu_r04.sh c4-ceiling).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
