@@ -677,7 +677,7 @@ std::vector<bt_field_def> table_of_def(const parser::ProtocolDefinition& d) {
 }  // namespace
 
 std::vector<uint8_t> GpuFieldBatch::bytes(size_t i, size_t k) const {
-    const auto& f = def_.fields.at(k);
+    const auto& f = def_->fields.at(k);
     if (!isSuccess(i)) return {};
     const uint8_t* b = image_.data() + i * span_ + f.offset;
     return std::vector<uint8_t>(b, b + f.length);
@@ -686,8 +686,8 @@ std::vector<uint8_t> GpuFieldBatch::bytes(size_t i, size_t k) const {
 ParseResult GpuFieldBatch::result(size_t i) const {   // parsePacketInternal (:238-284)
     ParseResult r;
     const uint32_t len = lens_.at(i);
-    r.protocolName = def_.name;
-    r.protocolVersion = def_.version;
+    r.protocolName = def_->name;
+    r.protocolVersion = def_->version;
     r.rawData.assign(frames_[i], frames_[i] + len);
     r.packetLength = len;
     r.parsedBytes = 0;
@@ -698,8 +698,8 @@ ParseResult GpuFieldBatch::result(size_t i) const {   // parsePacketInternal (:2
     }
     size_t parsed = 0;
     const uint8_t* img = image_.data() + i * span_;
-    for (size_t k = 0; k < def_.fields.size(); ++k) {
-        const auto& f = def_.fields[k];
+    for (size_t k = 0; k < def_->fields.size(); ++k) {
+        const auto& f = def_->fields[k];
         if (f.offset + f.length > len) continue;   // :252-254 (never once len >= span)
         FieldValue v = field_value(f, raw(i, k), img + f.offset);
         r.fields[f.name] = v;   // ParseResult::addField (ParserResult.cpp:351-353)
@@ -740,7 +740,7 @@ void GpuProtocolParser::countParses(const std::string& protocol, uint64_t ok, ui
 }
 
 void GpuProtocolParser::extract(GpuFieldBatch& b) {
-    const auto table = table_of_def(b.def_);
+    const auto table = table_of_def(*b.def_);
     for (const auto& f : table)
         if (f.type == BT_FT_BOOLEAN && f.length == 0)
             throw std::invalid_argument("GpuProtocolParser: BOOLEAN field of length 0 (undefined in the reference)");
@@ -765,13 +765,13 @@ void GpuProtocolParser::extract(GpuFieldBatch& b) {
     if (rc != BT_OK) throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     const uint64_t ok = (uint64_t)std::count(b.status_.begin(), b.status_.end(), (uint8_t)0);
-    countParses(b.def_.name, ok, n - ok, us);
+    countParses(b.def_->name, ok, n - ok, us);
 }
 
 bool GpuProtocolParser::registerProtocol(const parser::ProtocolDefinition& protocol) {   // :41-50
     std::unique_lock<std::shared_mutex> lk(protocols_mu_);
     if (protocols_.find(protocol.name) != protocols_.end()) return false;
-    protocols_[protocol.name] = protocol;
+    protocols_[protocol.name] = std::make_shared<const parser::ProtocolDefinition>(protocol);
     return true;
 }
 
@@ -801,44 +801,56 @@ void GpuProtocolParser::setConfig(const parser::ProtocolParser::ParserConfig& co
     if (config_.enablePerformanceMetrics) profiling_ = true;
 }
 
-GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets,
-                                           const parser::ProtocolDefinition& protocol) {
+GpuProtocolParser::DefPtr GpuProtocolParser::findProtocol(const std::string& name) const {
+    std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+    auto it = protocols_.find(name);
+    return it == protocols_.end() ? nullptr : it->second;
+}
+
+std::vector<GpuProtocolParser::DefPtr> GpuProtocolParser::allProtocols() const {
+    std::shared_lock<std::shared_mutex> lk(protocols_mu_);
+    std::vector<DefPtr> defs;
+    defs.reserve(protocols_.size());
+    for (const auto& kv : protocols_) defs.push_back(kv.second);   // the reference's iteration order (:117)
+    return defs;
+}
+
+GpuFieldBatch GpuProtocolParser::batchOf(const std::vector<Packet>& packets, DefPtr def) {
     GpuFieldBatch b;
-    b.def_ = protocol;
+    b.def_ = std::move(def);
     adopt(ctx_, packets, b);
     extract(b);
     return b;
 }
 
+GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets,
+                                           const parser::ProtocolDefinition& protocol) {
+    return batchOf(packets, std::make_shared<const parser::ProtocolDefinition>(protocol));
+}
+
 GpuFieldBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets, const std::string& protocolName) {
-    parser::ProtocolDefinition def;
-    {
-        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
-        auto it = protocols_.find(protocolName);
-        if (it == protocols_.end()) throw std::out_of_range("GpuProtocolParser: protocol not found: " + protocolName);
-        def = it->second;
-    }
-    return parseBatch(packets, def);
+    DefPtr def = findProtocol(protocolName);
+    if (!def) throw std::out_of_range("GpuProtocolParser: protocol not found: " + protocolName);
+    return batchOf(packets, std::move(def));
 }
 
 std::vector<GpuFieldBatch> GpuProtocolParser::parseBatchMultipleProtocols(const std::vector<Packet>& packets) {
-    std::vector<parser::ProtocolDefinition> defs;
-    {
-        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
-        for (const auto& kv : protocols_) defs.push_back(kv.second);   // the reference's iteration order (:117)
-    }
     std::vector<GpuFieldBatch> out;
-    for (const auto& d : defs) out.push_back(parseBatch(packets, d));
+    for (auto& d : allProtocols()) out.push_back(batchOf(packets, std::move(d)));
     return out;
 }
 
-ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol) {
+ParseResult GpuProtocolParser::parseOne(const std::vector<uint8_t>& packet, DefPtr def) {
     GpuFieldBatch b;   // :97-110; a batch of one, borrowing the caller's vector for the call
-    b.def_ = protocol;
+    b.def_ = std::move(def);
     b.frames_.push_back(packet.data());
     b.lens_.push_back((uint32_t)packet.size());
     extract(b);
     return b.result(0);
+}
+
+ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, const parser::ProtocolDefinition& protocol) {
+    return parseOne(packet, std::make_shared<const parser::ProtocolDefinition>(protocol));
 }
 
 ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, const std::string& protocolName) {
@@ -847,29 +859,19 @@ ParseResult GpuProtocolParser::parsePacket(const std::vector<uint8_t>& packet, c
         if (all.empty()) throw std::out_of_range("GpuProtocolParser::parsePacket: no protocol registered");
         return all[0];
     }
-    parser::ProtocolDefinition def;
-    {
-        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
-        auto it = protocols_.find(protocolName);
-        if (it == protocols_.end()) {   // :76-81: no stats update
-            ParseResult r;
-            r.status = ParseStatus::PROTOCOL_NOT_FOUND;
-            r.errorMessage = "Protocol not found: " + protocolName;
-            return r;
-        }
-        def = it->second;
+    DefPtr def = findProtocol(protocolName);
+    if (!def) {   // :76-81: no stats update
+        ParseResult r;
+        r.status = ParseStatus::PROTOCOL_NOT_FOUND;
+        r.errorMessage = "Protocol not found: " + protocolName;
+        return r;
     }
-    return parsePacket(packet, def);
+    return parseOne(packet, std::move(def));
 }
 
 std::vector<ParseResult> GpuProtocolParser::parsePacketMultipleProtocols(const std::vector<uint8_t>& packet) {
-    std::vector<parser::ProtocolDefinition> defs;
-    {
-        std::shared_lock<std::shared_mutex> lk(protocols_mu_);
-        for (const auto& kv : protocols_) defs.push_back(kv.second);   // the reference's iteration order (:117)
-    }
     std::vector<ParseResult> out;
-    for (const auto& d : defs) out.push_back(parsePacket(packet, d));
+    for (auto& d : allProtocols()) out.push_back(parseOne(packet, std::move(d)));
     return out;
 }
 

@@ -118,7 +118,10 @@ private:
 class GpuFieldBatch {
 public:
     size_t size() const { return lens_.size(); }
-    const parser::ProtocolDefinition& protocol() const { return def_; }
+    const parser::ProtocolDefinition& protocol() const {
+        static const parser::ProtocolDefinition kNone{};   // a default-constructed batch
+        return def_ ? *def_ : kNone;
+    }
     parser::ParseStatus status(size_t i) const { return static_cast<parser::ParseStatus>(status_.at(i)); }
     bool isSuccess(size_t i) const { return status_.at(i) == 0; }
     // extractValue<T> bits of field k (0 for byte-typed fields and packets that did not parse)
@@ -137,7 +140,7 @@ public:
 
 private:
     friend class GpuProtocolParser;
-    parser::ProtocolDefinition def_;
+    std::shared_ptr<const parser::ProtocolDefinition> def_;   // the registered definition, shared
     bool validate_ = true;
     uint64_t span_ = 0;
     std::vector<uint8_t> status_;
@@ -245,11 +248,18 @@ private:
     static void adopt(bt_ctx* ctx, const std::vector<Packet>& packets, Batch& b);
     void run(GpuParsedBatch& b);
     void extract(GpuFieldBatch& b);
+    using DefPtr = std::shared_ptr<const parser::ProtocolDefinition>;
+    GpuFieldBatch batchOf(const std::vector<Packet>& packets, DefPtr def);
+    parser::ParseResult parseOne(const std::vector<uint8_t>& packet, DefPtr def);
+    DefPtr findProtocol(const std::string& name) const;   // nullptr when not registered
+    std::vector<DefPtr> allProtocols() const;             // the reference's iteration order
     void countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us);
     bt_ctx* ctx_ = nullptr;
     size_t hostBelow_ = kHostBelowDefault;
     parser::ProtocolParser::ParserConfig config_;
-    std::unordered_map<std::string, parser::ProtocolDefinition> protocols_;   // as the reference's protocols_
+    // as the reference's protocols_; each definition immutable and shared, so a call takes a
+    // reference under the lock instead of copying the field table (parsePacket copied it twice)
+    std::unordered_map<std::string, DefPtr> protocols_;
     std::unordered_map<std::string, std::function<bool(const std::vector<uint8_t>&, const parser::ParseResult&)>>
         customValidators_;
     std::unordered_map<std::string, std::function<std::string(const parser::ParseResult&)>> customFormatters_;
