@@ -43,6 +43,10 @@ ap.add_argument("--host-gather", action="store_true",
 ap.add_argument("--ring-batch-blocks", type=int, default=128)
 ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="bt_opts.flags (A/B, e.g. 0x8000 no lean PCIe round A)")
 ap.add_argument("--host-threads", type=int, default=0)
+ap.add_argument("--data-node", default="none",
+                help="'auto': move the capture onto the device's NUMA node (where the context pins its "
+                     "gather threads) before timing, as a NUMA-aware capture allocates its ring; N: that node; "
+                     "'none': where the generator's threads first touched it (the default)")
 ap.add_argument("--group", type=int, default=0,
                 help="drive a bt_group of N members (devices 0..N-1; members share device 0 when fewer GPUs "
                      "are visible, labelled 'shared device'): host gather (bt_group_parse_filter) and zero-copy "
@@ -50,6 +54,37 @@ ap.add_argument("--group", type=int, default=0,
 a = ap.parse_args()
 cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4}[a.config]
 data, desc = synth.capture(cfg, a.packets)
+
+
+_held = []
+
+
+def place_on(arr, node):
+    """A copy of arr in anonymous memory bound to NUMA node `node` (mbind(2) before the first
+    touch); the original is released by the caller."""
+    import ctypes
+    import mmap
+    import numpy as np
+    if node is None or node < 0:
+        return arr
+    size = (arr.nbytes + 4095) & ~4095
+    m = mmap.mmap(-1, size)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(m))
+    mask = (ctypes.c_ulong * 2)(0, 0)
+    mask[node // 64] |= 1 << (node % 64)
+    libc = ctypes.CDLL(None, use_errno=True)
+    if libc.syscall(237, ctypes.c_void_p(addr), ctypes.c_ulong(size), 2, mask, ctypes.c_ulong(129), 0) != 0:
+        raise OSError(ctypes.get_errno(), "mbind")
+    out = np.frombuffer(m, dtype=arr.dtype, count=arr.size)
+    np.copyto(out, arr)
+    _held.append(m)
+    return out
+
+
+def data_node_for(placement):
+    if a.data_node == "none":
+        return None
+    return placement["numa_node"] if a.data_node == "auto" else int(a.data_node)
 
 
 def page_nodes(arr, samples=8):
@@ -76,6 +111,7 @@ if a.group:
     grp = abi.Group(devices, host_chunk_packets=a.chunk, host_threads=a.host_threads,
                     flags=a.flags | (abi.OPT_GROUP_SHARED_DEVICE if shared else 0))
     grp.compile(FILTERS)
+    data = place_on(data, data_node_for(grp.placement(0)))
     n = a.packets
     where = {"members": m, "devices": devices, "shared_device": shared, "usable_cpus": abi.usable_cpus(),
              "flags": a.flags,
@@ -125,10 +161,12 @@ if a.group:
     sys.exit(0)
 ctx = abi.Context(0, host_chunk_packets=a.chunk, host_threads=a.host_threads, flags=a.flags)
 ctx.compile(FILTERS)
+data = place_on(data, data_node_for(ctx.placement()))
 if a.tpacket:
     import numpy as np
     ring, rdesc, used = synth.tpv3_ring(data, desc)
     del data
+    ring = place_on(ring, data_node_for(ctx.placement()))
     bs, n = synth.TPV3_BLOCK, len(rdesc)
     B = a.ring_batch_blocks
     nbat = (used + B - 1) // B
