@@ -1,0 +1,123 @@
+"""GPU: a time-bounded randomized parity sweep over every entry form.
+
+Each round draws a capture (C2 / C3 / C4 / fuzz frames, a random seed and a packet count
+that is rarely a tile multiple), a random program over the built-in kinds (the reference's
+expression quirks, throwing expressions, disabled filters; tests/random_programs.py) and one
+entry form of the product:
+  host      bt_parse_filter: frames in host memory, the host pipeline (records sometimes)
+  ptrs      bt_parse_filter_ptrs: one pointer per frame (the std::vector<Packet> form)
+  device    bt_parse_filter_device: batch resident in device memory
+  mapped    bt_group_parse_filter_mapped over 1-3 shared-device members: frames and outputs
+            in registered host memory, read in place over PCIe (the lean first round)
+  grouphost bt_group_parse_filter over 2-3 members (split or routed)
+and checks decisions (and records when asked, and the verdict words / pass list) against the
+oracle (tests/oracle_lib.py, pinned by the compiled reference's goldens). The sweep runs for
+BT_FUZZ_SECONDS (default 15 s in the suite; a longer run is the same test with a larger
+value) and prints one line per round.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+from beatrice_amd import abi, synth
+from random_programs import random_programs
+
+pytestmark = pytest.mark.gpu
+
+FORMS = ("host", "ptrs", "device", "mapped", "grouphost")
+
+
+def _check(out, dec, n, npass, where):
+    bad = np.nonzero(out["decide"][:n] != dec)[0]
+    assert len(bad) == 0, f"{where}: {len(bad)} decisions differ, first {bad[:5]}"
+    if out.get("verdict") is not None:
+        bits = np.unpackbits(out["verdict"].view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(bits, (dec >> 6) == 0), f"{where}: verdict words"
+    if out.get("pass_idx") is not None:
+        exp = np.nonzero((dec >> 6) == 0)[0].astype(np.uint32)
+        assert out["n_pass"] == npass == len(exp) and np.array_equal(out["pass_idx"], exp), f"{where}: pass list"
+
+
+def _mapped(grp, data, desc, n, records):
+    tiles = max(1, (n + 63) // 64)
+    h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
+    h_dec = np.zeros(tiles * 64, np.uint8)
+    h_ver = np.zeros(tiles, np.uint64)
+    pidx = np.zeros(max(n, 1), np.uint32)
+    npass = np.zeros(1, np.uint32)
+    held = [a for a in (data, desc, h_rec, h_dec, h_ver) if a is not None]
+    for a in held:
+        grp.register(a)
+    try:
+        grp.run_mapped(abi.Batch(data.ctypes.data, desc.ctypes.data, 0, n, data.nbytes, abi.DESC_PACKED, 0),
+                       abi.Outputs(None if h_rec is None else h_rec.ctypes.data, n, h_ver.ctypes.data,
+                                   h_dec.ctypes.data, pidx.ctypes.data, npass.ctypes.data))
+    finally:
+        for a in held:
+            grp.unregister(a)
+    return {"decide": h_dec[:n], "verdict": h_ver, "pass_idx": pidx[:int(npass[0])], "n_pass": int(npass[0]),
+            "records": abi.untile_records(h_rec, n) if records else None}
+
+
+def test_randomized_parity_sweep():
+    seconds = float(os.environ.get("BT_FUZZ_SECONDS", "15"))
+    seed0 = int(os.environ.get("BT_FUZZ_SEED", str(int(time.time()) & 0xFFFFFF)))
+    rng = np.random.default_rng(seed0)
+    print(f"fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
+    ctx = abi.Context(0)
+    groups = {}
+    t_end = time.time() + seconds
+    rounds = 0
+    try:
+        while time.time() < t_end or rounds < len(FORMS):
+            cfg = [synth.C2, synth.C3, synth.C4, synth.FUZZ][int(rng.integers(0, 4))]
+            n = int(rng.choice([1, 63, 64, 65, 127, 4097, int(rng.integers(1, 70000))]))
+            cap_seed = int(rng.integers(1, 1 << 30))
+            data, desc = synth.capture(cfg, n, seed=cap_seed)
+            if data.nbytes < 64:   # fuzz frames of length 0: a registrable buffer all the same
+                data = np.concatenate([data, np.zeros(64, np.uint8)])
+            prog = random_programs(int(rng.integers(1, 1 << 30)), 1)[0]
+            if rng.random() < 0.2:   # the metric's own set
+                prog = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+                        {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+                        {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+            form = FORMS[rounds % len(FORMS)] if rounds < len(FORMS) else FORMS[int(rng.integers(0, len(FORMS)))]
+            records = bool(rng.random() < 0.4)
+            where = f"round {rounds} form {form} cfg {cfg} n {n} seed {cap_seed:#x} records {records} program {prog}"
+            rec, dec, npass = ol.oracle_run(data, desc, n, prog, parse=records)
+            if form in ("host", "ptrs", "device"):
+                ctx.compile(prog)
+                if form == "host":
+                    out = ctx.run_host(data, desc, records=records)
+                elif form == "ptrs":
+                    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+                    frames = [data[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)]
+                    grp = groups.setdefault(1, abi.Group([0]))
+                    grp.compile(prog)
+                    out = grp.run_ptrs(frames, records=records)
+                else:
+                    r = abi.DeviceRun(ctx, data, desc, n, records=records)
+                    r.run()
+                    out = r.fetch()
+                    r.free()
+            else:
+                m = int(rng.integers(1, 4)) if form == "mapped" else int(rng.integers(2, 4))
+                if m not in groups:
+                    groups[m] = abi.Group([0] * m, flags=abi.OPT_GROUP_SHARED_DEVICE if m > 1 else 0)
+                grp = groups[m]
+                grp.compile(prog)
+                out = _mapped(grp, data, desc, n, records) if form == "mapped" else grp.run_host(data, desc, records=records)
+            _check(out, dec, n, npass, where)
+            if records:
+                bad = np.nonzero((out["records"][:n] != rec).any(axis=1))[0]
+                assert len(bad) == 0, f"{where}: {len(bad)} records differ, first {bad[:5]}"
+            rounds += 1
+            print(f"ok round {rounds} {form} cfg {cfg} n {n} filters {len(prog)} records {records}", flush=True)
+    finally:
+        for g in groups.values():
+            g.close()
+        ctx.close()
+    assert rounds >= len(FORMS)
