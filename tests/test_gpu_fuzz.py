@@ -121,3 +121,56 @@ def test_randomized_parity_sweep():
             g.close()
         ctx.close()
     assert rounds >= len(FORMS)
+
+
+REGEX_POOL = ["GET", "[\\x00-\\x1f][a-z]", "^..?\\d", "MAG+IC", "a|b", "\\d\\d", "[^a-z]{3}", "(ab|cd)e",
+              "x*y", "^$", ".", "HTTP/1\\.[01]", "[A-Z][a-z]+", "\\x00\\x00", "^\\w", "z$"]
+
+
+@pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref (compiled reference) not built")
+def test_randomized_payload_programs_vs_reference():
+    """The same sweep with GPU PAYLOAD slots (regexes compiled to DFAs) between built-ins,
+    checked against the compiled reference's own PacketFilter (std::regex per packet), on
+    host, device-resident and zero-copy mapped batches. Runs BT_FUZZ_SECONDS / 3."""
+    from golden_util import compare_decisions
+    seconds = float(os.environ.get("BT_FUZZ_SECONDS", "15")) / 3
+    seed0 = int(os.environ.get("BT_FUZZ_SEED", str(int(time.time()) & 0xFFFFFF))) ^ 0x9A
+    rng = np.random.default_rng(seed0)
+    print(f"payload fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
+    ctx = abi.Context(0)
+    grp = abi.Group([0, 0], flags=abi.OPT_GROUP_SHARED_DEVICE)
+    t_end = time.time() + seconds
+    rounds = 0
+    try:
+        while time.time() < t_end or rounds < 3:
+            cfg = [synth.C3, synth.C4, synth.FUZZ][int(rng.integers(0, 3))]
+            n = int(rng.integers(1, 3000))
+            data, desc = synth.capture(cfg, n, seed=int(rng.integers(1, 1 << 30)))
+            if data.nbytes < 64:
+                data = np.concatenate([data, np.zeros(64, np.uint8)])
+            prog = random_programs(int(rng.integers(1, 1 << 30)), 1)[0]
+            for k in range(int(rng.integers(1, 3))):
+                prog.insert(int(rng.integers(0, len(prog) + 1)),
+                            {"type": abi.PAYLOAD, "expr": REGEX_POOL[int(rng.integers(0, len(REGEX_POOL)))],
+                             "priority": 40 + k})
+            form = ("host", "device", "mapped")[rounds % 3]
+            where = f"payload round {rounds} form {form} cfg {cfg} n {n} program {prog}"
+            if form == "mapped":
+                grp.compile(prog)
+                out = _mapped(grp, data, desc, n, False)
+            else:
+                ctx.compile(prog)
+                if form == "host":
+                    out = ctx.run_host(data, desc, records=False)
+                else:
+                    r = abi.DeviceRun(ctx, data, desc, n, records=False)
+                    r.run()
+                    out = r.fetch()
+                    r.free()
+            code, src = ol.ref_filter(data, desc, n, prog)
+            compare_decisions(out["decide"][:n], code, src, prog, where=where)
+            rounds += 1
+            print(f"ok payload round {rounds} {form} cfg {cfg} n {n} filters {len(prog)}", flush=True)
+    finally:
+        grp.close()
+        ctx.close()
