@@ -21,6 +21,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -848,11 +849,112 @@ static void on_fatal(int sig) {
     _exit(128 + sig);
 }
 
+// A randomized round for `test_adapter fuzz`: one program on one capture through a fresh
+// GpuPacketFilter (members contexts on device 0, a 4,096-packet staging chunk so batches span
+// chunks) against the reference PacketFilter: the vector form (results, exception kind), the
+// single-packet form on the first packets, classify's pass list, and the stats.
+static bool fuzz_case(const char* label, const Capture& cap, const std::vector<Spec>& specs, int members) {
+    PacketFilter ref;
+    bt_opts o{};
+    o.flags = members > 1 ? BT_OPT_GROUP_SHARED_DEVICE : 0u;
+    o.host_chunk_packets = 4096;
+    GpuPacketFilter gpu(std::vector<int>(members, 0), &o);
+    install(ref, specs);
+    install(gpu, specs);
+    std::vector<PacketFilter::FilterResult> a, b;
+    std::exception_ptr ea, eb;
+    try { a = ref.applyFilters(cap.packets); } catch (...) { ea = std::current_exception(); }
+    try { b = gpu.applyFilters(cap.packets); } catch (...) { eb = std::current_exception(); }
+    CHECK((bool)ea == (bool)eb, "%s: exception mismatch ref=%d gpu=%d", label, (bool)ea, (bool)eb);
+    if (ea) {
+        CHECK(what_kind(ea) == what_kind(eb), "%s: %s vs %s", label, what_kind(ea).c_str(), what_kind(eb).c_str());
+    } else {
+        for (size_t i = 0; i < a.size(); ++i)
+            CHECK(a[i].passed == b[i].passed && a[i].filterName == b[i].filterName && a[i].reason == b[i].reason,
+                  "%s: packet %zu ref=(%d,%s) gpu=(%d,%s)", label, i, a[i].passed, a[i].filterName.c_str(), b[i].passed,
+                  b[i].filterName.c_str());
+        std::vector<uint32_t> want;
+        for (size_t i = 0; i < a.size(); ++i)
+            if (a[i].passed) want.push_back((uint32_t)i);
+        const GpuPacketFilter::Verdicts v = gpu.classify(cap.packets);
+        CHECK(v.pass_idx == want, "%s: classify pass list (%zu vs %zu)", label, v.pass_idx.size(), want.size());
+        ref.applyFilters(cap.packets);   // the reference's stats count classify's packets too
+    }
+    for (size_t i = 0; i < std::min<size_t>(cap.packets.size(), 300); ++i) {
+        PacketFilter::FilterResult x, y;
+        std::exception_ptr ex, ey;
+        try { x = ref.applyFilters(cap.packets[i]); } catch (...) { ex = std::current_exception(); }
+        try { y = gpu.applyFilters(cap.packets[i]); } catch (...) { ey = std::current_exception(); }
+        CHECK((bool)ex == (bool)ey && (!ex || what_kind(ex) == what_kind(ey)) &&
+                  (ex || (x.passed == y.passed && x.filterName == y.filterName && x.reason == y.reason)),
+              "%s: single packet %zu", label, i);
+    }
+    if (!ea) {
+        const auto sa = ref.getStats(), sb = gpu.getStats();
+        CHECK(sa.packetsProcessed == sb.packetsProcessed && sa.packetsPassed == sb.packetsPassed &&
+                  sa.packetsDropped == sb.packetsDropped && sa.filterCounts == sb.filterCounts,
+              "%s: stats differ (processed %lu/%lu passed %lu/%lu)", label, (unsigned long)sa.packetsProcessed,
+              (unsigned long)sb.packetsProcessed, (unsigned long)sa.packetsPassed, (unsigned long)sb.packetsPassed);
+    }
+    return true;
+}
+
+static int fuzz_main(double seconds, uint64_t seed) {
+    using T = PacketFilter::FilterType;
+    std::mt19937_64 rng(seed);
+    auto pick = [&](size_t n) { return (size_t)(rng() % n); };
+    const std::vector<std::pair<T, std::vector<std::string>>> pools = {
+        {T::BPF, {"", "tcp", "udp", "icmp", "not udp", "UDP", "tcp or udp", "ip", "xyz"}},
+        {T::PROTOCOL, {"tcp", "udp", "icmp", "ip", "UDP", "", "foo"}},
+        {T::IP_RANGE, {"10.0.0.0/8", "192.168.0.0/16", "0.0.0.0/0", "10.1.2.3", "10.0.0.0/33", "10.0.0.0/-1",
+                       "266.0.0.0/8", "10.0.0", " 10.0.0.0/8", "abc", "10.0.0.0/x"}},
+        {T::PORT_RANGE, {"1000-2000", "53", "0-65535", "2000-1000", "66770", "-5", "80-80", "abc", "1000-", "0-1023"}},
+        {T::PAYLOAD, {"GET", "[\\x00-\\x1f][a-z]", "^..?\\d", "a|b", "\\d\\d", "(ab|cd)e", "x*y", ".", "[A-Z][a-z]+"}},
+        {T::CUSTOM, {""}}};
+    const char* names[] = {"a", "zeta", "m7", "q", "beta", "k2", "proto", "net", "ports", "x1", "hi", "c"};
+    std::printf("fuzz seed %#llx, %.0f s\n", (unsigned long long)seed, seconds);
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(seconds);
+    int rounds = 0;
+    while (std::chrono::steady_clock::now() < t_end || rounds < 4) {
+        const int cfg = (int[]){3, 4, 9}[pick(3)];
+        const uint32_t n = (uint32_t[]){1, 2047, 2048, 2049, 4097, (uint32_t)(1 + pick(6000))}[pick(6)];
+        const Capture cap = capture(cfg, n, rng());
+        std::vector<Spec> specs;
+        const size_t m = 1 + pick(6);
+        std::vector<size_t> used;
+        for (size_t k = 0; k < m; ++k) {
+            size_t ni = pick(12);
+            while (std::find(used.begin(), used.end(), ni) != used.end()) ni = (ni + 1) % 12;
+            used.push_back(ni);
+            const auto& pool = pools[pick(pools.size())];
+            Spec sp{names[ni], pool.first, pool.second[pick(pool.second.size())], (int)pick(6), pick(10) != 0, 0};
+            if (sp.type == T::CUSTOM) sp.custom = 1 + (int)pick(3);
+            specs.push_back(sp);
+        }
+        const int members = 1 + (int)pick(2);
+        char label[96];
+        std::snprintf(label, sizeof(label), "fuzz#%d cfg%d n%u m%zu g%d", rounds, cfg, n, m, members);
+        if (!fuzz_case(label, cap, specs, members)) {
+            for (const auto& sp : specs)
+                std::printf("  spec %s type %d expr '%s' prio %d enabled %d custom %d\n", sp.name.c_str(), (int)sp.type,
+                            sp.expr.c_str(), sp.priority, sp.enabled, sp.custom);
+            break;
+        }
+        ++rounds;
+        if (rounds % 25 == 0) std::printf("ok   fuzz %d rounds\n", rounds);
+    }
+    std::printf("%s: %d rounds (%d failures)\n", g_fail ? "FAILED" : "ALL OK", rounds, g_fail);
+    return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
     std::setvbuf(stdout, nullptr, _IOLBF, 0);
     signal(SIGSEGV, on_fatal);
     signal(SIGABRT, on_fatal);
     using T = PacketFilter::FilterType;
+    if (argc > 1 && std::string(argv[1]) == "fuzz")   // test_adapter fuzz [seconds] [seed]
+        return fuzz_main(argc > 2 ? std::atof(argv[2]) : 10.0,
+                         argc > 3 ? std::strtoull(argv[3], nullptr, 0) : (uint64_t)std::random_device{}());
     if (argc > 2 && std::string(argv[1]) == "small") {   // test_adapter small <capture.bin> <label>
         const Capture cap = load_capture(argv[2]);
         const char* label = argc > 3 ? argv[3] : argv[2];

@@ -77,3 +77,16 @@ def test_small_calls_host_and_device_branches(cap, tmp_path):
     r = subprocess.run([BIN, "small", str(path), cap], capture_output=True, text=True, timeout=600, cwd=ROOT)
     print(r.stdout[-4000:])
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_adapter_randomized_against_reference():
+    """`test_adapter fuzz`: random programs over every filter type (PAYLOAD regexes, CUSTOM
+    callbacks that throw, the reference's expression quirks, ties, disabled filters) on random
+    captures whose sizes straddle the host / device threshold and the staging chunk, through
+    one- and two-lane filters: the vector form, single packets, classify and the stats equal
+    the compiled reference PacketFilter's. BT_FUZZ_SECONDS long (default 10 s here)."""
+    secs = os.environ.get("BT_FUZZ_SECONDS", "10")
+    r = subprocess.run([BIN, "fuzz", secs], capture_output=True, text=True, timeout=float(secs) + 300, cwd=ROOT)
+    print(r.stdout[-2000:])
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
