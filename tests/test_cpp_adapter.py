@@ -87,6 +87,8 @@ def test_adapter_randomized_against_reference():
     one- and two-lane filters: the vector form, single packets, classify and the stats equal
     the compiled reference PacketFilter's. BT_FUZZ_SECONDS long (default 10 s here)."""
     secs = os.environ.get("BT_FUZZ_SECONDS", "10")
-    r = subprocess.run([BIN, "fuzz", secs], capture_output=True, text=True, timeout=float(secs) + 300, cwd=ROOT)
+    seed = os.environ.get("BT_FUZZ_SEED", "0xB1A5")   # fixed in the suite; "random": the binary picks
+    args = [BIN, "fuzz", secs] + ([] if seed == "random" else [seed])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=float(secs) + 300, cwd=ROOT)
     print(r.stdout[-2000:])
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]

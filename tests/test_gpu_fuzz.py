@@ -30,6 +30,13 @@ pytestmark = pytest.mark.gpu
 FORMS = ("host", "ptrs", "device", "mapped", "grouphost")
 
 
+def _seed():
+    """The sweep's seed: fixed in the suite (a failure reproduces), BT_FUZZ_SEED=random for a
+    fresh one, or a given number."""
+    e = os.environ.get("BT_FUZZ_SEED", "0xB1A5")
+    return int(time.time()) & 0xFFFFFF if e == "random" else int(e, 0)
+
+
 def _check(out, dec, n, npass, where):
     bad = np.nonzero(out["decide"][:n] != dec)[0]
     assert len(bad) == 0, f"{where}: {len(bad)} decisions differ, first {bad[:5]}"
@@ -64,7 +71,7 @@ def _mapped(grp, data, desc, n, records):
 
 def test_randomized_parity_sweep():
     seconds = float(os.environ.get("BT_FUZZ_SECONDS", "15"))
-    seed0 = int(os.environ.get("BT_FUZZ_SEED", str(int(time.time()) & 0xFFFFFF)))
+    seed0 = _seed()
     rng = np.random.default_rng(seed0)
     print(f"fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
     ctx = abi.Context(0)
@@ -134,7 +141,7 @@ def test_randomized_payload_programs_vs_reference():
     host, device-resident and zero-copy mapped batches. Runs BT_FUZZ_SECONDS / 3."""
     from golden_util import compare_decisions
     seconds = float(os.environ.get("BT_FUZZ_SECONDS", "15")) / 3
-    seed0 = int(os.environ.get("BT_FUZZ_SEED", str(int(time.time()) & 0xFFFFFF))) ^ 0x9A
+    seed0 = _seed() ^ 0x9A
     rng = np.random.default_rng(seed0)
     print(f"payload fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
     ctx = abi.Context(0)
