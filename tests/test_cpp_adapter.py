@@ -89,6 +89,12 @@ def test_adapter_randomized_against_reference():
     secs = os.environ.get("BT_FUZZ_SECONDS", "10")
     seed = os.environ.get("BT_FUZZ_SEED", "0xB1A5")   # fixed in the suite; "random": the binary picks
     args = [BIN, "fuzz", secs] + ([] if seed == "random" else [seed])
-    r = subprocess.run(args, capture_output=True, text=True, timeout=float(secs) + 300, cwd=ROOT)
-    print(r.stdout[-2000:])
-    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+    # lines are passed on as they come (a long run keeps writing its progress)
+    p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=ROOT)
+    lines = []
+    for line in p.stdout:
+        print(line, end="", flush=True)
+        lines.append(line)
+    rc = p.wait(timeout=float(secs) + 300)
+    out = "".join(lines[-60:])
+    assert rc == 0 and "ALL OK" in out, out
