@@ -934,6 +934,9 @@ static int fuzz_main(double seconds, uint64_t seed) {
         const int members = 1 + (int)pick(2);
         char label[96];
         std::snprintf(label, sizeof(label), "fuzz#%d cfg%d n%u m%zu g%d", rounds, cfg, n, m, members);
+        // every 4th round with a capture of up to 1,500 packets: the parser's batch, layers,
+        // formatters and detector on it against the reference's ProtocolParser
+        if (rounds % 4 == 0 && n <= 1500 && !parser_case(label, cap)) break;
         if (!fuzz_case(label, cap, specs, members)) {
             for (const auto& sp : specs)
                 std::printf("  spec %s type %d expr '%s' prio %d enabled %d custom %d\n", sp.name.c_str(), (int)sp.type,
