@@ -19,6 +19,8 @@
 #   kernel-ab      device-resident A/B of beatrice_amd/ab/prev against the tree's library (§6)
 #   route-ab       group tests, then concurrent callers routed whole / always split (§7)
 #   single         single-packet and small-batch surfaces (§6)
+#   pool-ab        the context's host pool at 8 (default) / 16 threads: host-gather e2e with the
+#                  capture on the device's node, the plugin, one-caller classify (§6)
 #   data-node-ab   host gather / zero-copy with the capture where its generator left it or moved
 #                  onto the device's NUMA node (e2e.py --data-node auto) (§6)
 set -o pipefail
@@ -120,6 +122,13 @@ PY
     timeout -k 10 400 tools/surfaces/surface_bench single --seconds 1.5 > "$OUT/surf_single.jsonl" 2> "$OUT/surf_single.err" \
       || { tail "$OUT/surf_single.err"; exit 1; }
     cat "$OUT/surf_single.jsonl" ;;
+  pool-ab)
+    for cfg in c2 c3 c4; do
+      bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- python tools/e2e.py --config $cfg --reps 3 --data-node auto || exit 1
+    done
+    bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- tools/surfaces/surface_bench plugin --seconds 2 --threads 16 || exit 1
+    bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- tools/surfaces/surface_bench filter --seconds 2 || exit 1
+    summ_ab "$OUT/ab.jsonl" ;;
   data-node-ab)
     for cfg in c2 c3 c4; do
       bash tools/ab_cmd.sh "$OUT" 2 "asis||" "local||--data-node auto" -- python tools/e2e.py --config $cfg --reps 3 || exit 1
