@@ -371,7 +371,7 @@ int bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested
     if (!members || !per_member) return bt::set_error(BT_E_INVALID_ARGUMENT, "zero members / null out");
     usable = std::max(usable, 1u);
     if (requested) *per_member = std::min(std::max(requested / members, 1u), 16u);
-    else *per_member = std::min(std::max(usable / members, 1u), 8u);
+    else *per_member = std::min(std::max(usable / members, 1u), 16u);
     return BT_OK;
 }
 

@@ -51,9 +51,13 @@ public:
         for (auto& t : th_) t.join();
     }
     unsigned size() const { return nthreads_; }
-    // runs fn(k) for every k in [0, size()) and waits
-    void run(const std::function<void(unsigned)>& fn) {
-        if (nthreads_ == 1) { fn(0); return; }
+    // runs fn(k) for every k in [0, count) and waits; count 0 (or above size()) = size().
+    // With count < size() the run's indices are fewer than its threads: the workers that find
+    // none left go back to sleep (the context's host pipeline runs a smaller share of the pool
+    // while other callers wait for it, bt_runtime.cpp pipeline_share)
+    void run(const std::function<void(unsigned)>& fn, unsigned count = 0) {
+        const unsigned want = count && count < nthreads_ ? count : nthreads_;
+        if (want == 1) { fn(0); return; }
         std::lock_guard<std::mutex> one_at_a_time(run_mu_);   // callers on several threads
         uint32_t g;
         {
@@ -61,9 +65,17 @@ public:
             fn_ = &fn;
             g = (uint32_t)++gen_;
             finished_ = 0;
+            count_ = fixed_ ? nthreads_ : want;
             claim_.store((uint64_t)g << 32, std::memory_order_release);
         }
-        cv_.notify_all();
+        // wake as many workers as the run has indices beyond the caller's (a worker that is not
+        // asleep yet sees the new generation in its wait predicate; one left asleep joins a
+        // later run): a share of the pool does not wake the rest of it for nothing
+        if (fixed_ || want == nthreads_) {
+            cv_.notify_all();
+        } else {
+            for (unsigned k = 1; k < want; ++k) cv_.notify_one();
+        }
         if (fixed_) {
             fn(0);
             std::lock_guard<std::mutex> lk(m_);
@@ -72,7 +84,7 @@ public:
             execute(g, fn);
         }
         std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [this] { return finished_ == nthreads_; });
+        done_.wait(lk, [this] { return finished_ == count_; });
         fn_ = nullptr;
     }
 
@@ -83,12 +95,12 @@ private:
         for (;;) {
             uint64_t c = claim_.load(std::memory_order_acquire);
             for (;;) {
-                if ((uint32_t)(c >> 32) != g || (uint32_t)c >= nthreads_) return;
+                if ((uint32_t)(c >> 32) != g || (uint32_t)c >= count_.load(std::memory_order_relaxed)) return;
                 if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) break;
             }
             fn((unsigned)(uint32_t)c);
             std::lock_guard<std::mutex> lk(m_);
-            if (++finished_ == nthreads_) done_.notify_one();
+            if (++finished_ == count_) done_.notify_one();
         }
     }
     void loop(unsigned id) {
@@ -120,6 +132,7 @@ private:
     const std::function<void(unsigned)>* fn_ = nullptr;
     std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
     unsigned finished_ = 0, nthreads_ = 1;
+    std::atomic<unsigned> count_{1};   // indices of the current run (set under m_ before its claims open)
     bool fixed_ = false;
     cpu_set_t pin_{};
     uint64_t gen_ = 0;

@@ -125,6 +125,7 @@ struct bt_ctx {
     HostSlot hs[2];
     bool host_ready = false;
     std::unique_ptr<HostPool> pool;   // created on first use (pool_of)
+    std::atomic<int> waiters{0};      // callers waiting for `mu` to run a host batch (pipeline_share)
     std::once_flag pool_once;
     // placement (place_ctx): the host NUMA node closest to the device and the CPUs of it this
     // process may use; the pool's workers run there when `pinned`
@@ -279,19 +280,19 @@ void place_ctx(bt_ctx* c) {
     c->pinned = !off && node_cpus(c->numa_node, &c->pin);
 }
 
-// The pool's size: opts.host_threads, else BT_HOST_THREADS, else 8 (at most the usable
-// CPUs); at most 16. A group sets each member's opts.host_threads from its budget (bt_group.cpp).
+// The pool's size: opts.host_threads, else BT_HOST_THREADS, else the usable CPUs; at most 16.
+// A group sets each member's opts.host_threads from its budget (bt_group.cpp). Round 3 capped
+// the default at 8: with callers on all 16 of a GPU box's CPUs (T callers of one
+// GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool oversubscribed them
+// (profiles/r03/surfaces/ab_pool_threads.jsonl). Now a chunk's gather takes at most 8 of the
+// pool while other callers wait (pipeline_share), and a lone caller all of it.
 unsigned pool_threads_of(const bt_ctx* c) {
     unsigned nt = c->opts.host_threads;
     if (!nt) {
-        // 8, not every usable CPU: with callers on all 16 of a GPU box's CPUs (T callers of
-        // one GpuPacketFilter, the plugin's onPacket threads) a 16-thread pool
-        // oversubscribes them: C2 applyFilters 136-142 against 163 Mpps, classify 161-163
-        // against 172-192 (tools/ab_cmd.sh, profiles/r03/surfaces/ab_pool_threads.jsonl)
         const char* e = getenv("BT_HOST_THREADS");
-        nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(8u, usable_cpus());
+        nt = e && atoi(e) > 0 ? (unsigned)atoi(e) : usable_cpus();
     }
-    return std::min(nt, 16u);
+    return std::max(1u, std::min(nt, 16u));
 }
 
 HostPool& pool_of(bt_ctx* c) {
@@ -592,18 +593,40 @@ int ensure_host(bt_ctx* c) {
 // The host pipeline's parallel steps for a chunk of `cnt` packets: on the pool, or for small
 // chunks on the calling thread (every w in turn), where waking the pool cost more than the
 // work (a 1k-packet classify took ~0.1 ms per call).
+// fn(w) for w in [0, T), T = pipeline_share(c).
 template <class Fn>
-void pipeline_run(bt_ctx* c, uint32_t cnt, Fn&& fn) {
+void pipeline_run(bt_ctx* c, uint32_t cnt, unsigned T, Fn&& fn) {
     static const uint32_t below = [] {
         const char* e = getenv("BT_HOST_INLINE_BELOW");   // A/B knob, 0 = always the pool
         return e ? (uint32_t)strtoul(e, nullptr, 10) : 8192u;
     }();
     if (cnt < below) {
-        for (unsigned w = 0, T = c->pool->size(); w < T; ++w) fn(w);
+        for (unsigned w = 0; w < T; ++w) fn(w);
     } else {
-        c->pool->run(fn);
+        c->pool->run(fn, T);
     }
 }
+
+// How much of the pool one chunk's gather / drain uses: all of it, or, while other callers
+// wait for this context, at most kSharedPool threads. A lone caller then gets every pool thread
+// (host-gather e2e with 16 of a 16-CPU host's: C4 349-408 -> 515-535 Mpps), while callers on
+// every CPU (T callers of one GpuPacketFilter) keep to the share that does not oversubscribe
+// them (16 callers lost 10-25 % with a 16-thread pool, profiles/r04/surfaces/ab_pool_8_16.jsonl).
+constexpr unsigned kSharedPool = 8;
+unsigned pipeline_share(const bt_ctx* c) {
+    const unsigned T = c->pool->size();
+    return c->waiters.load(std::memory_order_relaxed) > 0 ? std::min(T, kSharedPool) : T;
+}
+
+// Counts the caller as waiting for the context until it holds the context's lock.
+struct WaitFor {
+    std::unique_lock<std::mutex> lk;
+    explicit WaitFor(bt_ctx* c) : lk(c->mu, std::defer_lock) {
+        c->waiters.fetch_add(1, std::memory_order_relaxed);
+        lk.lock();
+        c->waiters.fetch_sub(1, std::memory_order_relaxed);
+    }
+};
 
 // One frame's staged prefix: m bytes of src to dst (16-B aligned, its slot rounded up to 16).
 // With `nt`, whole 16-B chunks go out as non-temporal stores (no read-for-ownership of the
@@ -635,13 +658,13 @@ void drain_slot(bt_ctx* c, HostSlot& s, bt_rec* records, uint64_t* verdict, uint
     const uint8_t* rec = s.h_out;
     const uint8_t* dec = s.h_out + (size_t)chunk * BT_REC_BYTES;
     const uint64_t* ver = reinterpret_cast<const uint64_t*>(dec + chunk);
-    const unsigned T = c->pool->size();
+    const unsigned T = pipeline_share(c);
     const uint32_t lo = s.lo, cnt = s.cnt;
     static const bool drain_nt = [] {   // A/B knob: BT_DRAIN_NT=1 streams the records out
         const char* e = getenv("BT_DRAIN_NT");
         return e && atoi(e) != 0;
     }();
-    pipeline_run(c, cnt, [&](unsigned w) {   // split on 64-packet boundaries
+    pipeline_run(c, cnt, T, [&](unsigned w) {   // split on 64-packet boundaries
         const uint32_t tiles = (cnt + 63) / 64;
         const uint32_t t0 = (uint32_t)((uint64_t)tiles * w / T), t1 = (uint32_t)((uint64_t)tiles * (w + 1) / T);
         const uint32_t a = t0 * 64, b = std::min(cnt, t1 * 64);
@@ -1135,10 +1158,10 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
             // per-worker byte counts, exclusive scan, then parallel copies
             uint8_t* pre = s.h_in;
             uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlotPayload);
-            const unsigned T = c->pool->size();
+            const unsigned T = pipeline_share(c);
             std::vector<uint64_t> part(T + 1, 0);
             const uint32_t base_i = next;
-            pipeline_run(c, cnt, [&](unsigned w) {
+            pipeline_run(c, cnt, T, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t sum = 0;
                 for (uint32_t i = a; i < b; ++i) {
@@ -1149,7 +1172,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 part[w + 1] = sum;
             });
             for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
-            pipeline_run(c, cnt, [&](unsigned w) {
+            pipeline_run(c, cnt, T, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t p = part[w];
                 for (uint32_t i = a; i < b; ++i) {
@@ -1240,7 +1263,7 @@ int bt_parse_filter(bt_ctx* c, const uint8_t* base, const bt_pkt_desc* desc, uin
                     uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (n && (!base || !desc)) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
-    std::lock_guard<std::mutex> lk(c->mu);
+    const WaitFor lk(c);
     return host_pipeline(
         c, n,
         [&](uint32_t i, uint32_t* len) {
@@ -1256,7 +1279,7 @@ int bt_parse_filter_ptrs(bt_ctx* c, const uint8_t* const* frames, const uint32_t
     if (n && (!frames || !lens)) return fail(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
     for (uint32_t i = 0; i < n; ++i)
         if (lens[i] > 0xFFFFu) return fail(BT_E_INVALID_ARGUMENT, "frame %u longer than 65535 bytes", i);
-    std::lock_guard<std::mutex> lk(c->mu);
+    const WaitFor lk(c);
     return host_pipeline(
         c, n,
         [&](uint32_t i, uint32_t* len) {

@@ -157,8 +157,13 @@ public:
             pack_ = env_int("BEATRICE_GPU_PACK", 0) != 0;
             // the plugin reads the device list: BEATRICE_GPU_DEVICES=0,1,... (a group), else
             // BEATRICE_GPU_DEVICE (one device, default 0)
-            filter_ = std::make_shared<GpuPacketFilter>(
-                GpuPacketFilter::devicesFromEnv(env_int("BEATRICE_GPU_DEVICE", 0)));
+            const std::vector<int> devs = GpuPacketFilter::devicesFromEnv(env_int("BEATRICE_GPU_DEVICE", 0));
+            // one device: its host pool at 8 threads, not every usable CPU, since the onPacket
+            // producers share the host (16 producers lost 5-15 % with a 16-thread pool,
+            // profiles/r04/surfaces/ab_pool_8_16.jsonl); BT_HOST_THREADS overrides
+            bt_opts o{};
+            if (devs.size() == 1 && !std::getenv("BT_HOST_THREADS")) o.host_threads = std::min(8u, std::max(1u, bt_usable_cpus()));
+            filter_ = std::make_shared<GpuPacketFilter>(devs, &o);
             if (const char* spec = std::getenv("BEATRICE_GPU_FILTERS")) configure(spec);
             whole_ = filter_->needsPackets();
             stage_ = stageWidth(*filter_);

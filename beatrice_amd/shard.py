@@ -43,11 +43,12 @@ def group_cost(mapped: bool, records: bool, filters: bool, desc_bytes: int = 8, 
 
 def member_threads(members: int, usable: int, requested: int = 0) -> int:
     """bt_group_thread_budget: host threads per group member. `requested` is the whole
-    group's budget (split evenly, 1..16 each); auto gives usable / members, 1..8 each."""
+    group's budget (split evenly, 1..16 each); auto gives usable / members, 1..16 each (a
+    member's host pipeline takes at most 8 of them while other callers wait for it)."""
     usable = max(usable, 1)
     if requested:
         return min(max(requested // members, 1), 16)
-    return min(max(usable // members, 1), 8)
+    return min(max(usable // members, 1), 16)
 
 
 def shard_bounds(lengths: np.ndarray, world: int, by_bytes: bool = True, cost=DEFAULT_COST):

@@ -279,8 +279,9 @@ typedef struct bt_opts {
     uint32_t host_chunk_bytes;     /* pinned staging bytes per chunk (0 = default 256 MiB) */
     uint32_t grid_waves;           /* 0 = auto (persistent grid sized to the device)    */
     uint32_t flags;                /* BT_OPT_*                                          */
-    uint32_t host_threads;         /* host-path threads (0 = auto: BT_HOST_THREADS, else 8,
-                                      at most the usable CPUs (affinity, cgroup quota)); <= 16 */
+    uint32_t host_threads;         /* host-path threads (0 = auto: BT_HOST_THREADS, else the
+                                      usable CPUs (affinity, cgroup quota)); <= 16; a host
+                                      batch uses <= 8 of them while others wait for the context */
     uint32_t reserved[3];
 } bt_opts;
 
@@ -574,8 +575,9 @@ int      bt_group_cost(bt_group* group, int mapped, int records, int filters, ui
                        bt_split_cost* out);
 /* Host threads per member: `requested` (opts.host_threads, else BT_HOST_THREADS; 0 = auto)
  * is the whole group's budget, split evenly (at least 1, at most 16 each); auto gives each
- * member usable / members, at least 1 and at most 8 (one context alone: min(8, usable), the
- * single-context default). Host only; bt_group_create applies it. */
+ * member usable / members, at least 1 and at most 16 (one context alone: min(16, usable), the
+ * single-context default; a context's host pipeline takes at most 8 of them while other callers
+ * wait for the context). Host only; bt_group_create applies it. */
 int      bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member);
 /* bt_host_parallel over the whole group's host threads: fn(user, w, workers) runs once for
  * every w in [0, workers), workers = the members' pool sizes summed (member k's pool, on its

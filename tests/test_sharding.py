@@ -135,9 +135,10 @@ def test_thread_budget_matches_mirror():
                 got = abi.group_thread_budget(members, usable, requested)
                 assert got == shard.member_threads(members, usable, requested)
                 assert 1 <= got <= 16
-    assert shard.member_threads(1, 16) == 8        # one context: the single-context default
+    assert shard.member_threads(1, 16) == 16       # one context: the single-context default
+    assert shard.member_threads(2, 16) == 8
     assert shard.member_threads(8, 16) == 2        # 8 GPUs on a 16-CPU job: 16 threads in all
-    assert shard.member_threads(8, 128) == 8
+    assert shard.member_threads(8, 128) == 16
     with pytest.raises(abi.BtError):
         abi.group_thread_budget(0, 16, 0)
 

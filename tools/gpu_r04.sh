@@ -19,8 +19,9 @@
 #   kernel-ab      device-resident A/B of beatrice_amd/ab/prev against the tree's library (§6)
 #   route-ab       group tests, then concurrent callers routed whole / always split (§7)
 #   single         single-packet and small-batch surfaces (§6)
-#   pool-ab        the context's host pool at 8 (default) / 16 threads: host-gather e2e with the
-#                  capture on the device's node, the plugin, one-caller classify (§6)
+#   pool-ab        the context's host pool at 8 (BT_HOST_THREADS=8, round 3's default) / the
+#                  default (the usable CPUs, a share of 8 while other callers wait): host-gather e2e
+#                  with the capture on the device's node, the plugin, one- and 16-caller classify (§6)
 #   data-node-ab   host gather / zero-copy with the capture where its generator left it or moved
 #                  onto the device's NUMA node (e2e.py --data-node auto) (§6)
 set -o pipefail
@@ -124,10 +125,10 @@ PY
     cat "$OUT/surf_single.jsonl" ;;
   pool-ab)
     for cfg in c2 c3 c4; do
-      bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- python tools/e2e.py --config $cfg --reps 3 --data-node auto || exit 1
+      bash tools/ab_cmd.sh "$OUT" 2 "p8|BT_HOST_THREADS=8|" "auto||" -- python tools/e2e.py --config $cfg --reps 3 --data-node auto || exit 1
     done
-    bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- tools/surfaces/surface_bench plugin --seconds 2 --threads 16 || exit 1
-    bash tools/ab_cmd.sh "$OUT" 2 "p8||" "p16|BT_HOST_THREADS=16|" -- tools/surfaces/surface_bench filter --seconds 2 || exit 1
+    bash tools/ab_cmd.sh "$OUT" 2 "p8|BT_HOST_THREADS=8|" "auto||" -- tools/surfaces/surface_bench plugin --seconds 2 --threads 16 || exit 1
+    bash tools/ab_cmd.sh "$OUT" 2 "p8|BT_HOST_THREADS=8|" "auto||" -- tools/surfaces/surface_bench filter --seconds 2 || exit 1
     summ_ab "$OUT/ab.jsonl" ;;
   data-node-ab)
     for cfg in c2 c3 c4; do
