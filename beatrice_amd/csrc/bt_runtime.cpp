@@ -126,6 +126,8 @@ struct bt_ctx {
     bool host_ready = false;
     std::unique_ptr<HostPool> pool;   // created on first use (pool_of)
     std::atomic<int> waiters{0};      // callers waiting for `mu` to run a host batch (pipeline_share)
+    uint64_t last_call = 0;           // under mu: the last host batch's thread tag and end (WaitFor)
+    bool shared_call = false;         // under mu: another thread used the context just before
     std::once_flag pool_once;
     // placement (place_ctx): the host NUMA node closest to the device and the CPUs of it this
     // process may use; the pool's workers run there when `pinned`
@@ -615,17 +617,32 @@ void pipeline_run(bt_ctx* c, uint32_t cnt, unsigned T, Fn&& fn) {
 constexpr unsigned kSharedPool = 8;
 unsigned pipeline_share(const bt_ctx* c) {
     const unsigned T = c->pool->size();
-    return c->waiters.load(std::memory_order_relaxed) > 0 ? std::min(T, kSharedPool) : T;
+    const bool shared = c->waiters.load(std::memory_order_relaxed) > 0 || c->shared_call;
+    return shared ? std::min(T, kSharedPool) : T;
 }
 
-// Counts the caller as waiting for the context until it holds the context's lock.
+// Counts the caller as waiting for the context until it holds the context's lock, and marks
+// the call shared when another thread held the context within the last kSharedWindowUs: callers
+// that spend time outside the context between their calls (building FilterResults) are not
+// waiting for it at the moment a chunk starts, but they are on the host's CPUs all the same.
+constexpr uint64_t kSharedWindowUs = 2000;
 struct WaitFor {
     std::unique_lock<std::mutex> lk;
-    explicit WaitFor(bt_ctx* c) : lk(c->mu, std::defer_lock) {
+    bt_ctx* c;
+    uint64_t me;
+    static uint64_t now_us() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    explicit WaitFor(bt_ctx* ctx) : lk(ctx->mu, std::defer_lock), c(ctx) {
         c->waiters.fetch_add(1, std::memory_order_relaxed);
         lk.lock();
         c->waiters.fetch_sub(1, std::memory_order_relaxed);
+        me = (uint64_t)std::hash<std::thread::id>{}(std::this_thread::get_id()) & 0xFFFFull;
+        const uint64_t last = c->last_call;   // (thread tag << 48) | end time in us, under mu
+        c->shared_call = last && (last >> 48) != me && now_us() - (last & 0xFFFFFFFFFFFFull) < kSharedWindowUs;
     }
+    ~WaitFor() { c->last_call = (me << 48) | (now_us() & 0xFFFFFFFFFFFFull); }
 };
 
 // One frame's staged prefix: m bytes of src to dst (16-B aligned, its slot rounded up to 16).
