@@ -515,8 +515,12 @@ void bench_group(const Capture& c, int threads, double seconds, const std::vecto
                     std::vector<Packet> part;
                     uint64_t mine = 0;
                     for (size_t at = 0; !stop.load(std::memory_order_relaxed); at = (at + chunk) % shard.size()) {
-                        part.assign(shard.begin() + at, shard.begin() + std::min(shard.size(), at + chunk));
-                        mine += f.classify(part).decide.size();
+                        if (chunk >= shard.size()) {   // one call over the whole shard: no copy of it per call
+                            mine += f.classify(shard).decide.size();
+                        } else {
+                            part.assign(shard.begin() + at, shard.begin() + std::min(shard.size(), at + chunk));
+                            mine += f.classify(part).decide.size();
+                        }
                         if (t == 0 && secs(t0, Clock::now()) > seconds) stop = true;
                     }
                     done += mine;
