@@ -78,10 +78,6 @@ struct bt_group {
     std::unique_ptr<std::atomic<uint32_t>[]> busy;   // per member: call parts running on it
     std::atomic<uint32_t> rr{0};
     uint32_t route_below = 0;
-    // every member on one device (lanes) and BT_GROUP_LANE_WHOLE=1: every host batch runs whole
-    // on the least busy lane, and each lane's pool has one device's budget (an experiment:
-    // a split over lanes adds no link or device)
-    bool lane_whole = false;
 };
 
 namespace {
@@ -208,7 +204,7 @@ int group_batch(bt_group* g, uint32_t n, LenAt len, Frames frames, bt_rec* recor
     const uint32_t m = (uint32_t)g->members.size();
     const uint32_t others = g->calls.load(std::memory_order_acquire);
     Hold in_flight(g->calls);
-    if (m > 1 && (g->lane_whole || (others > 0 && n <= g->route_below))) {   // concurrent callers: whole calls, spread
+    if (m > 1 && others > 0 && n <= g->route_below) {   // concurrent callers: whole calls, spread
         const uint32_t start = g->rr.fetch_add(1, std::memory_order_relaxed) % m;
         uint32_t k = start, least = UINT32_MAX;
         for (uint32_t j = 0; j < m; ++j) {
@@ -406,13 +402,8 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         const char* e = getenv("BT_HOST_THREADS");
         if (e && atoi(e) > 0) requested = (uint32_t)atoi(e);
     }
-    bool one_device = n_devices > 1;
-    for (uint32_t i = 1; i < n_devices; ++i) one_device = one_device && devices[i] == devices[0];
-    const char* lw = getenv("BT_GROUP_LANE_WHOLE");
-    const bool lane_whole = one_device && lw && atoi(lw) != 0;
-    (void)bt_group_thread_budget(lane_whole ? 1 : n_devices, bt::usable_cpus(), requested, &mo.host_threads);
+    (void)bt_group_thread_budget(n_devices, bt::usable_cpus(), requested, &mo.host_threads);
     auto* g = new bt_group();
-    g->lane_whole = lane_whole;
     for (uint32_t i = 0; i < n_devices; ++i) {
         bt_ctx* c = nullptr;
         const int rc = bt_create(devices[i], &mo, &c);
