@@ -3,7 +3,7 @@
 // integrator calls").
 //
 //   surface_bench [all|filter|ref|mt|parser|sizes|single|group|plugin|plugin-hot] [--packets N] [--seconds S] [--threads T]
-//                 [--plugin SO] [--chunks 16384,65536] [--members 1,2,4]
+//                 [--plugin SO] [--chunks 16384,65536] [--members 1,2,4] [--data-node none|auto|N]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
 // (the reference's batch type, include/beatrice/Packet.hpp) and C3's 5-tuple filter set:
@@ -27,6 +27,10 @@
 //   plugin    libgpu_parse_filter_plugin.so through createPlugin(): onPacket from 1 and from
 //             T threads (PluginManager::processPacket's per-packet call), until the verdict
 //             sink has seen every packet.
+// --data-node auto (or a node number) sets this process's memory policy to prefer the NUMA node
+// nearest device 0 (bt_context_placement) before the captures are built, so the frames, the
+// Packets and their control blocks sit where the host gather's pinned threads run
+// (tools/e2e.py --data-node does the same for its buffers); default none: first touch.
 // One JSON object per line. The parity of every surface is tests/cpp/test_adapter.cpp's
 // and test_plugin.cpp's job; this tool only times them.
 #include <dlfcn.h>
@@ -53,6 +57,8 @@
 #include "beatrice_gpu_plugin.h"
 
 #include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
 extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
@@ -648,11 +654,17 @@ int main(int argc, char** argv) {
     const char* so = "beatrice_amd/libgpu_parse_filter_plugin.so";
     std::vector<size_t> chunks = {16384, 65536};
     std::vector<int> members = {1, 2, 4};
+    std::string data_node = "none";
+    int node = -1;
     for (int i = 2; i + 1 < argc; i += 2) {
         if (!std::strcmp(argv[i], "--packets")) n2 = n3 = (uint32_t)std::atol(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--seconds")) seconds = std::atof(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--threads")) threads = std::atoi(argv[i + 1]);
         else if (!std::strcmp(argv[i], "--plugin")) so = argv[i + 1];
+        else if (!std::strcmp(argv[i], "--data-node")) {
+            data_node = argv[i + 1];
+            if (data_node != "auto" && data_node != "none") node = std::atoi(argv[i + 1]);
+        }
         else if (!std::strcmp(argv[i], "--members")) {   // comma-separated group sizes of "group"
             members.clear();
             for (const char* q = argv[i + 1]; *q;) {
@@ -670,7 +682,17 @@ int main(int argc, char** argv) {
             }
         }
     }
-    std::fprintf(stderr, "surface_bench: %d usable CPUs\n", threads);
+    if (data_node == "auto") {
+        bt_ctx* ctx = nullptr;
+        bt_placement pl{};
+        node = bt_create(0, nullptr, &ctx) == BT_OK && bt_context_placement(ctx, &pl) == BT_OK ? pl.numa_node : -1;
+        bt_destroy(ctx);
+    }
+    if (node >= 0 && node < 64) {   // MPOL_PREFERRED: allocations go to `node` while it has room
+        const unsigned long mask = 1ul << node;
+        if (syscall(SYS_set_mempolicy, 1, &mask, 64) != 0) node = -1;
+    }
+    std::fprintf(stderr, "surface_bench: %d usable CPUs, data node %d\n", threads, node);
     const Capture caps[2] = {capture("c2", 2, n2, 0xC2), capture("c3", 3, n3, 0xC3)};
     for (const Capture& c : caps) {
         if (what == "all" || what == "filter" || what == "ref") {
