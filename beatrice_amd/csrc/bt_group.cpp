@@ -34,6 +34,7 @@
 #include <thread>
 #include <vector>
 
+#include "bt_device.h"
 #include "bt_host.h"
 #include "bt_host_pool.h"
 
@@ -78,6 +79,10 @@ struct bt_group {
     std::unique_ptr<std::atomic<uint32_t>[]> busy;   // per member: call parts running on it
     std::atomic<uint32_t> rr{0};
     uint32_t route_below = 0;
+    // the host batches' staged window per frame without / with records (bt_host_stage_bytes of
+    // the installed program), cached when a program is installed so that a split reads it
+    // without taking member 0's context lock (which a host batch in flight holds)
+    std::atomic<uint32_t> stage_window[2] = {{0u}, {0u}};
 };
 
 namespace {
@@ -430,6 +435,7 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         g->route_below = rb ? (uint32_t)strtoul(rb, nullptr, 10) : (1u << 20);
         g->busy = std::make_unique<std::atomic<uint32_t>[]>(n_devices);
         for (uint32_t i = 0; i < n_devices; ++i) g->busy[i].store(0, std::memory_order_relaxed);
+        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::stage_bytes_of(g->members[0], r != 0));
     }
     if (n_devices > 1) {
         std::vector<const cpu_set_t*> pins;
@@ -470,7 +476,9 @@ int bt_group_filter_compile(bt_group* g, const bt_filter_desc* filters, uint32_t
         std::unique_lock<std::shared_mutex> lk(g->prog_mu);
         bt::CompiledProgram p;   // compiled once, installed on every device
         if (int rc = bt::compile_program(filters, n, bt::ctx_flags(g->members[0]), &p)) return rc;
-        return run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
+        const int rc = run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
+        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::stage_bytes_of(g->members[0], r != 0));
+        return rc;
     } catch (const std::exception& e) {
         return bt::set_error(BT_E_INTERNAL, "bt_group_filter_compile: %s", e.what());
     }
@@ -481,10 +489,14 @@ int bt_group_cost(bt_group* g, int mapped, int records, int filters, uint32_t de
     *out = bt_split_cost{};
     out->align = 16;
     if (mapped) {
-        out->window = records ? 128u : 48u;
+        // filter-only: the lean first round reads frame bytes [kLeanLo, kLeanPcie) = [12, 38),
+        // 26 B in two or three 16-B chunks by the frame's alignment: 32 + one chunk of slack
+        constexpr uint32_t kLeanWindow = (bt::kLeanPcie - bt::kLeanLo + 15u) / 16u * 16u + 16u;
+        static_assert(kLeanWindow == 48u, "bt_group_cost's documented lean window");
+        out->window = records ? 128u : kLeanWindow;
         out->fixed = desc_bytes + (records ? 64u : 0u) + (filters ? 1u : 0u);
     } else {
-        out->window = bt::stage_bytes_of(g->members[0], records != 0);
+        out->window = g->stage_window[records != 0].load(std::memory_order_relaxed);
         out->fixed = desc_bytes + (records ? (uint32_t)BT_REC_BYTES : 0u) + (filters ? 1u : 0u);
     }
     return BT_OK;
@@ -584,6 +596,11 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
     if (!b->desc && b->stride == 0 && n) return bt::set_error(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
     if (b->desc_format > BT_DESC_XDP) return bt::set_error(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
     if (b->desc && !b->bytes) return bt::set_error(BT_E_INVALID_ARGUMENT, "descriptor batch with bytes == 0");
+    // fixed stride: the members' ranges are carved out of [base, base + n * stride), so a
+    // smaller stated size is refused here, as a single context refuses it (run_device)
+    if (!b->desc && b->bytes && b->bytes < (uint64_t)n * b->stride)
+        return bt::set_error(BT_E_INVALID_ARGUMENT, "fixed-stride batch: bytes %llu < n * stride %llu",
+                             (unsigned long long)b->bytes, (unsigned long long)n * b->stride);
     if (o->records && o->n_cap < n) return bt::set_error(BT_E_INVALID_ARGUMENT, "records n_cap %u < n %u", o->n_cap, n);
     const bool filter = o->verdict || o->decide || o->pass_idx || o->n_pass;
     const bool want_pass = o->pass_idx || o->n_pass;

@@ -30,7 +30,7 @@ public:
     // pin (optional): the CPUs the workers run on, e.g. those of the device's NUMA node
     // (bt_runtime.cpp place_ctx); the caller, worker 0, stays where it is
     explicit HostPool(unsigned n, const cpu_set_t* pin = nullptr) {
-        nthreads_ = n ? n : 1;
+        nthreads_ = n ? (n < 0xFFFFu ? n : 0xFFFFu) : 1;   // indices fit the claim word's 16 bits
         static const bool fixed = getenv("BT_POOL_FIXED") != nullptr;   // A/B: each worker its own index
         fixed_ = fixed;
         if (pin) pin_ = *pin;
@@ -66,7 +66,10 @@ public:
             g = (uint32_t)++gen_;
             finished_ = 0;
             count_ = fixed_ ? nthreads_ : want;
-            claim_.store((uint64_t)g << 32, std::memory_order_release);
+            fixed_want_ = want;   // fixed mode: workers with id >= want finish without running fn
+            // the run's index count travels in the claim word itself: a worker still holding the
+            // previous run's generation must never pair it with this run's (larger) count
+            claim_.store(((uint64_t)g << 32) | ((uint64_t)want << 16), std::memory_order_release);
         }
         // wake as many workers as the run has indices beyond the caller's (a worker that is not
         // asleep yet sees the new generation in its wait predicate; one left asleep joins a
@@ -89,16 +92,20 @@ public:
     }
 
 private:
-    // claims indices of run g (the generation in the counter's high half keeps a late
-    // worker from claiming in a later run with an earlier run's function) and runs them
+    // claims indices of run g and runs them. The claim word is generation << 32 | count << 16 |
+    // next index: the generation keeps a late worker from claiming in a later run with an
+    // earlier run's function, and reading the count from the same word keeps it from claiming
+    // index `count` of its own run while the next run is being set up (with the count in a
+    // separate variable, a worker that read the old claim word and the next run's larger count
+    // ran one index past its run, on a function object that may already be the next run's)
     void execute(uint32_t g, const std::function<void(unsigned)>& fn) {
         for (;;) {
             uint64_t c = claim_.load(std::memory_order_acquire);
             for (;;) {
-                if ((uint32_t)(c >> 32) != g || (uint32_t)c >= count_.load(std::memory_order_relaxed)) return;
+                if ((uint32_t)(c >> 32) != g || (c & 0xFFFFu) >= ((c >> 16) & 0xFFFFu)) return;
                 if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) break;
             }
-            fn((unsigned)(uint32_t)c);
+            fn((unsigned)(c & 0xFFFFu));
             std::lock_guard<std::mutex> lk(m_);
             if (++finished_ == count_) done_.notify_one();
         }
@@ -108,6 +115,7 @@ private:
         for (;;) {
             const std::function<void(unsigned)>* f;
             uint32_t g;
+            unsigned want;
             {
                 std::unique_lock<std::mutex> lk(m_);
                 cv_.wait(lk, [&] { return gen_ != seen; });
@@ -115,10 +123,11 @@ private:
                 if (stop_) return;
                 f = fn_;   // null when that run has already finished
                 g = (uint32_t)gen_;
+                want = fixed_want_;
             }
             if (!f) continue;
             if (fixed_) {   // round 2's pool: worker id runs index id, the caller waits for all
-                (*f)(id);
+                if (id < want) (*f)(id);   // a run of fewer indices than threads: the rest only check in
                 std::lock_guard<std::mutex> lk(m_);
                 if (++finished_ == nthreads_) done_.notify_one();
             } else {
@@ -130,8 +139,9 @@ private:
     std::mutex m_, run_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)>* fn_ = nullptr;
-    std::atomic<uint64_t> claim_{0};   // (generation << 32) | next index
+    std::atomic<uint64_t> claim_{0};   // (generation << 32) | (count << 16) | next index
     unsigned finished_ = 0, nthreads_ = 1;
+    unsigned fixed_want_ = 1;   // fixed mode: the current run's index count (under m_)
     std::atomic<unsigned> count_{1};   // indices of the current run (set under m_ before its claims open)
     bool fixed_ = false;
     cpu_set_t pin_{};

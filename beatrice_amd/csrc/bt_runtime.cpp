@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "beatrice_gpu_bench.h"
 #include "bt_device.h"
 #include "bt_host_pool.h"
 #include "bt_host.h"
@@ -126,7 +127,8 @@ struct bt_ctx {
     bool host_ready = false;
     std::unique_ptr<HostPool> pool;   // created on first use (pool_of)
     std::atomic<int> waiters{0};      // callers waiting for `mu` to run a host batch (pipeline_share)
-    uint64_t last_call = 0;           // under mu: the last host batch's thread tag and end (WaitFor)
+    uint64_t last_caller = 0;         // under mu: the last host batch's thread tag (WaitFor::thread_tag)
+    uint64_t last_end = 0;            // ... and its end time in us
     bool shared_call = false;         // under mu: another thread used the context just before
     std::once_flag pool_once;
     // placement (place_ctx): the host NUMA node closest to the device and the CPUs of it this
@@ -638,11 +640,21 @@ struct WaitFor {
         c->waiters.fetch_add(1, std::memory_order_relaxed);
         lk.lock();
         c->waiters.fetch_sub(1, std::memory_order_relaxed);
-        me = (uint64_t)std::hash<std::thread::id>{}(std::this_thread::get_id()) & 0xFFFFull;
-        const uint64_t last = c->last_call;   // (thread tag << 48) | end time in us, under mu
-        c->shared_call = last && (last >> 48) != me && now_us() - (last & 0xFFFFFFFFFFFFull) < kSharedWindowUs;
+        me = thread_tag();
+        const uint64_t now = now_us();
+        c->shared_call = c->last_end && c->last_caller != me && now - c->last_end < kSharedWindowUs;
     }
-    ~WaitFor() { c->last_call = (me << 48) | (now_us() & 0xFFFFFFFFFFFFull); }
+    ~WaitFor() {
+        c->last_caller = me;
+        c->last_end = now_us();
+    }
+    // a process-unique number per thread (a hash of std::thread::id cut to 16 bits let two
+    // threads collide and look like one lone caller)
+    static uint64_t thread_tag() {
+        static std::atomic<uint64_t> next{1};
+        thread_local const uint64_t tag = next.fetch_add(1, std::memory_order_relaxed);
+        return tag;
+    }
 };
 
 // One frame's staged prefix: m bytes of src to dst (16-B aligned, its slot rounded up to 16).

@@ -2,6 +2,8 @@
 // src/PacketFilter.cpp:<line> (Open-Sentra/beatrice).
 #include "GpuPacketFilter.hpp"
 
+#include "bt_slot_eval.h"
+
 #include <algorithm>
 #include <sys/mman.h>
 
@@ -21,33 +23,13 @@ namespace {
 const std::string kPassedReason = "Packet passed all filters";   // src/PacketFilter.cpp:102-105
 
 uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-uint32_t be32(const uint8_t* p) { return (be16(p) << 16) | be16(p + 2); }
 
-// The device's eval_slot (bt_kernels.hip) for one packet: used only to continue a
-// packet whose chain the device handed to the host at a PAYLOAD/CUSTOM slot.
-// 1 pass, 0 reject, 2 throw.
+// A built-in slot on one packet: the kernels' own FilterIn / eval_slot (bt_slot_eval.h).
+// 1 pass, 0 reject, 2 throw (PAYLOAD / HOST slots are the callers' before they get here).
 int eval_builtin(const bt_filter_slot& s, const uint8_t* d, size_t len) {
-    const bool gate = len >= 34 && be16(d + 12) == 0x0800;
-    const uint32_t proto = gate ? d[23] : 0;
-    const bool l4ok = gate && ((proto == 6 && len >= 54) || (proto == 17 && len >= 42));
-    switch (s.kind) {
-    case BT_K_TRUE: return 1;
-    case BT_K_FALSE: return 0;
-    case BT_K_BPF:
-        return gate && (((s.a & 1) && proto == 6) || ((s.a & 2) && proto == 17) || ((s.a & 4) && proto == 1));
-    case BT_K_PROTO_EQ: return gate && proto == s.a;
-    case BT_K_PROTO_NZ: return gate && proto != 0;
-    case BT_K_IP_MASK:
-        return gate && (((be32(d + 26) & s.b) == s.a) || ((be32(d + 30) & s.b) == s.a));
-    case BT_K_PORT: {
-        if (!l4ok) return 0;
-        const uint32_t sp = be16(d + 34), dp = be16(d + 36);
-        return (sp >= s.a && sp <= s.b) || (dp >= s.a && dp <= s.b);
-    }
-    case BT_K_IP_THROW: return gate ? 2 : 0;
-    case BT_K_PORT_THROW: return l4ok ? 2 : 0;
-    default: return 1;
-    }
+    const uint32_t l = len > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)len;
+    const bt::FilterIn x = bt::filter_in([d](uint32_t i) { return (uint32_t)d[i]; }, l);
+    return (int)bt::eval_slot(s.kind, s.a, s.b, x);
 }
 
 // applyPayloadFilter (src/PacketFilter.cpp:288-321) for a non-empty, valid regex.

@@ -304,6 +304,24 @@ def load_traffic(path, key, n):
     return rec, os.path.relpath(path, ROOT)
 
 
+def aggregate_roofline(ranks: list, world: int) -> dict:
+    """The job's roofline over its N devices: the algorithmic bytes of every
+    rank's main-kernel launch summed, over the slowest rank's kernel time, against N x the HBM
+    peak ("frac"); and the same bytes over the slowest rank's whole step (compaction and
+    launch gaps included, "frac_step"). At N = 1 it equals the line's own roofline."""
+    algo = float(sum(r["algo"] for r in ranks))
+    kms = max(r["main_ms"] for r in ranks)
+    step = max(r["step_s"] for r in ranks)
+    peak = HBM_PEAK_GBS * world
+    ach = algo / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    ach_step = algo / step / 1e9 if step > 0 else 0.0
+    return {"bound": "hbm", "devices": world, "unit": "GB/s", "peak": peak,
+            "algorithmic_bytes": int(algo), "kernel_ms_max": round(kms, 4),
+            "achieved": round(ach, 1), "frac": round(ach / peak, 4),
+            "ms_per_step_max": round(step * 1e3, 4), "achieved_step": round(ach_step, 1),
+            "frac_step": round(ach_step / peak, 4)}
+
+
 def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     """GPU half of one workload: build, warm up, time K steps. Returns this rank's
     results (the CPU baseline and the cross-rank max are filled in by the caller)."""
@@ -422,7 +440,8 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     timing["kernel_pass"]["ms_per_step"] = round(tk.span_ms / args.steps, 4)
     out = {"workload": wl["name"], "value": round(value, 2), "unit": "Mpps", "ms_per_step": round(step_max * 1e3, 4),
            "scaling": "strong" if strong else "weak", "packets_per_gpu": n, "packets_total": n_job,
-           "pass_fraction": round(n_pass / n, 4) if filt and n else None, "roofline": roof, "timing": timing}
+           "pass_fraction": round(n_pass / n, 4) if filt and n else None, "roofline": roof,
+           "roofline_aggregate": aggregate_roofline(ranks, world), "timing": timing}
     if world > 1:
         out["per_rank"] = [{"rank": i, "packets": r["n"], "ms_per_step": round(r["step_s"] * 1e3, 4),
                             "kernel_ms": round(r["main_ms"], 4),
@@ -558,8 +577,13 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
     (bt_group_host_register + bt_group_parse_filter_mapped), C3's 5-tuple filter, decisions and
     verdict words written back into registered host memory. PCIe-inclusive, strong scaling (one
     batch split n_dev ways), never the line's `value`. Rank 0 runs it after every rank's
-    device-resident timing, the other ranks waiting at a barrier."""
+    device-resident timing, the other ranks waiting at a barrier.
+
+    The capture is placed the way INTEGRATION.md §4 tells a deployment to allocate its ring or
+    UMEM: each member's byte range of the batch on its device's NUMA node (the nodes the
+    members' gather threads are pinned to), reported in `placement` / `data_nodes`."""
     import time as _time
+    from beatrice_amd import numa
     visible = abi.device_count()
     if visible < n_dev:
         return {"skipped": f"rank 0 sees {visible} device(s), the job has {n_dev}"}
@@ -569,11 +593,18 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
                        "C3's 5-tuple filter, decisions + verdict words back into host memory",
            "n_devices": n_dev, "packets": packets, "scaling": "strong", "pcie_inclusive": True, "unit": "Mpps"}
     for name, cfg in (("c2", synth.C2), ("c3", synth.C3)):
-        data, desc = synth.capture(cfg, packets)
+        raw, desc = synth.capture(cfg, packets)
         grp = abi.Group(devs)
         held = []
         try:
             grp.compile(C3_FILTERS)
+            # each member's range of frames on its device's node (the mapped call's split)
+            bounds = abi.group_split(synth.desc_len(desc), n_dev, grp.cost(True, False, True), plan=True)
+            nodes = [grp.placement(k)["numa_node"] for k in range(n_dev)]
+            spans = numa.member_byte_ranges(synth.desc_off(desc), synth.desc_len(desc), bounds)
+            data = numa.place_ranges(raw, [(lo, hi, nd) for (lo, hi), nd in zip(spans, nodes)])
+            del raw
+            data_nodes = [numa.page_nodes(data[lo:hi]) if hi > lo else [] for lo, hi in spans]
             tiles = (packets + 63) // 64
             dec = np.zeros(tiles * 64, np.uint8)
             ver = np.zeros(tiles, np.uint64)
@@ -594,7 +625,8 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
             out[name] = {"value": round(packets / med / 1e6, 1), "best": round(packets / min(times) / 1e6, 1),
                          "ms_per_call": round(med * 1e3, 3), "pass_fraction": round(float(bits.mean()), 4),
                          "verdicts_match_decisions": consistent,
-                         "placement": [grp.placement(k) for k in range(n_dev)]}
+                         "placement": [grp.placement(k) for k in range(n_dev)],
+                         "data_nodes": data_nodes, "member_nodes": nodes}
             if name == "c3":   # the same frames through the members' host gathers (bt_group_parse_filter)
                 grp.run_host(data, desc, records=False)
                 ht = []
@@ -721,8 +753,6 @@ def main():
               flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        args.no_cpu = True   # the CPU baseline is a rank-0, N=1 figure: an N > 1 line carries none
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -763,22 +793,15 @@ def main():
             res, sample = measure(name, wl, args, ctx, flags, dist, rank, world, strong)
         results[key] = res
         samples[key] = (sample, wl)
+    # the reference CPU parser + filter on rank 0, after every rank's GPU timing; at N > 1 the
+    # other ranks wait at the barrier below meanwhile (north_star: "timed on the node's own host
+    # cores ... in the same run", at every GPU count)
     cpus = host_cpus()
     if rank == 0 and not args.no_cpu:
-        for key, (sample, wl) in samples.items():
-            if sample is not None and wl.get("extract"):
-                results[key]["cpu_baseline"] = cpu_baseline_extract(sample, wl, args.cpu_seconds, cpus)
-            elif sample is not None and not (key != "__head__" and results[key]["scaling"] == "strong"):
-                results[key]["cpu_baseline"] = cpu_baseline(sample, wl, args.cpu_seconds, cpus)
-                if key == "__head__" and cpus["affinity_cpus"] > cpus["threads"]:
-                    # the same on one thread per affinity CPU, past the cgroup quota: shows
-                    # whether the quota, not the thread count, bounds the reference
-                    wide = cpu_baseline(sample, wl, max(1.0, args.cpu_seconds / 2),
-                                        dict(cpus, threads=cpus["affinity_cpus"]))
-                    results[key]["cpu_baseline"]["all_affinity_threads"] = {
-                        "threads": wide["cores"], "value": wide["value"], "unit": wide["unit"]}
-            else:
-                results[key]["cpu_baseline"] = None
+        attach_cpu_baselines(results, samples, cpus, world,
+                             lambda smp, wl, sec, c: (cpu_baseline_extract if wl.get("extract") else cpu_baseline)(
+                                 smp, wl, sec, c),
+                             args.cpu_seconds)
 
     # the product's multi-GPU ingest (one process, every device of the job), after every rank's
     # device-resident timing: the other ranks wait at a barrier meanwhile
@@ -793,34 +816,71 @@ def main():
         dist.barrier()
 
     if rank == 0:
-        h = results.pop("__head__")
-        line = {
-            "metric": METRIC,
-            "value": h["value"],
-            "unit": "Mpps",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": h["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": h["scaling"],
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64, streamed to HBM)",
-            "config": {"workload": h["workload"], "packets_per_gpu": h["packets_per_gpu"],
-                       "packets_total": h["packets_total"], "parallelism": f"batch split x{world}",
-                       "pass_fraction": h.get("pass_fraction"), **devices},
-            "roofline": h["roofline"],
-            "cpu_baseline": h.get("cpu_baseline"),
-            "timing": h["timing"],
-        }
-        if "per_rank" in h:
-            line["per_rank"] = h["per_rank"]
-        line["configs"] = results
-        print(json.dumps(line), flush=True)
+        print(json.dumps(build_line(results, args, world, devices)), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def attach_cpu_baselines(results: dict, samples: dict, cpus: dict, world: int, timer, seconds: float) -> None:
+    """Rank 0's CPU baselines, one per workload entry: timer(sample, wl, seconds, cpus) runs the
+    reference (oracle/_ref) on the host CPUs. A strong-scaling entry whose weak twin was timed
+    on the same capture (rank 0's weak sample is the strong batch's first packets: same seed)
+    quotes that figure; the headline also reports one thread per affinity CPU when a cgroup
+    quota caps the threads. Every baseline states the job's GPU count beside it."""
+    for key, (sample, wl) in samples.items():
+        entry = results[key]
+        if sample is None:
+            entry["cpu_baseline"] = None
+            continue
+        twin = key.replace("_strong", "")
+        if entry.get("scaling") == "strong" and key != "__head__" and \
+                (results.get(twin) or {}).get("cpu_baseline"):
+            entry["cpu_baseline"] = dict(results[twin]["cpu_baseline"], same_as=f"configs.{twin}")
+            continue
+        entry["cpu_baseline"] = timer(sample, wl, seconds, cpus)
+        if key == "__head__" and cpus["affinity_cpus"] > cpus["threads"]:
+            # the same on one thread per affinity CPU, past the cgroup quota: shows
+            # whether the quota, not the thread count, bounds the reference
+            wide = timer(sample, wl, max(1.0, seconds / 2), dict(cpus, threads=cpus["affinity_cpus"]))
+            entry["cpu_baseline"]["all_affinity_threads"] = {
+                "threads": wide["cores"], "value": wide["value"], "unit": wide["unit"]}
+    for entry in results.values():
+        if isinstance(entry.get("cpu_baseline"), dict):
+            entry["cpu_baseline"]["n_gpus_in_job"] = world
+            entry["cpu_baseline"]["timed"] = ("rank 0, after every rank's GPU timing" +
+                                              (", the other ranks waiting at a barrier" if world > 1 else ""))
+
+
+def build_line(results: dict, args, world: int, devices: dict) -> dict:
+    """Rank 0's JSON line from the per-workload entries (results["__head__"] = the headline)."""
+    results = dict(results)
+    h = results.pop("__head__")
+    line = {
+        "metric": METRIC,
+        "value": h["value"],
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": h["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": h["scaling"],
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (beatrice_amd/csrc/bt_synth.cpp, seeded mt19937_64, streamed to HBM)",
+        "config": {"workload": h["workload"], "packets_per_gpu": h["packets_per_gpu"],
+                   "packets_total": h["packets_total"], "parallelism": f"batch split x{world}",
+                   "pass_fraction": h.get("pass_fraction"), **devices},
+        "roofline": h["roofline"],
+        "roofline_aggregate": h.get("roofline_aggregate"),
+        "cpu_baseline": h.get("cpu_baseline"),
+        "timing": h["timing"],
+    }
+    if "per_rank" in h:
+        line["per_rank"] = h["per_rank"]
+    line["configs"] = results
+    return line
 
 
 if __name__ == "__main__":

@@ -569,8 +569,10 @@ int      bt_group_split_plan(const uint32_t* lens, uint32_t n, uint32_t parts, c
  *   host batches: window = bt_host_stage_bytes (48 / 112 / 176), align 16,
  *                 fixed = desc_bytes + 96 (records, bt_rec D2H) + 1 (decision D2H)
  *   mapped:       window = 128 with records (the walk's wide window) else 48 (the lean
- *                 46-B first round), align 16, fixed = desc_bytes + 64 (records: packed
- *                 slabs) + 1 (decision) — all of it PCIe traffic of the member's link. */
+ *                 first round reads frame bytes 12..37: two or three 16-B chunks by the
+ *                 frame's alignment, 32 B + one chunk of slack), align 16, fixed =
+ *                 desc_bytes + 64 (records: packed slabs) + 1 (decision) — all of it PCIe
+ *                 traffic of the member's link. */
 int      bt_group_cost(bt_group* group, int mapped, int records, int filters, uint32_t desc_bytes,
                        bt_split_cost* out);
 /* Host threads per member: `requested` (opts.host_threads, else BT_HOST_THREADS; 0 = auto)
@@ -606,67 +608,15 @@ int      bt_group_host_unregister(bt_group* group, void* host);
  * Synchronous: every output is complete on return. */
 int      bt_group_parse_filter_mapped(bt_group* group, const bt_batch* batch, const bt_outputs* out);
 
-/* ---- helpers for hosts without a HIP toolchain (ctypes / cgo / JNI) ---------- */
-int  bt_dev_malloc(bt_ctx* ctx, uint64_t bytes, void** out);
-int  bt_dev_free(bt_ctx* ctx, void* p);
-int  bt_memcpy_h2d(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
-int  bt_memcpy_d2h(bt_ctx* ctx, void* dst, const void* src, uint64_t bytes);
-int  bt_memset_d(bt_ctx* ctx, void* dst, int value, uint64_t bytes);
+/* ---- context helpers ------------------------------------------------------------ */
 /* Waits for the context's stream and its compaction stream (bt_parse_filter_device_async). */
 int  bt_synchronize(bt_ctx* ctx);
 /* Runs fn(user, w, workers) once on each of the context's host threads (w = 0 .. workers-1,
  * the caller is worker 0) and returns when all have: the pool that gathers and drains the
  * host-batch pipeline, lent to host-side post-processing of a batch. */
 int  bt_host_parallel(bt_ctx* ctx, void (*fn)(void* user, uint32_t worker, uint32_t workers), void* user);
-/* Caller-owned streams on the context's device (a hipStream_t, non-blocking) for the
- * `stream` arguments above, for hosts that cannot create one themselves. Destroying a
- * stream waits for its work. */
-int  bt_stream_create(bt_ctx* ctx, void** stream);
-int  bt_stream_synchronize(bt_ctx* ctx, void* stream);
-int  bt_stream_destroy(bt_ctx* ctx, void* stream);
-/* Timing of a device-resident run on the context stream: `iters` steps, each = the
- * main kernel between an event pair + the compaction kernels; returns the event span
- * per step and the mean main-kernel time. With BT_OPT_GRAPH the steps are captured
- * once into a hipGraph (first call per (batch, outputs, iters)) and replayed, and
- * main_ms is -1 (HIP does not time events recorded inside a graph). */
-int  bt_time_device(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out,
-                    uint32_t iters, float* ms_per_iter, float* main_kernel_ms);
-/* The same with a breakdown of where the host's wall time goes (bench.py puts it in its
- * JSON line). The host waits by polling hipEventQuery (no interrupt wake-up): the time
- * until the first event is seen complete and from there until the last one are
- * reported separately, so a late start on the GPU and a late completion notice can be
- * told apart. */
-typedef struct bt_timing {
-    float span_ms;                 /* GPU: event before the first step -> after the last */
-    float main_ms;                 /* mean main-kernel time (its own dispatch events)     */
-    float main_min_ms, main_max_ms;
-    float lead_ms;                 /* GPU: first event -> first main kernel's start       */
-    float gap_ms;                  /* GPU: sum over steps of (next main start - main end) */
-    double enqueue_ms;             /* host: all launches enqueued                         */
-    double first_seen_ms;          /* host: enqueue done -> first event seen complete     */
-    double last_seen_ms;           /* host: first event seen -> last event seen           */
-    double query_ms;               /* host: elapsed-time queries                          */
-    double wall_ms;                /* host: the whole call                                */
-    int32_t spin_rc;               /* hipSetDeviceFlags(spin) result at bt_create, -1 unset */
-    uint32_t device_flags;         /* hipGetDeviceFlags after bt_create                   */
-    uint32_t reserved[6];
-} bt_timing;
-int  bt_time_device_ex(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t iters,
-                       bt_timing* timing);
-/* The general form. Step i writes output set out[i % n_out]. mode:
- *   BT_TIME_KERNEL_EVENTS  an event pair on every main kernel (main_ms, lead_ms, gap_ms);
- *                          recorded by the kernel's own dispatch, they cost the GPU ~9 us
- *                          per step on gfx950, so a throughput loop leaves them out and
- *                          the kernel is timed in a second call;
- *   BT_TIME_PIPELINED      the steps as bt_parse_filter_device_async (n_out = 2 keeps the
- *                          API's rule that a call's verdict buffer is not rewritten
- *                          before its compaction is done).
- * bt_time_device_ex = mode BT_TIME_KERNEL_EVENTS (| BT_TIME_PIPELINED under
- * BT_OPT_PIPELINE), n_out = 1. Without kernel events main_ms.. are -1, lead/gap 0. */
-#define BT_TIME_KERNEL_EVENTS 0x1u
-#define BT_TIME_PIPELINED     0x2u
-int  bt_time_device2(bt_ctx* ctx, const bt_batch* batch, const bt_outputs* out, uint32_t n_out,
-                     uint32_t iters, uint32_t mode, bt_timing* timing);
+/* Device memory, copies, streams and timing loops for hosts without a HIP toolchain (tests,
+ * benchmarks, ctypes): include/beatrice_gpu_bench.h. */
 
 /* ---- user-defined protocols: ProtocolParser with any ProtocolDefinition -------------
  * Replaces ProtocolParser::parsePacketInternal / extractField / extractValue<T>
@@ -728,16 +678,6 @@ int  bt_extract(bt_ctx* ctx, const uint8_t* const* frames, const uint32_t* lens,
  * bt_extract call). extractValue<T>'s bits exactly as bt_extract_tile decodes them. */
 int  bt_extract_host(const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,
                      uint32_t n_fields, uint8_t* status, uint64_t* values, uint8_t* image);
-/* bt_extract_device `iters` times on the context's stream, each launch timed by an event
- * pair from its own dispatch packet (bt_timing.main_* = the extraction kernel). For
- * benchmarks; the outputs are those of the last launch. BT_E_INVALID_ARGUMENT for an empty
- * batch or a table whose span no frame can reach (nothing would launch). */
-int  bt_time_extract_ex(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
-                        const bt_extract_out* out, uint32_t iters, bt_timing* timing);
-/* The same with a mode (BT_TIME_KERNEL_EVENTS only; without it main_ms.. are -1). */
-int  bt_time_extract2(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
-                      const bt_extract_out* out, uint32_t iters, uint32_t mode, bt_timing* timing);
-
 /* ---- text output --------------------------------------------------------------
  * The text the reference's ParseResult formatters print for every walked layer of
  * records [0, n) (reference src/parser/ParserResult.cpp:214-349; each layer is the

@@ -1,5 +1,6 @@
-"""CPU: the C-ABI library loads, exports every entry point include/beatrice_gpu.h
-declares, and refuses to run without a GPU (no CPU fallback)."""
+"""CPU: the C-ABI library loads, exports every entry point include/beatrice_gpu.h (the
+product) and include/beatrice_gpu_bench.h (tests and benchmarks) declare, keeps the two apart,
+and refuses to run without a GPU (no CPU fallback)."""
 import ctypes
 import os
 import re
@@ -12,21 +13,34 @@ from beatrice_amd import abi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BT_E_INVALID_ARGUMENT = 1   # include/beatrice_gpu.h (beatrice::ErrorCode::INVALID_ARGUMENT)
 HEADER = os.path.join(ROOT, "include", "beatrice_gpu.h")
+BENCH_HEADER = os.path.join(ROOT, "include", "beatrice_gpu_bench.h")
 
 
-def declared():
-    src = open(HEADER).read()
+def declared(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(bt_[a-z0-9_]+)\s*\(", src, flags=re.M)))
 
 
 def test_every_declared_symbol_is_exported():
-    names = declared()
+    names = declared() + declared(BENCH_HEADER)
     assert len(names) >= 19, names
     L = ctypes.CDLL(abi.LIB_PATH)
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, f"not exported: {missing}"
     assert set(abi.EXPORTS) <= set(names)
+
+
+def test_product_header_holds_no_harness_entry_points():
+    """The drop-in contract is beatrice_gpu.h alone: raw device memory, streams
+    and timing loops are the tests' and bench.py's (beatrice_gpu_bench.h)."""
+    product, harness = set(declared()), set(declared(BENCH_HEADER))
+    assert not product & harness
+    for name in ("bt_dev_malloc", "bt_memcpy_h2d", "bt_stream_create", "bt_time_device2", "bt_time_extract2"):
+        assert name in harness and name not in product
+    for name in ("bt_create", "bt_filter_compile", "bt_parse_filter", "bt_parse_filter_device",
+                 "bt_group_parse_filter_mapped", "bt_synchronize"):
+        assert name in product
 
 
 def test_abi_version_and_struct_sizes():

@@ -254,6 +254,14 @@ def test_group_mapped_fixed_stride_and_edges():
             rec, dec, _ = ol.oracle_run(buf, desc[:n], n, C3_SET)
             assert np.array_equal(out["records"], rec), n
             _check_filter(out, dec, n)
+        # a stated size below n * stride is refused before the split (a member past it would
+        # otherwise get an underflowed bound and read past the registered range)
+        buf, _ = synth.capture(synth.C2, 1000, seed=9)
+        buf = np.ascontiguousarray(buf[:1000 * 64])
+        for nbytes in (64, 999 * 64 + 63):
+            with pytest.raises(abi.BtError) as e:
+                _run_mapped(grp, buf, None, 1000, stride=64, nbytes=nbytes)
+            assert "bytes" in str(e.value) and "n * stride" in str(e.value)
     finally:
         grp.close()
 

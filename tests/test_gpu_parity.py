@@ -81,6 +81,27 @@ def test_fixed_stride_matches_oracle(gpu_ctx, stride):
     check_filter_outputs(out, n)
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 127, 128, 129, 191, 69893, 70001, 1 << 17])
+def test_fixed_stride_tile_pairs_and_tails(gpu_ctx, n):
+    """The 64-B parse+filter kernel (the headline's) stores a pair of tiles' decisions and
+    verdict words at once: every tail form — an odd tile count (a lone last tile), a pair cut
+    by n, a single tile — against the oracle, with and without the records."""
+    data, desc = synth.capture(synth.C2, n, seed=0x7A11 + n)
+    buf = np.ascontiguousarray(data[:n * 64])
+    filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+               {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+               {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+    gpu_ctx.compile(filters)
+    rec, dec, npass = ol.oracle_run(buf, None, n, filters, stride=64)
+    for records in (True, False):
+        out = run_dev(gpu_ctx, buf, None, n, stride=64, records=records)
+        if records:
+            assert np.array_equal(out["records"], rec)
+        assert np.array_equal(out["decide"], dec)
+        assert out["n_pass"] == npass
+        check_filter_outputs(out, n)
+
+
 @pytest.mark.parametrize("cfg,n", [(synth.C3, 1 << 20), (synth.C4, 1 << 20), (synth.FUZZ, 1 << 20),
                                    (synth.FUZZ, 777)])
 def test_seeded_captures_match_oracle(gpu_ctx, cfg, n):

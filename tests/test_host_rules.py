@@ -119,16 +119,3 @@ def test_gpu_scripts_parse():
     for sc in scripts:
         r = subprocess.run(["bash", "-n", sc], capture_output=True, text=True)
         assert r.returncode == 0, f"{sc}: {r.stderr}"
-
-
-def test_e2e_place_on_binds_a_copy():
-    """tools/e2e.py --data-node: place_on copies the capture into a mapping bound to a NUMA node
-    (node 0 exists everywhere) with the same bytes."""
-    import numpy as np
-    src = open(os.path.join(ROOT, "tools", "e2e.py")).read()
-    ns = {}
-    exec(src[src.index("_held = []"):src.index("def data_node_for")], ns)
-    a = np.random.default_rng(1).integers(0, 256, 300001, dtype=np.uint8)
-    b = ns["place_on"](a, 0)
-    assert b is not a and np.array_equal(a, b) and b.ctypes.data % 4096 == 0
-    assert ns["place_on"](a, None) is a and ns["place_on"](a, -1) is a

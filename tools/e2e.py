@@ -56,47 +56,13 @@ cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4}[a.config]
 data, desc = synth.capture(cfg, a.packets)
 
 
-_held = []
-
-
-def place_on(arr, node):
-    """A copy of arr in anonymous memory bound to NUMA node `node` (mbind(2) before the first
-    touch); the original is released by the caller."""
-    import ctypes
-    import mmap
-    import numpy as np
-    if node is None or node < 0:
-        return arr
-    size = (arr.nbytes + 4095) & ~4095
-    m = mmap.mmap(-1, size)
-    addr = ctypes.addressof(ctypes.c_char.from_buffer(m))
-    mask = (ctypes.c_ulong * 2)(0, 0)
-    mask[node // 64] |= 1 << (node % 64)
-    libc = ctypes.CDLL(None, use_errno=True)
-    if libc.syscall(237, ctypes.c_void_p(addr), ctypes.c_ulong(size), 2, mask, ctypes.c_ulong(129), 0) != 0:
-        raise OSError(ctypes.get_errno(), "mbind")
-    out = np.frombuffer(m, dtype=arr.dtype, count=arr.size)
-    np.copyto(out, arr)
-    _held.append(m)
-    return out
+from beatrice_amd.numa import page_nodes, place_on  # noqa: E402
 
 
 def data_node_for(placement):
     if a.data_node == "none":
         return None
     return placement["numa_node"] if a.data_node == "auto" else int(a.data_node)
-
-
-def page_nodes(arr, samples=8):
-    """NUMA nodes of a few of the array's pages (move_pages(2) query; -1 unknown)."""
-    import ctypes
-    libc = ctypes.CDLL(None, use_errno=True)
-    base, nb = arr.ctypes.data, arr.nbytes
-    pages = (ctypes.c_void_p * samples)(*[(base + nb * i // samples) & ~4095 for i in range(samples)])
-    status = (ctypes.c_int * samples)()
-    if libc.syscall(279, 0, ctypes.c_ulong(samples), pages, None, status, 0) != 0:
-        return []
-    return sorted(set(int(x) for x in status))
 
 
 FILTERS = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},

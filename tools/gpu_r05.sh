@@ -1,0 +1,59 @@
+# Round 5's GPU experiments, one case per call (run through gpurun):
+#
+#   OUT=gpurun_out/r05/x bash tools/gpu_r05.sh CASE
+#
+# Cases:
+#   c2f_split  where the headline's extra time over parse-only goes: c2 (parse only), c2f
+#              and c2f with its filter outputs dropped (--outputs), alternating processes,
+#              ROUNDS rounds; then two SQ-counter passes of c2f and c2     
+#   ab         AB_LIB (a build under beatrice_amd/ab/) against the in-tree library: first the
+#              fixed-stride / full-size parity tests on AB_LIB (AB_TESTS, a -k expression),
+#              then tools/gpu_abx.sh over AB_CFGS (default c2f), AB_REPS rounds
+# Every GPU step runs under its own timeout; the first failure ends the call.
+set -o pipefail
+OUT=${OUT:-gpurun_out/r05}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fail() { echo "step $1 failed (rc $2)"; tail -30 "$3" 2>/dev/null; exit "$2"; }
+
+sq_pass() {   # sq_pass NAME CONFIG COUNTERS...: one rocprofv3 PMC pass of a bench config
+  local name=$1 cfg=$2; shift 2
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/sq_${cfg}_$name" -o run -- \
+    python3 bench.py --config $cfg --configs none --steps 5 --warmup 2 --no-cpu > /dev/null 2> "$OUT/sq_${cfg}_$name.err" \
+    || fail "sq $cfg $name" $? "$OUT/sq_${cfg}_$name.err"
+}
+
+case $1 in
+  c2f_split)
+    for r in $(seq 1 ${ROUNDS:-3}); do
+      for v in c2 c2f c2f:records c2f:records,decide c2f:records,verdict; do
+        cfg=${v%%:*}; outs=${v#*:}
+        extra=""; [ "$outs" != "$v" ] && extra="--outputs $outs"
+        timeout -k 10 120 python3 bench.py --config $cfg --configs none --no-cpu --steps 50 --warmup 5 $extra \
+          > "$OUT/split_${r}_${v//[:,]/_}.json" 2> "$OUT/split.err" || fail "split $v" $? "$OUT/split.err"
+        python3 - "$OUT/split_${r}_${v//[:,]/_}.json" "$v" "$r" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+r = d["roofline"]
+print(f"round {sys.argv[3]} {sys.argv[2]:22s} kernel {r['kernel_ms']:.4f} ms (min {r['kernel_ms_min']:.4f}) "
+      f"step {d['ms_per_step']:.4f} frac {r['frac']}", flush=True)
+PY
+      done
+    done
+    for cfg in c2f c2; do
+      sq_pass a $cfg SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU
+      sq_pass b $cfg SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH
+      sq_pass g $cfg GRBM_GUI_ACTIVE GRBM_COUNT
+    done
+    python3 tools/sq_summary.py "$OUT" c2f c2 | tee "$OUT/sq_summary.txt" ;;
+  ab)
+    L=${AB_LIB:?AB_LIB=beatrice_amd/ab/<name>/libbeatrice_gpu.so}
+    BT_LIB_PATH=$PWD/$L timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -m gpu -x -q \
+      -p no:cacheprovider --timeout 300 --timeout-method thread -k "${AB_TESTS:-fixed_stride or full_size or tile_pairs}" \
+      > "$OUT/ab_pytest.log" 2>&1 || fail "ab pytest" $? "$OUT/ab_pytest.log"
+    tail -1 "$OUT/ab_pytest.log"
+    bash tools/gpu_abx.sh beatrice_amd/libbeatrice_gpu.so $L "${AB_CFGS:-c2f}" ${AB_REPS:-4} --steps 50 \
+      | tee "$OUT/ab.txt" || fail ab $? "$OUT/ab.txt" ;;
+  *) echo "unknown case $1"; exit 8 ;;
+esac
+echo "== done $(date +%T)"
