@@ -689,14 +689,6 @@ constexpr bool late_issue(int fixed_log2, int rec, int filter, bool prefetch) {
     return fixed_log2 >= 0 && !prefetch && rec != kRecAoS && filter == 1;
 }
 
-// Paired tiles (the late-issue kernel): a wave takes tiles 2p and 2p+1 back to back, holds
-// the even tile's decision bytes and verdict word in registers, and stores the pair's 128
-// decision bytes (one whole 128-B line, one 2-B store per lane) and 16 verdict bytes at once
-// (see the kernel).
-#ifndef BT_PAIR_TILES
-#define BT_PAIR_TILES 0
-#endif
-
 template <int FIXED_LOG2, int REC, int FILTER, bool PREFETCH>
 __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
@@ -706,7 +698,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     __shared__ __attribute__((aligned(16))) uint32_t lds_all[kWavesPerBlock * kImg + 32];   // + tail pad
     extern __shared__ uint4 dyn_lds[];   // PAYLOAD DFA pool (a.dfa_bytes), else empty
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
     uint32_t* img = lds_all + wid * kImg;
     const uint32_t* row = img + lane * kRow;
     if (FILTER == 2 && a.dfa_bytes) {   // uniform: the whole block copies the pool once
@@ -722,27 +714,17 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     // Tile order: cyclic (wave w takes w, w+W, ...) or blocked (wave w takes one
     // contiguous range, so concurrent accesses spread over the whole buffer).
     const uint32_t gw = blockIdx.x * kWavesPerBlock + wid;
-    constexpr bool LATE = late_issue(FIXED_LOG2, REC, FILTER, PREFETCH);
-    constexpr bool PAIR = LATE && BT_PAIR_TILES;
     uint32_t t, t_end, step;
     if (a.blocked) {
-        uint32_t per = (a.ntiles + total_waves - 1) / total_waves;
-        if (PAIR) per = (per + 1u) & ~1u;   // even: every range starts on a pair
+        const uint32_t per = (a.ntiles + total_waves - 1) / total_waves;
         t = gw * per;
         t_end = min(a.ntiles, t + per);
         step = 1;
     } else {
-        t = PAIR ? 2u * gw : gw;
+        t = gw;
         t_end = a.ntiles;
         step = total_waves;
     }
-    // the tile after t: grid-stride, or with pairs 2p -> 2p+1 -> 2(p + step)
-    auto next_tile = [&](uint32_t x) -> uint32_t {
-        if (!PAIR || a.blocked) return x + step;
-        return (x & 1u) ? x - 1u + 2u * step : x + 1u;
-    };
-    uint32_t held_dec = 0;     // PAIR: the even tile's decision byte (per lane)
-    uint64_t held_pass = 0;    // ... and its verdict word (wave-uniform)
     const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
     const HotProgram hot = hot_program(prog);
     bool wide = false;   // wave-uniform: previous tile mostly needed chunks 4..7
@@ -757,6 +739,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
     // whose staging loads would have to wait behind the next tile's loads, and not
     // parse-only (nothing to overlap: C2 0.321 against 0.319 ms). Its header loads are
     // always non-temporal (BT_OPT_CACHE_DEFAULT keeps the default policy for the rest).
+    constexpr bool LATE = late_issue(FIXED_LOG2, REC, FILTER, PREFETCH);
     if ((PREFETCH || LATE) && t < t_end) issue_loads<FIXED_LOG2, LATE>(a, t, lane, st, wide, need_max);
     if (LATE && FILTER && t < t_end) {
         // stand-ins for a tile's decision / verdict stores (an empty range: dropped), so
@@ -767,11 +750,10 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         const u32x2 z = {0u, 0u};
         __builtin_amdgcn_raw_buffer_store_b64(z, r, 16, 0, 0);
     }
-    for (; t < t_end; t = next_tile(t)) {
+    for (; t < t_end; t += step) {
         const uint32_t p0 = t * 64u;
         const uint32_t my = p0 + lane;
         const bool live = my < a.n;
-        const uint32_t tn = next_tile(t);
 
         // ---- 1. LOAD (this tile's windows -> LDS; next tile's loads go in flight) ----
         if (!PREFETCH && !LATE) issue_loads<FIXED_LOG2>(a, t, lane, st, wide, need_max);
@@ -848,63 +830,19 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
             }
         }
 
-        if (LATE && tn < t_end) issue_loads<FIXED_LOG2, LATE>(a, tn, lane, st, wide, need_max);
+        if (LATE && t + step < t_end) issue_loads<FIXED_LOG2, LATE>(a, t + step, lane, st, wide, need_max);
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
             uint32_t slot;
             const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            if (PAIR) {
-                // every path issues at least two stores (the loop top's counted wait): an even
-                // tile with a partner holds its outputs and issues two dropped stores; the odd
-                // tile stores the pair's 128 decision bytes as one 2-B store per lane (lane l:
-                // packets 2l, 2l+1 of the pair) and the two verdict words as one 16-B store; a
-                // pair cut by n, and an even tile with no partner, store byte by byte
-                const uint32_t dcode = (code << 6) | slot;
-                const bool odd = (t & 1u) != 0u;
-                const bool hold = !odd && t + 1u < t_end;
-                const uint32_t pe = odd ? p0 - 64u : p0;   // the pair's first packet
-                const uint32_t cnt = min(128u, a.n - pe);
-                const uint32_t tv = odd ? t - 1u : t;      // the pair's first verdict word
-                const bool v_in = BT_IN(&g_bounds_main, kSiteVerdict, tv + (odd ? 1u : 0u), a.ntiles);
-                if (hold) {
-                    held_dec = dcode;
-                    held_pass = pass;
-                    const auto r = rsrc_of(g_zero16, 0u);
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, r, 0, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, r, 16, 0, 0);
-                } else if (odd && cnt == 128u) {
-                    const uint32_t pk = held_dec | (dcode << 8);
-                    const uint32_t w0 = (uint32_t)__shfl((int)pk, (int)((2u * lane) & 63u));
-                    const uint32_t w1 = (uint32_t)__shfl((int)pk, (int)((2u * lane + 1u) & 63u));
-                    const uint32_t sh = lane < 32u ? 0u : 8u;
-                    const uint32_t v = ((w0 >> sh) & 0xFFu) | (((w1 >> sh) & 0xFFu) << 8);
-                    const auto rd = rsrc_of(a.decide ? a.decide + pe : nullptr, a.decide ? 128u : 0u);
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rd, (int)(2u * lane), 0, 0);
-                    const auto rv = rsrc_of(a.verdict ? a.verdict + tv : nullptr, a.verdict && v_in ? 16u : 0u);
-                    const u32x4 pv = {(uint32_t)held_pass, (uint32_t)(held_pass >> 32), (uint32_t)pass,
-                                      (uint32_t)(pass >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b128(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
-                } else {   // odd tile of a pair cut by n (cnt < 128), or a lone even tile
-                    const auto rd = rsrc_of(a.decide ? a.decide + pe : nullptr, a.decide ? cnt : 0u);
-                    if (odd) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)held_dec, rd, (int)lane, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)dcode, rd, (int)(lane + (odd ? 64u : 0u)), 0, 0);
-                    const auto rv = rsrc_of(a.verdict ? a.verdict + tv : nullptr,
-                                            a.verdict && v_in ? (odd ? 16u : 8u) : 0u);
-                    if (odd) {
-                        const u32x2 hv = {(uint32_t)held_pass, (uint32_t)(held_pass >> 32)};
-                        __builtin_amdgcn_raw_buffer_store_b64(hv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
-                    }
-                    const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? (odd ? 8 : 0) : (int)kOob, 0, 0);
-                }
-            } else if (LATE) {   // unconditional buffer stores: a static count behind the next loads
+            if (LATE) {   // unconditional buffer stores: a static count behind the next loads
                 const uint32_t cnt = min(64u, a.n - p0);
                 const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((code << 6) | slot), rd, (int)lane, 0, 0);
                 const bool v_in = BT_IN(&g_bounds_main, kSiteVerdict, t, a.ntiles);
                 const auto rv = rsrc_of(a.verdict ? a.verdict + t : nullptr, a.verdict && v_in ? 8u : 0u);
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 pv = {(uint32_t)pass, (uint32_t)(pass >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b64(pv, rv, lane == 0 ? 0 : (int)kOob, 0, 0);
             } else {

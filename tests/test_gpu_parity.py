@@ -81,11 +81,12 @@ def test_fixed_stride_matches_oracle(gpu_ctx, stride):
     check_filter_outputs(out, n)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 127, 128, 129, 191, 69893, 70001, 1 << 17])
-def test_fixed_stride_tile_pairs_and_tails(gpu_ctx, n):
-    """The 64-B parse+filter kernel (the headline's) stores a pair of tiles' decisions and
-    verdict words at once: every tail form — an odd tile count (a lone last tile), a pair cut
-    by n, a single tile — against the oracle, with and without the records."""
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 127, 128, 129, 191, 255, 256, 257, 69893, 70001, 70003, 1 << 17])
+def test_fixed_stride_tile_groups_and_tails(gpu_ctx, n):
+    """The 64-B parse+filter kernel (the headline's) may store a block's four tiles' decisions
+    and verdict words at once: every tail form — a tile count not a multiple of 4, a group cut
+    by n, n not a multiple of 4, a single tile — against the oracle, with and without the
+    records."""
     data, desc = synth.capture(synth.C2, n, seed=0x7A11 + n)
     buf = np.ascontiguousarray(data[:n * 64])
     filters = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},

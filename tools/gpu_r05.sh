@@ -9,6 +9,8 @@
 #   ab         AB_LIB (a build under beatrice_amd/ab/) against the in-tree library: first the
 #              fixed-stride / full-size parity tests on AB_LIB (AB_TESTS, a -k expression),
 #              then tools/gpu_abx.sh over AB_CFGS (default c2f), AB_REPS rounds
+#   abn        timing only: the in-tree library and every build named in AB_NAMES
+#              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
 # Every GPU step runs under its own timeout; the first failure ends the call.
 set -o pipefail
 OUT=${OUT:-gpurun_out/r05}
@@ -49,11 +51,23 @@ PY
   ab)
     L=${AB_LIB:?AB_LIB=beatrice_amd/ab/<name>/libbeatrice_gpu.so}
     BT_LIB_PATH=$PWD/$L timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -m gpu -x -q \
-      -p no:cacheprovider --timeout 300 --timeout-method thread -k "${AB_TESTS:-fixed_stride or full_size or tile_pairs}" \
+      -p no:cacheprovider --timeout 300 --timeout-method thread -k "${AB_TESTS:-fixed_stride or full_size or tile_groups}" \
       > "$OUT/ab_pytest.log" 2>&1 || fail "ab pytest" $? "$OUT/ab_pytest.log"
     tail -1 "$OUT/ab_pytest.log"
     bash tools/gpu_abx.sh beatrice_amd/libbeatrice_gpu.so $L "${AB_CFGS:-c2f}" ${AB_REPS:-4} --steps 50 \
       | tee "$OUT/ab.txt" || fail ab $? "$OUT/ab.txt" ;;
+  abn)
+    for r in $(seq 1 ${AB_REPS:-3}); do
+      for cfg in ${AB_CFGS:-c2f}; do
+        for v in base ${AB_NAMES:?AB_NAMES}; do
+          L=$PWD/beatrice_amd/libbeatrice_gpu.so; [ $v != base ] && L=$PWD/beatrice_amd/ab/$v/libbeatrice_gpu.so
+          BT_LIB_PATH=$L timeout -k 10 200 python bench.py --configs none --config $cfg --steps 50 --warmup 3 --no-cpu \
+            > "$OUT/abn_${cfg}_${v}_$r.json" 2> "$OUT/abn.err" || fail "abn $cfg $v" $? "$OUT/abn.err"
+          python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline']; print(sys.argv[2], sys.argv[3], sys.argv[4], 'step', d['ms_per_step'], 'kern', r['kernel_ms'], 'frac', r['frac'])" \
+            "$OUT/abn_${cfg}_${v}_$r.json" $r $cfg $v | tee -a "$OUT/abn.txt"
+        done
+      done
+    done ;;
   *) echo "unknown case $1"; exit 8 ;;
 esac
 echo "== done $(date +%T)"
