@@ -526,14 +526,11 @@ class Context:
                                 values.ctypes.data if nf else None, image.ctypes.data if span else None))
         return status[:n], values[:nf * n].reshape(nf, n), image[:n * span].reshape(n, span)
 
-    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
-        """bt_parse_filter over host buffers. Returns dict of numpy outputs."""
+    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True, outs: dict | None = None):
+        """bt_parse_filter over host buffers. Returns dict of numpy outputs. `outs` (from
+        host_outputs) reuses output arrays across calls, as a capture loop does."""
         n = len(desc)
-        rec = np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None
-        ver = np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None
-        dec = np.zeros(n, dtype=np.uint8) if filters else None
-        pidx = np.zeros(max(n, 1), dtype=np.uint32) if filters else None
-        npass = np.zeros(1, dtype=np.uint32) if filters else None
+        rec, ver, dec, pidx, npass = _host_outputs(n, records, filters, outs)
         p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
         data = np.ascontiguousarray(data)
         desc = np.ascontiguousarray(desc, dtype=np.uint64)
@@ -543,6 +540,29 @@ class Context:
             out["pass_idx"] = pidx[: int(npass[0])]
             out["n_pass"] = int(npass[0])
         return out
+
+
+def host_outputs(n: int, records=True, filters=True) -> dict:
+    """Output arrays for run_host calls of n packets, allocated and touched once (a capture
+    loop reuses its outputs; fresh arrays would fault their pages in inside every call)."""
+    o = {"records": np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None,
+         "verdict": np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None,
+         "decide": np.zeros(n, dtype=np.uint8) if filters else None,
+         "pass_idx": np.zeros(max(n, 1), dtype=np.uint32) if filters else None,
+         "n_pass": np.zeros(1, dtype=np.uint32) if filters else None}
+    for a in o.values():
+        if a is not None:
+            a.fill(0)   # first touch now, outside any timed call
+    return o
+
+
+def _host_outputs(n, records, filters, outs):
+    if outs is None:
+        outs = host_outputs(n, records, filters)
+    else:
+        assert (outs["records"] is not None) == bool(records) and (outs["decide"] is not None) == bool(filters)
+        assert outs["decide"] is None or len(outs["decide"]) == n
+    return outs["records"], outs["verdict"], outs["decide"], outs["pass_idx"], outs["n_pass"]
 
 
 def group_split(lens: np.ndarray, parts: int, cost=None, plan=False) -> list[tuple[int, int]]:
@@ -637,11 +657,11 @@ class Group:
         arr = filter_descs(filters)
         _check(lib().bt_group_filter_compile(self.h, arr, len(filters)))
 
-    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True):
+    def run_host(self, data: np.ndarray, desc: np.ndarray, records=True, filters=True, outs: dict | None = None):
         """bt_group_parse_filter over host buffers (the same outputs as Context.run_host)."""
         return self._run(lambda *o: lib().bt_group_parse_filter(self.h, data.ctypes.data, desc.ctypes.data,
                                                                 len(desc), *o),
-                         len(desc), records, filters, keep=(np.ascontiguousarray(data),))
+                         len(desc), records, filters, keep=(np.ascontiguousarray(data),), outs=outs)
 
     def run_ptrs(self, frames, records=True, filters=True):
         """bt_group_parse_filter_ptrs over a list of frames (the std::vector<Packet> form)."""
@@ -651,12 +671,8 @@ class Group:
         return self._run(lambda *o: lib().bt_group_parse_filter_ptrs(self.h, ptrs, lens.ctypes.data, len(frames), *o),
                          len(frames), records, filters, keep=(bufs, lens))
 
-    def _run(self, call, n, records, filters, keep=()):
-        rec = np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None
-        ver = np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None
-        dec = np.zeros(n, dtype=np.uint8) if filters else None
-        pidx = np.zeros(max(n, 1), dtype=np.uint32) if filters else None
-        npass = np.zeros(1, dtype=np.uint32) if filters else None
+    def _run(self, call, n, records, filters, keep=(), outs=None):
+        rec, ver, dec, pidx, npass = _host_outputs(n, records, filters, outs)
         p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
         _check(call(p(rec), p(ver), p(dec), p(pidx), p(npass)))
         del keep

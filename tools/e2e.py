@@ -51,6 +51,9 @@ ap.add_argument("--group", type=int, default=0,
                 help="drive a bt_group of N members (devices 0..N-1; members share device 0 when fewer GPUs "
                      "are visible, labelled 'shared device'): host gather (bt_group_parse_filter) and zero-copy "
                      "(bt_group_host_register + bt_group_parse_filter_mapped) rows, with host CPU-seconds per Mpkt")
+ap.add_argument("--fresh-outputs", action="store_true",
+                help="host-gather rows: allocate the output arrays inside every call (rounds 1-4's form) "
+                     "instead of once, as a capture loop reuses them")
 a = ap.parse_args()
 cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4}[a.config]
 data, desc = synth.capture(cfg, a.packets)
@@ -82,7 +85,8 @@ if a.group:
     where = {"members": m, "devices": devices, "shared_device": shared, "usable_cpus": abi.usable_cpus(),
              "flags": a.flags,
              "placement": [grp.placement(k) for k in range(m)], "data_nodes": page_nodes(data),
-             "numa_pin": os.environ.get("BT_NUMA_PIN", "1"), "shared_serial": os.environ.get("BT_GROUP_SHARED_SERIAL", "0")}
+             "numa_pin": os.environ.get("BT_NUMA_PIN", "1"), "shared_serial": os.environ.get("BT_GROUP_SHARED_SERIAL", "0"),
+             "outputs": "fresh per call" if a.fresh_outputs else "allocated once"}
 
     def timed(fn):
         best, cpu = 1e9, 0.0
@@ -97,7 +101,8 @@ if a.group:
 
     for mode in ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
-        best, cpu = timed(lambda: grp.run_host(data, desc, records=rec))
+        houts = None if a.fresh_outputs else abi.host_outputs(a.packets, records=rec)
+        best, cpu = timed(lambda: grp.run_host(data, desc, records=rec, outs=houts))
         print(json.dumps({"config": a.config, "flags": a.flags, "mode": f"group {m}, host gather, {mode}",
                           "packets": n, "seconds": round(best, 4), "mpps": round(n / best / 1e6, 1),
                           "host_cpu_s_per_mpkt": round(cpu / (n / 1e6), 4), "cost_model": grp.cost(False, rec, True),
@@ -306,10 +311,11 @@ if a.zero_copy:
 for mode in ("verdicts", "records+verdicts"):
     rec = mode != "verdicts"
     ctx.run_host(data[: 1 << 20], desc[: 1 << 14], records=rec)     # warm pinned buffers
+    houts = None if a.fresh_outputs else abi.host_outputs(a.packets, records=rec)
     best = 1e9
     for _ in range(a.reps):
         t0 = time.perf_counter()
-        out = ctx.run_host(data, desc, records=rec)
+        out = ctx.run_host(data, desc, records=rec, outs=houts)
         best = min(best, time.perf_counter() - t0)
     lens = synth.desc_len(desc)
     h2d = float((((lens.clip(max=112) + 15) // 16) * 16).sum() + 8 * a.packets)
@@ -317,4 +323,5 @@ for mode in ("verdicts", "records+verdicts"):
     print(json.dumps({"config": a.config, "flags": a.flags, "mode": mode, "packets": a.packets, "seconds": round(best, 4),
                       "mpps": round(a.packets / best / 1e6, 1), "h2d_GBps": round(h2d / best / 1e9, 2),
                       "d2h_GBps": round(d2h / best / 1e9, 2), "n_pass": out["n_pass"], "data_nodes": page_nodes(data),
-                      "placement": ctx.placement(), "numa_pin": os.environ.get("BT_NUMA_PIN", "1")}), flush=True)
+                      "placement": ctx.placement(), "numa_pin": os.environ.get("BT_NUMA_PIN", "1"),
+                      "outputs": "fresh per call" if a.fresh_outputs else "allocated once"}), flush=True)

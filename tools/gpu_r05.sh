@@ -9,6 +9,8 @@
 #   ab         AB_LIB (a build under beatrice_amd/ab/) against the in-tree library: first the
 #              fixed-stride / full-size parity tests on AB_LIB (AB_TESTS, a -k expression),
 #              then tools/gpu_abx.sh over AB_CFGS (default c2f), AB_REPS rounds
+#   e2e_outs   host-gather e2e (tools/e2e.py, capture on the device's node) with output arrays
+#              allocated once against fresh per call, alternating, E2E_REPS pairs per config
 #   abn        timing only: the in-tree library and every build named in AB_NAMES
 #              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
 # Every GPU step runs under its own timeout; the first failure ends the call.
@@ -65,6 +67,17 @@ PY
             > "$OUT/abn_${cfg}_${v}_$r.json" 2> "$OUT/abn.err" || fail "abn $cfg $v" $? "$OUT/abn.err"
           python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline']; print(sys.argv[2], sys.argv[3], sys.argv[4], 'step', d['ms_per_step'], 'kern', r['kernel_ms'], 'frac', r['frac'])" \
             "$OUT/abn_${cfg}_${v}_$r.json" $r $cfg $v | tee -a "$OUT/abn.txt"
+        done
+      done
+    done ;;
+  e2e_outs)
+    for r in $(seq 1 ${E2E_REPS:-2}); do
+      for cfg in ${E2E_CFGS:-c2 c3 c4}; do
+        for v in once fresh; do
+          extra=""; [ $v = fresh ] && extra="--fresh-outputs"
+          timeout -k 10 300 python tools/e2e.py --config $cfg --data-node auto --reps 5 $extra \
+            >> "$OUT/e2e_outs.jsonl" 2> "$OUT/e2e_outs.err" || fail "e2e $cfg $v" $? "$OUT/e2e_outs.err"
+          tail -2 "$OUT/e2e_outs.jsonl" | cut -c1-160
         done
       done
     done ;;
