@@ -95,7 +95,7 @@ WORKLOADS["c1"] = dict(cfg=synth.C2, fixed=True, parse=False, filters=None, extr
                             "extracted from 16M x 64B frames, fixed stride: status, extractValue<T> values, field "
                             "bytes (ProtocolParser::parsePacket(frame, ProtocolDefinition), BASELINE configs[0])")
 # the kernels and their launch shapes (bt_runtime.cpp's cache-policy bits are A/B flags)
-KERNEL_SOURCES = ["beatrice_amd/csrc/bt_kernels.hip", "beatrice_amd/csrc/bt_device.h",
+KERNEL_SOURCES = ["beatrice_amd/csrc/bt_kernels.hip", "beatrice_amd/csrc/bt_device.h", "beatrice_amd/csrc/bt_slot_eval.h",
                   "beatrice_amd/csrc/bt_extract.hip"]
 
 
