@@ -11,6 +11,10 @@
 #              then tools/gpu_abx.sh over AB_CFGS (default c2f), AB_REPS rounds
 #   e2e_outs   host-gather e2e (tools/e2e.py, capture on the device's node) with output arrays
 #              allocated once against fresh per call, alternating, E2E_REPS pairs per config
+#   fuzz       fresh-seed randomized sweeps sized to the call: FUZZ_SECONDS (S) for the entry-form
+#              sweep, S/3 for the PAYLOAD sweep, S for the C++ adapter sweep, each under its own
+#              timeout; refuses to start unless S + S/3 + S + 240 s of start-up fits GPURUN_LIMIT
+#              (the --timeout given to gpurun for this call)
 #   abn        timing only: the in-tree library and every build named in AB_NAMES
 #              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
 # Every GPU step runs under its own timeout; the first failure ends the call.
@@ -81,6 +85,18 @@ PY
         done
       done
     done ;;
+  fuzz)
+    S=${FUZZ_SECONDS:-120}; LIMIT=${GPURUN_LIMIT:?GPURUN_LIMIT = the gpurun --timeout of this call}
+    need=$(( S + S / 3 + S + 240 ))
+    [ $need -le $LIMIT ] || { echo "fuzz: ${need} s of sweeps + start-up exceed the call's ${LIMIT} s"; exit 7; }
+    BT_FUZZ_SECONDS=$S BT_FUZZ_SEED=random timeout -k 10 $(( S + S / 3 + 120 )) python -u -m pytest tests/test_gpu_fuzz.py \
+      -m gpu -s -q -p no:cacheprovider --timeout $(( S + 120 )) --timeout-method thread > "$OUT/fuzz_gpu.log" 2>&1 \
+      || fail "fuzz gpu" $? "$OUT/fuzz_gpu.log"
+    grep -iE "rounds|passed|failed" "$OUT/fuzz_gpu.log" | tail -6
+    BT_FUZZ_SECONDS=$S BT_FUZZ_SEED=random timeout -k 10 $(( S + 100 )) python -u -m pytest tests/test_cpp_adapter.py \
+      -k randomized -m gpu -s -q -p no:cacheprovider --timeout $(( S + 90 )) --timeout-method thread \
+      > "$OUT/fuzz_adapter.log" 2>&1 || fail "fuzz adapter" $? "$OUT/fuzz_adapter.log"
+    grep -iE "rounds|passed|failed" "$OUT/fuzz_adapter.log" | tail -4 ;;
   *) echo "unknown case $1"; exit 8 ;;
 esac
 echo "== done $(date +%T)"
