@@ -506,7 +506,9 @@ def measure_extract(name, wl, args, ctx, rank):
     out = {"workload": wl["name"], "value": round(n / step_s / 1e6, 2), "unit": "Mpps",
            "ms_per_step": round(step_s * 1e3, 4), "scaling": "weak", "packets_per_gpu": n, "packets_total": n,
            "parsed_fraction": round(ok / n, 4), "table": [list(f) for f in fields], "span": span,
-           "roofline": roof, "timing": timing,
+           "roofline": roof,
+           "roofline_aggregate": aggregate_roofline([{"algo": algo, "main_ms": tk.main_ms, "step_s": step_s}], 1),
+           "timing": timing,
            "published": "parser_example: 25 us to parse its one 17-byte packet (README.md:1110; BASELINE.md §1)"}
     sample = cap.cpu_sample(wl, seed, args.cpu_sample) if rank == 0 and not args.no_cpu else None
     ex.free()

@@ -118,7 +118,7 @@ def test_rocprof_stats_agree_with_bench_events(cfg):
 
 
 R02 = os.path.join(ROOT, "profiles", "r02")
-ROUNDS = ["r02", "r03", "r04"]   # the closing files of each round since the bench took its current form
+ROUNDS = ["r02", "r03", "r04", "r05"]   # the closing files of each round since the bench took its current form
 
 
 def _check_entry(e, n_gpus=1):
@@ -227,6 +227,42 @@ def test_group_ingest_entry():
     for n in (2, 4):
         r = _line(os.path.join(ROOT, "profiles", "r04", f"bench_{n}rank_one_gpu.json"))
         assert "skipped" in r["configs"]["zero_copy_group"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_r05_lines_carry_cpu_baseline_and_aggregate_roofline_at_every_n(n):
+    """Round 5's rule: at every GPU count the line carries the reference CPU
+    baseline, timed on rank 0 in the same run, and the roofline over all N devices."""
+    name = "bench_default.json" if n == 1 else f"bench_{n}rank_one_gpu.json"
+    d = _line(os.path.join(ROOT, "profiles", "r05", name))
+    assert d["n_gpus"] == n
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["cores"] >= 1 and cb["value"] > 0 and cb["n_gpus_in_job"] == n
+    entries = [d] + [e for k, e in d["configs"].items() if k != "zero_copy_group"]
+    for e in entries:
+        agg = e["roofline_aggregate"]
+        assert agg["devices"] == n and agg["peak"] == n * bench.HBM_PEAK_GBS
+        assert agg["frac"] == pytest.approx(agg["achieved"] / agg["peak"], rel=2e-3)
+        assert e["cpu_baseline"] and e["cpu_baseline"]["value"] > 0
+        if n == 1:   # one device: the aggregate is the line's own roofline
+            assert agg["frac"] == pytest.approx(e["roofline"]["frac"], rel=2e-3)
+        else:        # the bytes of every rank's launch over the slowest rank's kernel time
+            ranks = e["per_rank"]
+            assert agg["kernel_ms_max"] == pytest.approx(max(r["kernel_ms"] for r in ranks), abs=1e-4)
+    if n > 1:
+        assert d["configs"]["c3_strong"]["cpu_baseline"]["same_as"] == "configs.c3"
+
+
+def test_r05_group_ingest_places_the_capture():
+    """The group-ingest entry binds each member's range of the capture to its device's NUMA
+    node and reuses its host-gather output arrays."""
+    d = _line(os.path.join(ROOT, "profiles", "r05", "bench_default.json"))
+    g = d["configs"]["zero_copy_group"]
+    for cap in ("c2", "c3"):
+        e = g[cap]
+        assert e["member_nodes"] == [p["numa_node"] for p in e["placement"]]
+        assert all(nodes == [m] for nodes, m in zip(e["data_nodes"], e["member_nodes"]) if m >= 0)
+    assert "allocated once" in g["c3_host_gather"]["workload"]
 
 
 def test_committed_traffic_is_keyed_to_these_kernels():
