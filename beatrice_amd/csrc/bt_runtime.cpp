@@ -429,6 +429,9 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     if (!b || !o) return fail(BT_E_INVALID_ARGUMENT, "null batch/outputs");
     if (b->n && !b->base) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer");
     if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
+    // the calling thread's current device may be another context's (a group's member threads,
+    // a host driving several devices): launches, events and allocations below are this one's
+    HIP_TRY(hipSetDevice(c->device));
     if (o->records && o->n_cap < b->n) return fail(BT_E_INVALID_ARGUMENT, "records n_cap %u < n %u", o->n_cap, b->n);
     const bool filter = o->verdict || o->decide || o->pass_idx || o->n_pass;
     const bool compact = o->pass_idx || o->n_pass;
@@ -1151,6 +1154,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                   uint32_t* pass_idx, uint32_t* n_pass) {
     int rc = ensure_host(c);
     if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));   // the calling thread may last have driven another device
     const bool want_filter = verdict || decide || pass_idx || n_pass;
     // pass indices come from the verdict words; keep a private copy when the caller
     // did not ask for them
