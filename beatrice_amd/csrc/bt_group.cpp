@@ -441,7 +441,11 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         std::vector<const cpu_set_t*> pins;
         for (bt_ctx* c : g->members) pins.push_back(bt::ctx_pin(c));
         try {
-            g->threads = std::make_unique<MemberThreads>(n_devices, pins);
+            // each member thread starts on its member's device (every entry point it calls selects
+            // the context's device too; this keeps any HIP call made there on the right one)
+            std::vector<int> devs(devices, devices + n_devices);
+            g->threads = std::make_unique<MemberThreads>(n_devices, pins,
+                                                         [devs](uint32_t k) { (void)hipSetDevice(devs[k]); });
         } catch (const std::exception& e) {
             bt_group_destroy(g);
             return bt::set_error(BT_E_RESOURCE, "group threads: %s", e.what());

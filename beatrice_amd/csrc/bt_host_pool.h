@@ -157,7 +157,10 @@ private:
 // serialises them).
 class MemberThreads {
 public:
-    MemberThreads(uint32_t members, const std::vector<const cpu_set_t*>& pins) : q_(members) {
+    // on_start (optional) runs first on member k's thread (the group selects k's device there)
+    MemberThreads(uint32_t members, const std::vector<const cpu_set_t*>& pins,
+                  std::function<void(uint32_t)> on_start = nullptr)
+        : q_(members), on_start_(std::move(on_start)) {
         for (uint32_t k = 1; k < members; ++k) {
             if (pins[k]) {
                 q_[k].pin = *pins[k];
@@ -212,6 +215,7 @@ private:
     void loop(uint32_t k) {
         Queue& q = q_[k];
         if (q.pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(q.pin), &q.pin);
+        if (on_start_) on_start_(k);
         for (;;) {
             Call* c;
             {
@@ -227,6 +231,7 @@ private:
         }
     }
     std::vector<Queue> q_;
+    std::function<void(uint32_t)> on_start_;
 };
 
 }  // namespace bt
