@@ -31,14 +31,22 @@ def _mbind(addr: int, size: int, node: int) -> None:
         raise OSError(ctypes.get_errno(), "mbind")
 
 
-def place_ranges(arr: np.ndarray, ranges: list[tuple[int, int, int]]) -> np.ndarray:
+def place_ranges(arr: np.ndarray, ranges: list[tuple[int, int, int]], hugepages: bool = False) -> np.ndarray:
     """A copy of `arr` whose byte range [lo, hi) of each (lo, hi, node) lies on NUMA node
     `node` (ranges rounded to pages; bytes no range covers follow the default policy). A node
-    < 0 leaves its range unbound. Returns `arr` itself when no range names a node."""
+    < 0 leaves its range unbound. Returns `arr` itself when no range names a node. With
+    `hugepages` the mapping asks for transparent huge pages (madvise, before the first touch);
+    off by default: same box, alternating, host-gather and zero-copy rates were level within
+    their spread either way (profiles/r05/e2e/ab_hugepages.jsonl)."""
     if not any(node >= 0 for _, _, node in ranges):
         return arr
     size = (arr.nbytes + _PAGE - 1) & ~(_PAGE - 1)
     m = mmap.mmap(-1, max(size, _PAGE))
+    if hugepages and hasattr(mmap, "MADV_HUGEPAGE"):
+        try:
+            m.madvise(mmap.MADV_HUGEPAGE)
+        except OSError:
+            pass   # THP off or unsupported: 4-KiB pages
     addr = ctypes.addressof(ctypes.c_char.from_buffer(m))
     for lo, hi, node in ranges:
         if node < 0:
@@ -53,11 +61,11 @@ def place_ranges(arr: np.ndarray, ranges: list[tuple[int, int, int]]) -> np.ndar
     return out
 
 
-def place_on(arr: np.ndarray, node: int | None) -> np.ndarray:
+def place_on(arr: np.ndarray, node: int | None, hugepages: bool = False) -> np.ndarray:
     """A copy of `arr` on NUMA node `node` (None / < 0: `arr` itself)."""
     if node is None or node < 0:
         return arr
-    return place_ranges(arr, [(0, arr.nbytes, node)])
+    return place_ranges(arr, [(0, arr.nbytes, node)], hugepages)
 
 
 def page_nodes(arr: np.ndarray, samples: int = 8) -> list[int]:

@@ -51,6 +51,8 @@ ap.add_argument("--group", type=int, default=0,
                 help="drive a bt_group of N members (devices 0..N-1; members share device 0 when fewer GPUs "
                      "are visible, labelled 'shared device'): host gather (bt_group_parse_filter) and zero-copy "
                      "(bt_group_host_register + bt_group_parse_filter_mapped) rows, with host CPU-seconds per Mpkt")
+ap.add_argument("--hugepages", action="store_true",
+                help="with --data-node: ask for transparent huge pages for the bound capture mapping")
 ap.add_argument("--fresh-outputs", action="store_true",
                 help="host-gather rows: allocate the output arrays inside every call (rounds 1-4's form) "
                      "instead of once, as a capture loop reuses them")
@@ -60,6 +62,10 @@ data, desc = synth.capture(cfg, a.packets)
 
 
 from beatrice_amd.numa import page_nodes, place_on  # noqa: E402
+
+
+def place(arr, node):
+    return place_on(arr, node, hugepages=a.hugepages)
 
 
 def data_node_for(placement):
@@ -80,7 +86,7 @@ if a.group:
     grp = abi.Group(devices, host_chunk_packets=a.chunk, host_threads=a.host_threads,
                     flags=a.flags | (abi.OPT_GROUP_SHARED_DEVICE if shared else 0))
     grp.compile(FILTERS)
-    data = place_on(data, data_node_for(grp.placement(0)))
+    data = place(data, data_node_for(grp.placement(0)))
     n = a.packets
     where = {"members": m, "devices": devices, "shared_device": shared, "usable_cpus": abi.usable_cpus(),
              "flags": a.flags,
@@ -132,12 +138,12 @@ if a.group:
     sys.exit(0)
 ctx = abi.Context(0, host_chunk_packets=a.chunk, host_threads=a.host_threads, flags=a.flags)
 ctx.compile(FILTERS)
-data = place_on(data, data_node_for(ctx.placement()))
+data = place(data, data_node_for(ctx.placement()))
 if a.tpacket:
     import numpy as np
     ring, rdesc, used = synth.tpv3_ring(data, desc)
     del data
-    ring = place_on(ring, data_node_for(ctx.placement()))
+    ring = place(ring, data_node_for(ctx.placement()))
     bs, n = synth.TPV3_BLOCK, len(rdesc)
     B = a.ring_batch_blocks
     nbat = (used + B - 1) // B

@@ -15,6 +15,8 @@
 #              sweep, S/3 for the PAYLOAD sweep, S for the C++ adapter sweep, each under its own
 #              timeout; refuses to start unless S + S/3 + S + 240 s of start-up fits GPURUN_LIMIT
 #              (the --timeout given to gpurun for this call)
+#   e2e_thp    host-gather and zero-copy e2e with the bound capture on transparent huge pages
+#              (--hugepages) against 4-KiB pages, alternating, E2E_REPS pairs per config
 #   abn        timing only: the in-tree library and every build named in AB_NAMES
 #              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
 # Every GPU step runs under its own timeout; the first failure ends the call.
@@ -97,6 +99,19 @@ PY
       -k randomized -m gpu -s -q -p no:cacheprovider --timeout $(( S + 90 )) --timeout-method thread \
       > "$OUT/fuzz_adapter.log" 2>&1 || fail "fuzz adapter" $? "$OUT/fuzz_adapter.log"
     grep -iE "rounds|passed|failed" "$OUT/fuzz_adapter.log" | tail -4 ;;
+  e2e_thp)
+    for r in $(seq 1 ${E2E_REPS:-2}); do
+      for cfg in ${E2E_CFGS:-c2 c3 c4}; do
+        for mode in "" "--zero-copy"; do
+          for v in thp small; do
+            extra=""; [ $v = thp ] && extra="--hugepages"
+            timeout -k 10 300 python tools/e2e.py --config $cfg --data-node auto --reps 5 $mode $extra \
+              | sed "s/^{/{\"pages\": \"$v\", /" >> "$OUT/e2e_thp.jsonl" 2> "$OUT/e2e_thp.err" || fail "e2e $cfg $v" $? "$OUT/e2e_thp.err"
+          done
+        done
+      done
+    done
+    tail -4 "$OUT/e2e_thp.jsonl" | cut -c1-120 ;;
   *) echo "unknown case $1"; exit 8 ;;
 esac
 echo "== done $(date +%T)"
