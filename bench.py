@@ -653,6 +653,28 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
     return out
 
 
+def group_ingest_isolated(n_dev: int, packets: int, timeout: int = 900) -> dict:
+    """measure_group_ingest in a child process (N > 1): the group then drives every device of
+    the node from one process, which only this entry does and which no 1-GPU box can rehearse;
+    a failure there (an error, or a fault that would end the process) is reported in the
+    line instead of ending rank 0 before it prints. A child process, never an exec."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--group-ingest-child", str(n_dev),
+                            "--group-ingest-packets", str(packets)], env=env, capture_output=True, text=True,
+                           timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"group ingest child did not finish in {timeout} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"group ingest child exited {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+    out = json.loads(lines[-1])
+    out["process"] = "child of rank 0"
+    return out
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -744,9 +766,18 @@ def main():
                     help="A/B only: comma list of the headline's outputs (records,decide,verdict,pass_idx)")
     ap.add_argument("--group-ingest-packets", type=int, default=1 << 24,
                     help="packets of the in-process group zero-copy ingest entry (0 = skip it)")
+    ap.add_argument("--group-ingest-child", type=int, default=0, help=argparse.SUPPRESS)   # internal
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
+
+    if args.group_ingest_child:   # group_ingest_isolated's child: only the group entry, one JSON line
+        try:
+            res = measure_group_ingest(args.group_ingest_child, args.group_ingest_packets)
+        except Exception as e:   # reported, never fatal to the parent's line
+            res = {"error": str(e)[:300]}
+        print(json.dumps(res), flush=True)
+        return
 
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
@@ -814,7 +845,8 @@ def main():
         dist.barrier()
     if rank == 0 and args.group_ingest_packets > 0 and args.configs != "none":
         try:
-            results["zero_copy_group"] = measure_group_ingest(world, args.group_ingest_packets)
+            results["zero_copy_group"] = (measure_group_ingest(world, args.group_ingest_packets) if world == 1
+                                          else group_ingest_isolated(world, args.group_ingest_packets))
         except Exception as e:   # reported, never fatal to the line
             results["zero_copy_group"] = {"error": str(e)[:300]}
     if dist is not None:

@@ -101,3 +101,13 @@ def test_no_sample_means_no_baseline():
     bench.attach_cpu_baselines(results, {"__head__": (None, {})}, {"affinity_cpus": 1, "threads": 1}, 2,
                                lambda *a: pytest.fail("timed without a sample"), 1.0)
     assert results["__head__"]["cpu_baseline"] is None
+
+
+def test_group_ingest_runs_in_a_child_process_at_n_gt_1(monkeypatch):
+    """At N > 1 rank 0 runs the group-ingest entry in a child process, so a failure there is
+    reported in the line instead of ending rank 0. Here (no GPU) the child reports the skip."""
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.setenv(k, "0" if k != "WORLD_SIZE" else "2")   # the parent's rank env must not leak
+    out = bench.group_ingest_isolated(2, 4096, timeout=240)
+    assert out.get("process") == "child of rank 0", out
+    assert "skipped" in out and "the job has 2" in out["skipped"]
