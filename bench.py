@@ -572,7 +572,7 @@ def cpu_baseline(sample, wl, seconds, cpus):
                       f"instances, disjoint shards"}
 
 
-def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
+def measure_group_ingest(n_dev: int, packets: int, reps: int = 5, shared: bool = False) -> dict:
     """The product's multi-GPU ingest, in one process: a bt_group over the job's n_dev devices
     reads one batch of frames in registered host memory (an AF_XDP UMEM / a capture ring's
     shape: frames back to back) in place, every device its range over its own PCIe link
@@ -583,20 +583,25 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
 
     The capture is placed the way INTEGRATION.md §4 tells a deployment to allocate its ring or
     UMEM: each member's byte range of the batch on its device's NUMA node (the nodes the
-    members' gather threads are pinned to), reported in `placement` / `data_nodes`."""
+    members' gather threads are pinned to), reported in `placement` / `data_nodes`.
+
+    shared (a rank rehearsal on a 1-GPU box, BT_BENCH_DEVICE): the n_dev members share device 0
+    (BT_OPT_GROUP_SHARED_DEVICE, one PCIe link), so the N > 1 code path runs end to end; its
+    rates are one link's, not a scaling point."""
     import time as _time
     from beatrice_amd import numa
     visible = abi.device_count()
-    if visible < n_dev:
+    if visible < (1 if shared else n_dev):
         return {"skipped": f"rank 0 sees {visible} device(s), the job has {n_dev}"}
-    devs = list(range(n_dev))
+    devs = [0] * n_dev if shared else list(range(n_dev))
     out = {"workload": "zero-copy ingest, one process, bt_group over the job's devices: frames in registered "
                        "host memory read in place over each device's PCIe link (bt_group_parse_filter_mapped), "
                        "C3's 5-tuple filter, decisions + verdict words back into host memory",
-           "n_devices": n_dev, "packets": packets, "scaling": "strong", "pcie_inclusive": True, "unit": "Mpps"}
+           "n_devices": n_dev, "packets": packets, "scaling": "strong", "pcie_inclusive": True, "unit": "Mpps",
+           "members_share_one_device": shared}
     for name, cfg in (("c2", synth.C2), ("c3", synth.C3)):
         raw, desc = synth.capture(cfg, packets)
-        grp = abi.Group(devs)
+        grp = abi.Group(devs, flags=abi.OPT_GROUP_SHARED_DEVICE if shared else 0)
         held = []
         try:
             grp.compile(C3_FILTERS)
@@ -653,7 +658,7 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5) -> dict:
     return out
 
 
-def group_ingest_isolated(n_dev: int, packets: int, timeout: int = 900) -> dict:
+def group_ingest_isolated(n_dev: int, packets: int, timeout: int = 900, shared: bool = False) -> dict:
     """measure_group_ingest in a child process (N > 1): the group then drives every device of
     the node from one process, which only this entry does and which no 1-GPU box can rehearse;
     a failure there (an error, or a fault that would end the process) is reported in the
@@ -663,8 +668,8 @@ def group_ingest_isolated(n_dev: int, packets: int, timeout: int = 900) -> dict:
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     try:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--group-ingest-child", str(n_dev),
-                            "--group-ingest-packets", str(packets)], env=env, capture_output=True, text=True,
-                           timeout=timeout)
+                            "--group-ingest-packets", str(packets)] + (["--group-ingest-shared"] if shared else []),
+                           env=env, capture_output=True, text=True, timeout=timeout)
     except subprocess.TimeoutExpired:
         return {"error": f"group ingest child did not finish in {timeout} s"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -767,13 +772,15 @@ def main():
     ap.add_argument("--group-ingest-packets", type=int, default=1 << 24,
                     help="packets of the in-process group zero-copy ingest entry (0 = skip it)")
     ap.add_argument("--group-ingest-child", type=int, default=0, help=argparse.SUPPRESS)   # internal
+    ap.add_argument("--group-ingest-shared", action="store_true", help=argparse.SUPPRESS)  # internal
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     if args.group_ingest_child:   # group_ingest_isolated's child: only the group entry, one JSON line
         try:
-            res = measure_group_ingest(args.group_ingest_child, args.group_ingest_packets)
+            res = measure_group_ingest(args.group_ingest_child, args.group_ingest_packets,
+                                       shared=args.group_ingest_shared)
         except Exception as e:   # reported, never fatal to the parent's line
             res = {"error": str(e)[:300]}
         print(json.dumps(res), flush=True)
@@ -846,7 +853,8 @@ def main():
     if rank == 0 and args.group_ingest_packets > 0 and args.configs != "none":
         try:
             results["zero_copy_group"] = (measure_group_ingest(world, args.group_ingest_packets) if world == 1
-                                          else group_ingest_isolated(world, args.group_ingest_packets))
+                                          else group_ingest_isolated(world, args.group_ingest_packets,
+                                                                     shared=devices["rehearsal_one_device"]))
         except Exception as e:   # reported, never fatal to the line
             results["zero_copy_group"] = {"error": str(e)[:300]}
     if dist is not None:
