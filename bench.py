@@ -36,7 +36,8 @@ Captures are generated range by range on the host (bt_synth_fill_range) and stre
 the device, so no rank holds a whole capture in host memory.
 
 Timing: W untimed warm-up steps; then barrier + device sync, K steps, device sync +
-barrier; max over ranks. bt_time_device2 enqueues the K steps between one event pair and
+barrier; each rank's clock runs from its release at the opening barrier to its closing sync
+(the closing barrier's latency is reported, not counted); max over ranks. bt_time_device2 enqueues the K steps between one event pair and
 waits by polling; its breakdown (enqueue / first event seen / last event seen / GPU span)
 goes into the line. Steps with a compaction are pipelined (bt_parse_filter_device_async:
 step i's compaction runs on a second stream beside step i+1's main kernel; two output
@@ -374,14 +375,20 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
         if dist is not None:
             dist.barrier()
 
+    # The K steps are bracketed by a barrier + device sync on both sides; each rank's clock runs
+    # from its release at the opening barrier to its closing sync, and the line takes the max
+    # over ranks. The closing barrier's own latency (gloo: ~0.1 ms at 2 ranks, ~0.4-0.6 ms at 8
+    # on a busy host, against ~7 ms for 20 c2f steps) is reported in `timing`, not counted as
+    # step time: ranks share no data, so it is not part of any rank's work.
     barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     tm = ctx.time_device2(run.batch, outs, args.steps, timed_mode)
     ta = time.perf_counter()
     ctx.synchronize()
-    barrier()
     t1 = time.perf_counter()
+    barrier()
+    tb = time.perf_counter()
     step_s = (t1 - t0) / args.steps
     # The main kernel's duration: the same K steps again, each main kernel between an
     # event pair recorded by its own dispatch. Those events cost the GPU ~9 us per step
@@ -400,7 +407,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     floor_write = rec_lines * LINE + ((n + (n + 63) // 64 * 8) if filt else 0)
     main_ms = tk.main_ms
     mine = {"step_s": step_s, "main_ms": main_ms, "n": n, "algo": algo, "pass": n_pass,
-            "host_ms": 1e3 * (ta - t0), "tail_ms": 1e3 * (t1 - ta)}
+            "host_ms": 1e3 * (ta - t0), "tail_ms": 1e3 * (t1 - ta), "barrier_ms": 1e3 * (tb - t1)}
     ranks = [mine]
     if dist is not None:
         ranks = [None] * world
@@ -432,6 +439,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     timing = tm.as_dict()
     timing.update({"wall_ms": round(1e3 * step_s * args.steps, 4), "host_call_ms": round(mine["host_ms"], 4),
                    "tail_sync_ms": round(mine["tail_ms"], 4),
+                   "closing_barrier_ms_max_over_ranks": round(max(r["barrier_ms"] for r in ranks), 4),
                    "wall_over_span": round(step_s * args.steps * 1e3 / tm.span_ms, 4) if tm.span_ms > 0 else None,
                    "pipelined": piped, "output_sets": len(outs),
                    "kernel_events_in_timed_region": bool(args.kernel_events_in_timed)})
