@@ -19,8 +19,6 @@ _SYS_MOVE_PAGES = 279
 _MPOL_BIND = 2
 _PAGE = 4096
 
-_held: list = []        # the mappings behind the arrays returned here (kept alive with them)
-
 
 def _mbind(addr: int, size: int, node: int) -> None:
     mask = (ctypes.c_ulong * 16)()
@@ -47,7 +45,8 @@ def place_ranges(arr: np.ndarray, ranges: list[tuple[int, int, int]], hugepages:
             m.madvise(mmap.MADV_HUGEPAGE)
         except OSError:
             pass   # THP off or unsupported: 4-KiB pages
-    addr = ctypes.addressof(ctypes.c_char.from_buffer(m))
+    anchor = ctypes.c_char.from_buffer(m)
+    addr = ctypes.addressof(anchor)
     for lo, hi, node in ranges:
         if node < 0:
             continue
@@ -55,9 +54,9 @@ def place_ranges(arr: np.ndarray, ranges: list[tuple[int, int, int]], hugepages:
         b = min(size, (hi + _PAGE - 1) & ~(_PAGE - 1))
         if b > a:
             _mbind(addr + a, b - a, node)
-    out = np.frombuffer(m, dtype=arr.dtype, count=arr.size)
+    del anchor   # the ctypes view's export of the mapping ends here
+    out = np.frombuffer(m, dtype=arr.dtype, count=arr.size)   # holds the mapping: freed with the array
     np.copyto(out, arr)
-    _held.append(m)
     return out
 
 
