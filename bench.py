@@ -53,6 +53,7 @@ from the reference sources) on rank 0, on every host CPU the process may use
 from __future__ import annotations
 
 import argparse
+import contextlib
 import hashlib
 import json
 import os
@@ -751,6 +752,21 @@ def check_devices(ctx, dist, world) -> dict:
             "rehearsal_one_device": bool(pinned and world > 1)}
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Point fd 1 at stderr for the duration (native libraries' prints included), so that
+    rank 0's stdout holds nothing but the line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -809,7 +825,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("gloo")
+        with stdout_to_stderr():   # gloo's "[Gloo] Rank r is connected to ..." lines: stdout is the JSON line's
+            dist.init_process_group("gloo")
     flags = args.flags if args.flags is not None else (abi.OPT_NO_PREFETCH if args.no_prefetch else 0)
     flags |= abi.OPT_SPIN_SYNC   # host waits spin: no wake-up latency inside the timed region
     # BT_BENCH_DEVICE: put every rank on one device (multi-rank rehearsal on a 1-GPU box)

@@ -111,3 +111,26 @@ def test_group_ingest_runs_in_a_child_process_at_n_gt_1(monkeypatch):
     out = bench.group_ingest_isolated(2, 4096, timeout=240)
     assert out.get("process") == "child of rank 0", out
     assert "skipped" in out and "the job has 2" in out["skipped"]
+
+
+def test_gloo_connection_lines_stay_off_stdout(tmp_path):
+    """At N > 1 every rank's gloo init prints "[Gloo] Rank r is connected to ..." on stdout;
+    bench.py points fd 1 at stderr around init_process_group so rank 0's stdout is the line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    code = ("import json, sys; sys.path.insert(0, %r); import bench, torch.distributed as d\n"
+            "with bench.stdout_to_stderr(): d.init_process_group('gloo')\n"
+            "d.barrier(); print(json.dumps({'rank': d.get_rank()}), flush=True); d.destroy_process_group()\n") % ROOT
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for r, (out, err) in enumerate(outs):
+        assert procs[r].returncode == 0, err
+        assert out.strip().splitlines() == ['{"rank": %d}' % r], out
