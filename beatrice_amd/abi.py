@@ -557,11 +557,28 @@ def host_outputs(n: int, records=True, filters=True) -> dict:
 
 
 def _host_outputs(n, records, filters, outs):
+    """The output arrays of a run_host call: `outs` (from host_outputs) checked against what
+    the call writes — the native side takes bare pointers, so a short or mistyped array would
+    be written past its end — or fresh ones."""
     if outs is None:
         outs = host_outputs(n, records, filters)
     else:
-        assert (outs["records"] is not None) == bool(records) and (outs["decide"] is not None) == bool(filters)
-        assert outs["decide"] is None or len(outs["decide"]) == n
+        need = {"records": (bool(records), np.uint8, n * BT_REC_BYTES),
+                "verdict": (bool(filters), np.uint64, (n + 63) // 64),
+                "decide": (bool(filters), np.uint8, n),
+                "pass_idx": (bool(filters), np.uint32, max(n, 1)),
+                "n_pass": (bool(filters), np.uint32, 1)}
+        for k, (want, dt, size) in need.items():
+            a = outs.get(k)
+            if (a is not None) != want:
+                raise ValueError(f"outs[{k!r}]: {'required' if want else 'must be None'} for this call")
+            if a is not None and (a.dtype != dt or not a.flags.c_contiguous or not a.flags.writeable or a.size < size):
+                raise ValueError(f"outs[{k!r}]: need a writable contiguous {np.dtype(dt).name} array of at least "
+                                 f"{size} elements, got {a.dtype} x {a.size}")
+        # views of this call's part (arrays sized for a larger batch are reused as they are)
+        outs = {k: None if outs[k] is None else outs[k].reshape(-1)[:size] for k, (_, _, size) in need.items()}
+        if outs["records"] is not None:
+            outs["records"] = outs["records"].reshape(n, BT_REC_BYTES)
     return outs["records"], outs["verdict"], outs["decide"], outs["pass_idx"], outs["n_pass"]
 
 

@@ -137,3 +137,19 @@ def test_host_stage_bytes_refuses_null_arguments():
     assert abi.lib().bt_host_stage_bytes(None, 0, ctypes.byref(b)) == BT_E_INVALID_ARGUMENT
     assert abi.lib().bt_host_stage_bytes(None, 1, None) == BT_E_INVALID_ARGUMENT
     assert b.value == 7
+
+
+def test_reused_host_outputs_are_checked_and_viewed_per_call():
+    """run_host's `outs`: the native side takes bare pointers, so arrays too short, of the
+    wrong type or missing are refused before the call; larger ones are reused as views."""
+    import numpy as np
+    o = abi.host_outputs(100)
+    rec, ver, dec, pidx, npass = abi._host_outputs(70, True, True, o)
+    assert rec.shape == (70, abi.BT_REC_BYTES) and rec.ctypes.data == o["records"].ctypes.data
+    assert len(ver) == 2 and len(dec) == 70 and len(pidx) == 70 and len(npass) == 1
+    for bad in (dict(o, decide=np.zeros(50, np.uint8)), dict(o, records=None),
+                dict(o, verdict=np.zeros(2, np.int64)), dict(o, pass_idx=np.zeros(200, np.uint32)[::2])):
+        with pytest.raises(ValueError):
+            abi._host_outputs(100, True, True, bad)
+    with pytest.raises(ValueError):   # records given to a filter-only call
+        abi._host_outputs(10, False, True, o)
