@@ -19,6 +19,8 @@
 #              (--hugepages) against 4-KiB pages, alternating, E2E_REPS pairs per config
 #   abn        timing only: the in-tree library and every build named in AB_NAMES
 #              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
+#   envab      timing only: the in-tree library with and without AB_ENV (e.g. BT_XCD_ORDER=1),
+#              alternating processes, AB_REPS rounds of AB_CFGS, 50 steps each
 # Every GPU step runs under its own timeout; the first failure ends the call.
 set -o pipefail
 OUT=${OUT:-gpurun_out/r05}
@@ -34,6 +36,23 @@ sq_pass() {   # sq_pass NAME CONFIG COUNTERS...: one rocprofv3 PMC pass of a ben
 }
 
 case $1 in
+  envab)
+    for r in $(seq 1 ${AB_REPS:-3}); do
+      for cfg in ${AB_CFGS:-c2f}; do
+        for v in base env; do
+          e=""; [ $v = env ] && e="${AB_ENV:?AB_ENV=NAME=VALUE}"
+          env $e timeout -k 10 150 python3 bench.py --config $cfg --configs none --no-cpu --steps 50 --warmup 5 \
+            > "$OUT/envab_${r}_${cfg}_$v.json" 2> "$OUT/envab.err" || fail "envab $cfg $v" $? "$OUT/envab.err"
+          python3 - "$OUT/envab_${r}_${cfg}_$v.json" "$cfg $v" "$r" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+r = d["roofline"]
+print(f"round {sys.argv[3]} {sys.argv[2]:10s} kernel {r['kernel_ms']:.4f} ms (min {r['kernel_ms_min']:.4f}) "
+      f"step {d['ms_per_step']:.4f} value {d['value']}", flush=True)
+PY
+        done
+      done
+    done ;;
   c2f_split)
     for r in $(seq 1 ${ROUNDS:-3}); do
       for v in c2 c2f c2f:records c2f:records,decide c2f:records,verdict; do
