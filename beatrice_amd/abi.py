@@ -77,6 +77,7 @@ OPT_PIPELINE = 0x2000
 OPT_GROUP_SHARED_DEVICE = 0x4000
 OPT_NO_LEAN_PCIE = 0x8000
 OPT_MAPPED_GATHER_SPARSE = 0x10000
+OPT_NO_LEAN_HOST = 0x20000
 TIME_KERNEL_EVENTS = 0x1
 TIME_PIPELINED = 0x2
 

@@ -79,8 +79,8 @@ struct bt_group {
     std::unique_ptr<std::atomic<uint32_t>[]> busy;   // per member: call parts running on it
     std::atomic<uint32_t> rr{0};
     uint32_t route_below = 0;
-    // the host batches' staged window per frame without / with records (bt_host_stage_bytes of
-    // the installed program), cached when a program is installed so that a split reads it
+    // the host batches' staged window per frame without / with records (the bytes the host
+    // pipeline copies for the installed program: 32 / 112 / 176), cached when a program is installed so that a split reads it
     // without taking member 0's context lock (which a host batch in flight holds)
     std::atomic<uint32_t> stage_window[2] = {{0u}, {0u}};
 };
@@ -435,7 +435,7 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         g->route_below = rb ? (uint32_t)strtoul(rb, nullptr, 10) : (1u << 20);
         g->busy = std::make_unique<std::atomic<uint32_t>[]>(n_devices);
         for (uint32_t i = 0; i < n_devices; ++i) g->busy[i].store(0, std::memory_order_relaxed);
-        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::stage_bytes_of(g->members[0], r != 0));
+        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::staged_bytes_of(g->members[0], r != 0));
     }
     if (n_devices > 1) {
         std::vector<const cpu_set_t*> pins;
@@ -481,7 +481,7 @@ int bt_group_filter_compile(bt_group* g, const bt_filter_desc* filters, uint32_t
         bt::CompiledProgram p;   // compiled once, installed on every device
         if (int rc = bt::compile_program(filters, n, bt::ctx_flags(g->members[0]), &p)) return rc;
         const int rc = run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
-        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::stage_bytes_of(g->members[0], r != 0));
+        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::staged_bytes_of(g->members[0], r != 0));
         return rc;
     } catch (const std::exception& e) {
         return bt::set_error(BT_E_INTERNAL, "bt_group_filter_compile: %s", e.what());

@@ -29,6 +29,9 @@ const cpu_set_t* ctx_pin(const bt_ctx* c);
 void ctx_forget_base(bt_ctx* c);
 // bt_host_stage_bytes without the C-ABI's checks.
 uint32_t stage_bytes_of(bt_ctx* c, bool records);
+// Bytes per frame the host pipeline copies to the device (<= stage_bytes_of: a filter-only
+// call stages bytes 12..43 only): the host batches' split cost.
+uint32_t staged_bytes_of(bt_ctx* c, bool records);
 // CPUs this process may use: its affinity set bounded by the cgroup v2 CPU quota.
 unsigned usable_cpus();
 // The CPUs of NUMA node `node` in this process's affinity set (false: none / unknown).

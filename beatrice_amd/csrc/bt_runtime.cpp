@@ -58,6 +58,9 @@ constexpr uint32_t kHostSlotPayload = 176;
 // ... and for calls that return no records and have no GPU PAYLOAD slot: the filters read
 // bytes 12..37 (kNeedFilter) and such calls never take a second round, so 48 B
 constexpr uint32_t kHostSlotFilter = 48;
+// ... of which a filter-only call stages bytes [kLeanLo, kLeanLo + 32)
+constexpr uint32_t kHostLeanWidth = 32;
+static_assert(kLeanLo + kHostLeanWidth >= kNeedFilter && kLeanLo + kHostLeanWidth <= kHostSlotFilter, "lean staging");
 constexpr uint32_t kGatherAheadDefault = 12;   // frames the host gather prefetches ahead
 static_assert(kHostSlotFilter >= kNeedFilter && kHostSlotFilter % 16 == 0, "filter-only staging");
 
@@ -1127,9 +1130,9 @@ int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t i
 
 namespace {
 
-// Bytes of each frame the host pipeline stages (bt_host_stage_bytes): the walk's 112 with
-// records; the filters' 38 B (as 48) for filter-only calls, whose kernels take no second
-// round (staging the walk's 112 B took 2-3x the gather and the copy for IMIX frames); the
+// Bytes of each frame the host pipeline reads (bt_host_stage_bytes): the walk's 112 with
+// records; the filters' 38 B (as 48; bytes 12..43 of them staged) for filter-only calls, whose
+// kernels take no second round (staging the walk's 112 B took 2-3x the gather and the copy for IMIX frames); the
 // payload window with a GPU PAYLOAD slot (bytes past the staged prefix would be the next
 // frame's).
 uint32_t stage_bytes(const bt_ctx* c, bool records) {
@@ -1142,6 +1145,11 @@ namespace bt {
 uint32_t stage_bytes_of(bt_ctx* c, bool records) {
     std::lock_guard<std::mutex> lk(c->mu);
     return stage_bytes(c, records);
+}
+uint32_t staged_bytes_of(bt_ctx* c, bool records) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const uint32_t w = stage_bytes(c, records);
+    return w == kHostSlotFilter && !(c->opts.flags & BT_OPT_NO_LEAN_HOST) ? kHostLeanWidth : w;
 }
 }  // namespace bt
 
@@ -1166,6 +1174,14 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
     // bytes staged per frame: the header walk's, or with a GPU PAYLOAD slot in the program
     // the payload window's too (bytes past the staged prefix would be the next frame's)
     const uint32_t slot = stage_bytes(c, records != nullptr);
+    // Filter-only calls (no records, no GPU PAYLOAD slot) stage only frame bytes [12, 44): the
+    // filters read 12..37 and such calls take no second round. Each frame's descriptor then
+    // points 12 B before its staged bytes (the buffer starts with a 16-B pad, so no offset is
+    // negative); bytes 0..11 of that window are the previous slot's, which nothing reads.
+    const bool lean = slot == kHostSlotFilter && !(c->opts.flags & BT_OPT_NO_LEAN_HOST);
+    const uint32_t lo = lean ? kLeanLo : 0u;
+    const uint32_t width = lean ? kHostLeanWidth : slot;
+    const uint32_t pad = lean ? 16u : 0u;
     static const bool prefetch = getenv("BT_NO_GATHER_PREFETCH") == nullptr;   // A/B knobs
     // non-temporal staging stores (BT_GATHER_NT=0: plain copies). Same-box A/B, 5 pairs over
     // two boxes (profiles/r04/e2e/ab_gather_nt*.jsonl): C2 verdicts +2..+34 % in every pair,
@@ -1200,10 +1216,11 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 for (uint32_t i = a; i < b; ++i) {
                     uint32_t len = 0;
                     (void)frame(base_i + i, &len);
-                    sum += (std::min(len, slot) + 15) & ~15u;
+                    sum += (std::min(len > lo ? len - lo : 0u, width) + 15) & ~15u;
                 }
                 part[w + 1] = sum;
             });
+            part[0] = pad;
             for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
             pipeline_run(c, cnt, T, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
@@ -1211,15 +1228,15 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 for (uint32_t i = a; i < b; ++i) {
                     if (prefetch && i + kGatherAhead < b) {   // frames far apart: start the miss early
                         uint32_t l2 = 0;
-                        const uint8_t* g = frame(base_i + i + kGatherAhead, &l2);
+                        const uint8_t* g = frame(base_i + i + kGatherAhead, &l2) + lo;
                         __builtin_prefetch(g);
-                        if (((uintptr_t)g & 63u) + std::min(l2, slot) > 64u) __builtin_prefetch(g + 64);
+                        if (((uintptr_t)g & 63u) + std::min(l2 > lo ? l2 - lo : 0u, width) > 64u) __builtin_prefetch(g + 64);
                     }
                     uint32_t len = 0;
                     const uint8_t* f = frame(base_i + i, &len);
-                    const uint32_t m = std::min(len, slot);
-                    if (m) stage_prefix(pre + p, f, m, nt);
-                    d[i] = BT_DESC(p, len);
+                    const uint32_t m = std::min(len > lo ? len - lo : 0u, width);
+                    if (m) stage_prefix(pre + p, f + lo, m, nt);
+                    d[i] = BT_DESC(p - lo, len);
                     p += (m + 15) & ~15u;
                 }
                 if (nt) __builtin_ia32_sfence();   // the prefixes are visible before the H2D copy

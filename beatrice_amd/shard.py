@@ -29,15 +29,17 @@ def packet_cost(lengths, cost=DEFAULT_COST) -> np.ndarray:
     return w + fixed
 
 
-def group_cost(mapped: bool, records: bool, filters: bool, desc_bytes: int = 8, stage_bytes: int = 48):
+def group_cost(mapped: bool, records: bool, filters: bool, desc_bytes: int = 8, stage_bytes: int | None = None):
     """bt_group_cost (include/beatrice_gpu.h): what one packet costs a group member.
-    Host batches stage round_up(min(len, stage_bytes), 16) bytes (bt_host_stage_bytes: 48
-    filter-only, 112 with records, 176 with a GPU PAYLOAD slot), copy its descriptor up and
-    its 96-B bt_rec and decision byte back; mapped batches read the header window over the
-    member's PCIe link (the lean 48 B filter-only, the walk's 128 with records) and write
-    packed record slabs (~64 B) and the decision."""
+    Host batches stage round_up(min(len, stage_bytes), 16) bytes (the bytes the host pipeline
+    copies: 32 filter-only, frame bytes 12..43; 112 with records; 176 with a GPU PAYLOAD slot),
+    copy its descriptor up and its 96-B bt_rec and decision byte back; mapped batches read the
+    header window over the member's PCIe link (the lean 48 B filter-only, the walk's 128 with
+    records) and write packed record slabs (~64 B) and the decision."""
     if mapped:
         return (128 if records else 48, 16, desc_bytes + (64 if records else 0) + (1 if filters else 0))
+    if stage_bytes is None:
+        stage_bytes = 112 if records else 32
     return (stage_bytes, 16, desc_bytes + (96 if records else 0) + (1 if filters else 0))
 
 

@@ -310,6 +310,8 @@ typedef struct bt_opts {
                                       mean spacing >= BT_MAPPED_GATHER_ABOVE, default 512 B)
                                       gathers their prefixes on its host threads instead of
                                       reading each frame's window over PCIe */
+#define BT_OPT_NO_LEAN_HOST 0x20000u /* host batches, filter-only: stage each frame's first 48 B
+                                      instead of bytes 12..43 (A/B only) */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */
@@ -417,7 +419,8 @@ int  bt_parse_filter_ptrs(bt_ctx* ctx, const uint8_t* const* frames, const uint3
                           bt_rec* records, uint64_t* verdict, uint8_t* decide,
                           uint32_t* pass_idx, uint32_t* n_pass);
 /* The bytes of each frame the two calls above read (and stage) with the context's current
- * program: min(len, *bytes) from the frame's start; 48 for filter-only calls, 112 with
+ * program: at most min(len, *bytes) from the frame's start; 48 for filter-only calls (which
+ * read and stage bytes 12..43 of it), 112 with
  * records, 176 when the program has a GPU PAYLOAD slot (with_records: whether the call asks
  * for records). A caller may pass, in place of a frame, a copy of that many of its first
  * bytes with the frame's true length (e.g. prefixes packed when the packet arrived). */
@@ -566,7 +569,8 @@ int      bt_group_split_plan(const uint32_t* lens, uint32_t n, uint32_t parts, c
 /* The cost model a group call uses (mapped: bt_group_parse_filter_mapped, else the host
  * batches), for a call that asks for records / filter outputs, with desc_bytes-byte
  * descriptors (8 packed, 16 xdp_desc, 0 fixed stride):
- *   host batches: window = bt_host_stage_bytes (48 / 112 / 176), align 16,
+ *   host batches: window = the bytes staged per frame (32: a filter-only call stages frame
+ *                 bytes 12..43; 112 with records; 176 with a GPU PAYLOAD slot), align 16,
  *                 fixed = desc_bytes + 96 (records, bt_rec D2H) + 1 (decision D2H)
  *   mapped:       window = 128 with records (the walk's wide window) else 48 (the lean
  *                 first round reads frame bytes 12..37: two or three 16-B chunks by the

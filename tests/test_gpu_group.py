@@ -308,6 +308,7 @@ def test_group_placement_and_budget():
                 assert p["numa_node"] >= 0 and p["pinned_cpus"] == len(abi.node_cpus(p["numa_node"]))
         assert grp.cost(True, False, True, 16) == (48, 16, 17)
         assert grp.cost(False, True, True, 8) == (112, 16, 105)
+        assert grp.cost(False, False, True, 8) == (32, 16, 9)   # filter-only host batches stage bytes 12..43
     finally:
         grp.close()
 

@@ -78,3 +78,28 @@ def test_stage_bytes_follow_the_program():
         assert (_stage_bytes(ctx, False), _stage_bytes(ctx, True)) == (48, 112)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("cap", ["c3", "c4", "fuzz", "edge"])
+def test_lean_staging_equals_full_prefixes(cap):
+    """Filter-only host batches stage bytes 12..43 of each frame (their descriptors point 12 B
+    before the staged bytes; frames of <= 12 B stage nothing). Decisions, verdicts and the pass
+    list equal the reference fixture and the 48-B staging kept for A/B (BT_OPT_NO_LEAN_HOST),
+    over every frame length the fixtures hold (the edge capture truncates every layer)."""
+    g, man = load_golden(cap)
+    filters = man["filter_sets"]["c3"]
+    lean, full = abi.Context(0, host_chunk_packets=4096), abi.Context(0, host_chunk_packets=4096,
+                                                                      flags=abi.OPT_NO_LEAN_HOST)
+    try:
+        outs = []
+        for ctx in (lean, full):
+            ctx.compile(filters)
+            outs.append(ctx.run_host(g["data"], g["desc"], records=False))
+        compare_decisions(outs[0]["decide"], g["code__c3"], g["src__c3"], filters, where=f"lean/{cap}")
+        for k in ("decide", "verdict", "pass_idx"):
+            assert np.array_equal(outs[0][k], outs[1][k]), f"{cap}: {k} differs between lean and 48-B staging"
+        lens = (g["desc"] >> 48).astype(np.int64)
+        assert (lens <= 12).any() or cap != "edge", "the edge capture should hold frames of <= 12 B"
+    finally:
+        lean.close()
+        full.close()

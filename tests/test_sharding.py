@@ -100,7 +100,7 @@ def test_native_split_cost_equals_shard_bounds(seed):
     from beatrice_amd import abi
     rng = np.random.default_rng(100 + seed)
     models = [shard.DEFAULT_COST] + [shard.group_cost(m, r, f, d, sb) for m in (False, True) for r in (False, True)
-                                     for f in (False, True) for d in (0, 8, 16) for sb in (48, 112, 176)]
+                                     for f in (False, True) for d in (0, 8, 16) for sb in (32, 48, 112, 176)]
     models += [(int(rng.integers(1, 300)), int(rng.choice([1, 4, 16, 64])), int(rng.integers(0, 200)))
                for _ in range(8)]
     for n in (0, 1, 64, 65, 4097, int(rng.integers(1, 200000))):
@@ -112,7 +112,7 @@ def test_native_split_cost_equals_shard_bounds(seed):
 
 
 def test_split_cost_balances_what_the_call_moves():
-    """A verdict-only host batch stages 48 B of each frame: with that model an IMIX batch's
+    """A verdict-only host batch stages 32 B of each frame: with that model an IMIX batch's
     members stage equal bytes, where the old 128 + 104 model over-weighted long frames."""
     _, desc = synth.capture(synth.C3, 200000)
     ln = synth.desc_len(desc)

@@ -9,6 +9,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from beatrice_amd import abi, synth  # noqa: E402
@@ -324,7 +326,13 @@ for mode in ("verdicts", "records+verdicts"):
         out = ctx.run_host(data, desc, records=rec, outs=houts)
         best = min(best, time.perf_counter() - t0)
     lens = synth.desc_len(desc)
-    h2d = float((((lens.clip(max=112) + 15) // 16) * 16).sum() + 8 * a.packets)
+    if rec:
+        staged = lens.clip(max=112)
+    elif a.flags & abi.OPT_NO_LEAN_HOST:
+        staged = lens.clip(max=48)
+    else:   # filter-only: frame bytes 12..43
+        staged = (lens.astype(np.int64) - 12).clip(min=0, max=32)
+    h2d = float((((staged + 15) // 16) * 16).sum() + 8 * a.packets)
     d2h = a.packets * (1 + 1 / 8 + (96 if rec else 0))
     print(json.dumps({"config": a.config, "flags": a.flags, "mode": mode, "packets": a.packets, "seconds": round(best, 4),
                       "mpps": round(a.packets / best / 1e6, 1), "h2d_GBps": round(h2d / best / 1e9, 2),

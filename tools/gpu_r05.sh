@@ -19,6 +19,8 @@
 #              (--hugepages) against 4-KiB pages, alternating, E2E_REPS pairs per config
 #   abn        timing only: the in-tree library and every build named in AB_NAMES
 #              (beatrice_amd/ab/<name>/), alternating processes, AB_REPS rounds of AB_CFGS
+#   e2e_envab  host-gather e2e (tools/e2e.py --data-node auto, E2E_ARGS appended) with and
+#              without AB_ENV, alternating processes, E2E_REPS rounds of E2E_CFGS
 #   envab      timing only: the in-tree library with and without AB_ENV (e.g. BT_XCD_ORDER=1),
 #              alternating processes, AB_REPS rounds of AB_CFGS, 50 steps each
 # Every GPU step runs under its own timeout; the first failure ends the call.
@@ -92,6 +94,18 @@ PY
             > "$OUT/abn_${cfg}_${v}_$r.json" 2> "$OUT/abn.err" || fail "abn $cfg $v" $? "$OUT/abn.err"
           python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline']; print(sys.argv[2], sys.argv[3], sys.argv[4], 'step', d['ms_per_step'], 'kern', r['kernel_ms'], 'frac', r['frac'])" \
             "$OUT/abn_${cfg}_${v}_$r.json" $r $cfg $v | tee -a "$OUT/abn.txt"
+        done
+      done
+    done ;;
+  e2e_envab)
+    for r in $(seq 1 ${E2E_REPS:-2}); do
+      for cfg in ${E2E_CFGS:-c2 c3 c4}; do
+        for v in base env; do
+          e=""; [ $v = env ] && e="${AB_ENV:?AB_ENV=NAME=VALUE}"
+          echo "{\"round\": $r, \"variant\": \"$v\"}" >> "$OUT/e2e_envab.jsonl"
+          env $e timeout -k 10 300 python tools/e2e.py --config $cfg --data-node auto --reps 5 ${E2E_ARGS:-} \
+            >> "$OUT/e2e_envab.jsonl" 2> "$OUT/e2e_envab.err" || fail "e2e $cfg $v" $? "$OUT/e2e_envab.err"
+          tail -1 "$OUT/e2e_envab.jsonl" | cut -c1-160
         done
       done
     done ;;
