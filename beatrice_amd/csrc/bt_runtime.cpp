@@ -1204,13 +1204,17 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
         if (next < n) {
             const uint32_t cnt = std::min(chunk, n - next);
             // gather the header prefixes (<= slot bytes) into pinned staging:
-            // per-worker byte counts, exclusive scan, then parallel copies
+            // per-worker byte counts, exclusive scan, then parallel copies (lean: every frame
+            // one 32-B slot, so worker w starts at pad + 32 * its first frame and the counting
+            // pass is skipped)
             uint8_t* pre = s.h_in;
             uint64_t* d = reinterpret_cast<uint64_t*>(s.h_in + (size_t)chunk * kHostSlotPayload);
             const unsigned T = pipeline_share(c);
             std::vector<uint64_t> part(T + 1, 0);
             const uint32_t base_i = next;
-            pipeline_run(c, cnt, T, [&](unsigned w) {
+            if (lean) {
+                for (unsigned w = 0; w <= T; ++w) part[w] = pad + (uint64_t)width * (uint32_t)((uint64_t)cnt * w / T);
+            } else pipeline_run(c, cnt, T, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t sum = 0;
                 for (uint32_t i = a; i < b; ++i) {
@@ -1220,8 +1224,8 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                 }
                 part[w + 1] = sum;
             });
-            part[0] = pad;
-            for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
+            if (!lean)
+                for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
             pipeline_run(c, cnt, T, [&](unsigned w) {
                 const uint32_t a = (uint32_t)((uint64_t)cnt * w / T), b = (uint32_t)((uint64_t)cnt * (w + 1) / T);
                 uint64_t p = part[w];
@@ -1237,7 +1241,7 @@ int host_pipeline_run(bt_ctx* c, uint32_t n, FrameFn frame, bt_rec* records, uin
                     const uint32_t m = std::min(len > lo ? len - lo : 0u, width);
                     if (m) stage_prefix(pre + p, f + lo, m, nt);
                     d[i] = BT_DESC(p - lo, len);
-                    p += (m + 15) & ~15u;
+                    p += lean ? width : (m + 15) & ~15u;
                 }
                 if (nt) __builtin_ia32_sfence();   // the prefixes are visible before the H2D copy
             });
