@@ -655,6 +655,9 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5, shared: bool =
                 out["c3_host_gather"] = {
                     "value": round(packets / hm / 1e6, 1), "best": round(packets / min(ht) / 1e6, 1),
                     "ms_per_call": round(hm * 1e3, 3), "decisions_match_zero_copy": bool(np.array_equal(h["decide"], dec[:packets])),
+                    # after the gathers: staging_node = where the members' pinned staging landed
+                    # (-1 in the zero-copy entries above, which stage nothing)
+                    "placement": [grp.placement(k) for k in range(n_dev)],
                     "workload": "C3 frames in ordinary host memory (each member's range on its device's NUMA node): "
                                 "each member gathers its range's 48-B prefixes on its NUMA-pinned host threads into "
                                 "pinned staging, H2D, kernels, decisions + verdicts + pass list back into output "
