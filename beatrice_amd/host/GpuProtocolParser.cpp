@@ -270,6 +270,52 @@ std::string GpuParsedBatch::format(uint32_t fmt) const {
     return format_recs(ctx_, recs_.data(), (uint32_t)recs_.size(), fmt);
 }
 
+GpuParsedBatch::~GpuParsedBatch() {
+    if (!store_) return;
+    detail::BatchStore& st = *store_;
+    std::lock_guard<std::mutex> lk(st.mu);   // the parser's destructor waits for this one
+    if (keep_.size() >= 65536 && st.ctx) {    // release the frames' references on the host threads
+        auto release = [](void* x, uint32_t w, uint32_t T) {
+            auto& k = *static_cast<detail::BatchStore::Keep*>(x);
+            for (size_t i = k.size() * w / T; i < k.size() * (w + 1) / T; ++i) k[i].reset();
+        };
+        if (bt_host_parallel(st.ctx, release, &keep_) != BT_OK) keep_.clear();
+    }
+    keep_.clear();
+    frames_.clear();
+    lens_.clear();
+    recs_.clear();
+    auto give = [](auto& pool, auto& v) {
+        if (v.capacity() && pool.size() < detail::BatchStore::kSets) pool.push_back(std::move(v));
+    };
+    give(st.recs, recs_);
+    give(st.frames, frames_);
+    give(st.lens, lens_);
+    give(st.keep, keep_);
+}
+
+namespace {
+// The largest array of `pool` for a batch about to be filled (empty if none).
+template <class V>
+V take_from(std::vector<V>& pool) {
+    if (pool.empty()) return V{};
+    auto it = std::max_element(pool.begin(), pool.end(),
+                               [](const V& a, const V& b) { return a.capacity() < b.capacity(); });
+    V v = std::move(*it);
+    pool.erase(it);
+    return v;
+}
+}  // namespace
+
+void GpuProtocolParser::newBatch(GpuParsedBatch& b) {
+    b.store_ = store_;
+    std::lock_guard<std::mutex> lk(store_->mu);
+    b.recs_ = take_from(store_->recs);
+    b.frames_ = take_from(store_->frames);
+    b.lens_ = take_from(store_->lens);
+    b.keep_ = take_from(store_->keep);
+}
+
 GpuProtocolParser::GpuProtocolParser(int device, const bt_opts* opts)
     : GpuProtocolParser(parser::ProtocolParser::ParserConfig{}, device, opts) {}
 
@@ -280,9 +326,16 @@ GpuProtocolParser::GpuProtocolParser(const parser::ProtocolParser::ParserConfig&
         throw std::runtime_error(std::string("GpuProtocolParser: ") + bt_last_error());
     if (config_.enablePerformanceMetrics) profiling_ = true;   // :31-35
     if (const char* e = std::getenv("BEATRICE_GPU_HOST_BELOW")) hostBelow_ = std::strtoull(e, nullptr, 10);
+    store_->ctx = ctx_;
 }
 
-GpuProtocolParser::~GpuProtocolParser() { bt_destroy(ctx_); }
+GpuProtocolParser::~GpuProtocolParser() {
+    {   // batches that outlive the parser release their references on their own thread
+        std::lock_guard<std::mutex> lk(store_->mu);
+        store_->ctx = nullptr;
+    }
+    bt_destroy(ctx_);
+}
 
 void GpuProtocolParser::run(GpuParsedBatch& b) {
     const uint32_t n = (uint32_t)b.frames_.size();
@@ -388,6 +441,7 @@ void GpuProtocolParser::adopt(bt_ctx* ctx, const std::vector<Packet>& packets, B
 
 GpuParsedBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets) {
     GpuParsedBatch b;
+    newBatch(b);
     adopt(ctx_, packets, b);
     run(b);
     return b;
@@ -395,9 +449,12 @@ GpuParsedBatch GpuProtocolParser::parseBatch(const std::vector<Packet>& packets)
 
 GpuParsedBatch GpuProtocolParser::parseBatch(const uint8_t* base, const bt_pkt_desc* desc, uint32_t n) {
     GpuParsedBatch b;
+    newBatch(b);
+    b.frames_.resize(n);
+    b.lens_.resize(n);
     for (uint32_t i = 0; i < n; ++i) {
-        b.frames_.push_back(base + BT_DESC_OFF(desc[i]));
-        b.lens_.push_back(BT_DESC_LEN(desc[i]));
+        b.frames_[i] = base + BT_DESC_OFF(desc[i]);
+        b.lens_[i] = BT_DESC_LEN(desc[i]);
     }
     run(b);
     return b;

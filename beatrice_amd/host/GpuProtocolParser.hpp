@@ -81,8 +81,34 @@ struct WalkedLayer {
     int tag;            // VLAN tag index (0/1), -1 otherwise
 };
 
+namespace detail {
+// What a destroyed GpuParsedBatch hands back to the parser that made it: its arrays, whose
+// pages are already in, for the next parseBatch (a fresh 96-B record per packet faulted in
+// during every call, and each packet's reference released on one thread at destruction, were
+// most of a large call's time); the references are released on the parser's host threads
+// while the parser lives (ctx is null once it is gone).
+struct BatchStore {
+    using Recs = std::vector<bt_rec, UninitAllocator<bt_rec>>;
+    using Keep = std::vector<std::shared_ptr<const uint8_t[]>>;
+    static constexpr size_t kSets = 2;   // sets of arrays kept for reuse
+    std::mutex mu;
+    bt_ctx* ctx = nullptr;
+    std::vector<Recs> recs;
+    std::vector<std::vector<const uint8_t*>> frames;
+    std::vector<std::vector<uint32_t>> lens;
+    std::vector<Keep> keep;
+};
+}  // namespace detail
+
 class GpuParsedBatch {
 public:
+    GpuParsedBatch() = default;
+    GpuParsedBatch(const GpuParsedBatch&) = default;
+    GpuParsedBatch(GpuParsedBatch&&) noexcept = default;
+    GpuParsedBatch& operator=(const GpuParsedBatch&) = default;
+    GpuParsedBatch& operator=(GpuParsedBatch&&) noexcept = default;
+    ~GpuParsedBatch();
+
     size_t size() const { return recs_.size(); }
     const bt_rec& record(size_t i) const { return recs_[i]; }
     std::vector<WalkedLayer> layers(size_t i) const;
@@ -111,6 +137,7 @@ private:
     std::vector<uint32_t> lens_;
     std::vector<std::shared_ptr<const uint8_t[]>> keep_;   // the frames of a vector<Packet> batch
     bt_ctx* ctx_ = nullptr;      // host pool for format(); owned by the GpuProtocolParser
+    std::shared_ptr<detail::BatchStore> store_;   // where the arrays go when the batch is destroyed
 };
 
 // One user protocol over a batch: the GPU's columns (status, extractValue<T> bits per
@@ -246,6 +273,7 @@ public:
 private:
     template <class Batch>
     static void adopt(bt_ctx* ctx, const std::vector<Packet>& packets, Batch& b);
+    void newBatch(GpuParsedBatch& b);   // arrays from the store, ready for reuse
     void run(GpuParsedBatch& b);
     void extract(GpuFieldBatch& b);
     using DefPtr = std::shared_ptr<const parser::ProtocolDefinition>;
@@ -255,6 +283,7 @@ private:
     std::vector<DefPtr> allProtocols() const;             // the reference's iteration order
     void countParses(const std::string& protocol, uint64_t ok, uint64_t bad, double us);
     bt_ctx* ctx_ = nullptr;
+    std::shared_ptr<detail::BatchStore> store_ = std::make_shared<detail::BatchStore>();
     size_t hostBelow_ = kHostBelowDefault;
     parser::ProtocolParser::ParserConfig config_;
     // as the reference's protocols_; each definition immutable and shared, so a call takes a

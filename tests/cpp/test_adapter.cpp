@@ -16,6 +16,7 @@
 //   plugin   dlopen of libgpu_parse_filter_plugin.so through createPlugin(), the
 //            IPacketPlugin lifecycle, pass count vs the reference.
 // Prints one line per check; exit status 0 = all passed.
+#include <optional>
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <signal.h>
@@ -374,7 +375,34 @@ static bool parser_case(const char* label, const Capture& cap) {
               (unsigned long)want.successfulParses, (unsigned long)got.successfulParses,
               (unsigned long)want.failedParses, (unsigned long)got.failedParses);
     }
-    std::printf("ok   parser  %-22s %zu packets, %zu layer results, detector, stats\n", label, cap.packets.size(), nlayers);
+    // GpuParsedBatch hands its arrays back to the parser when destroyed (and releases a large
+    // batch's packet references on the parser's host threads): batches made from recycled
+    // arrays hold the same records, at a size past the parallel-release threshold too, and a
+    // batch that outlives its parser stays readable
+    if (!cap.packets.empty()) {
+        std::vector<Packet> big;
+        while (big.size() < 70000) big.insert(big.end(), cap.packets.begin(), cap.packets.end());
+        auto same = [&](const beatrice::gpu::GpuParsedBatch& b, const std::vector<Packet>& pk) {
+            if (b.size() != pk.size()) return false;
+            for (size_t i = 0; i < b.size(); ++i)
+                if (std::memcmp(&b.record(i), &batch.record(i % cap.packets.size()), sizeof(bt_rec))) return false;
+            return true;
+        };
+        for (int r = 0; r < 3; ++r) {
+            auto b3 = gpu.parseBatch(r == 1 ? cap.packets : big);
+            CHECK(same(b3, r == 1 ? cap.packets : big), "%s: records from recycled arrays differ (round %d)", label, r);
+        }
+        std::optional<beatrice::gpu::GpuParsedBatch> late;
+        {
+            beatrice::gpu::GpuProtocolParser p2(0);
+            late = p2.parseBatch(big);
+            (void)p2.parseBatch(big);
+        }
+        CHECK(same(*late, big), "%s: a batch outliving its parser", label);
+        late.reset();
+    }
+    std::printf("ok   parser  %-22s %zu packets, %zu layer results, detector, stats, recycled arrays\n", label,
+                cap.packets.size(), nlayers);
     return true;
 }
 
