@@ -97,6 +97,12 @@ struct BatchStore {
     std::vector<std::vector<const uint8_t*>> frames;
     std::vector<std::vector<uint32_t>> lens;
     std::vector<Keep> keep;
+    BatchStore() {   // a destructor hands arrays back without allocating
+        recs.reserve(kSets);
+        frames.reserve(kSets);
+        lens.reserve(kSets);
+        keep.reserve(kSets);
+    }
 };
 }  // namespace detail
 
