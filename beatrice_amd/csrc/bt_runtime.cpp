@@ -1784,18 +1784,31 @@ int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, ui
         return BT_OK;   // image: n x span bytes the caller could not have allocated anyway
     }
     const uint32_t span = t.span;
-    std::lock_guard<std::mutex> lk(c->mu);
+    const WaitFor lk(c);
     HIP_TRY(hipSetDevice(c->device));
-    // chunks of at most 1M packets: [prefixes | descriptors] in, [status | values | image] out
+    (void)pool_of(c);
+    // chunks of at most 1M packets: [prefixes | descriptors] in, [status | values | image] out.
+    // The gather and the drain run on the context's host threads (a serial gather, length
+    // check and drain were most of a 1M-packet call). Tables up to 256 B give every frame one
+    // slot of round_up(span, 16) bytes, so the gather needs no prefix pass; wider ones pack
+    // each frame's round_up(min(len, span), 16) bytes after a per-worker count and scan.
     const uint32_t chunk = 1u << 20;
+    const size_t slot = ((size_t)span + 15u) & ~(size_t)15u;
+    const bool fixed = slot <= 256;
     for (uint32_t lo = 0; lo < n; lo += chunk) {
         const uint32_t m = std::min(chunk, n - lo);
-        std::vector<uint64_t> pos(m + 1, 0);
-        for (uint32_t i = 0; i < m; ++i) {
-            if (lens[lo + i] > 0xFFFFu) return fail(BT_E_INVALID_ARGUMENT, "frame %u longer than 65535 bytes", lo + i);
-            pos[i + 1] = pos[i] + ((std::min(lens[lo + i], span) + 15u) & ~15u);
+        const unsigned T = pipeline_share(c);
+        std::vector<uint64_t> part(T + 1, 0);   // packed: each worker's first staging byte
+        if (!fixed) {
+            pipeline_run(c, m, T, [&](unsigned w) {
+                const uint32_t a = (uint32_t)((uint64_t)m * w / T), e = (uint32_t)((uint64_t)m * (w + 1) / T);
+                uint64_t sum = 0;
+                for (uint32_t i = a; i < e; ++i) sum += (std::min(lens[lo + i], span) + 15u) & ~15u;
+                part[w + 1] = sum;
+            });
+            for (unsigned w = 0; w < T; ++w) part[w + 1] += part[w];
         }
-        const size_t pre = pos[m] + 16, dsc = (size_t)m * 8;
+        const size_t pre = (fixed ? (size_t)m * slot : part[T]) + 16, dsc = (size_t)m * 8;
         const size_t st_b = ((size_t)m + 15) & ~(size_t)15, val_b = (size_t)n_fields * m * 8, img_b = (size_t)m * span;
         const size_t in_b = pre + dsc, out_b = st_b + val_b + img_b;
         const size_t need = in_b + out_b + 64;
@@ -1812,11 +1825,21 @@ int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, ui
         }
         uint8_t* h = c->ex_h;
         uint64_t* d = reinterpret_cast<uint64_t*>(h + pre);
-        for (uint32_t i = 0; i < m; ++i) {   // only [0, span) of a frame is ever read
-            const uint32_t k = std::min(lens[lo + i], span);
-            if (k) std::memcpy(h + pos[i], frames[lo + i], k);
-            d[i] = BT_DESC(pos[i], lens[lo + i]);
-        }
+        std::vector<uint32_t> bad(T, UINT32_MAX);   // per worker: first frame longer than 65535 B
+        pipeline_run(c, m, T, [&](unsigned w) {
+            const uint32_t a = (uint32_t)((uint64_t)m * w / T), e = (uint32_t)((uint64_t)m * (w + 1) / T);
+            uint64_t p = fixed ? (uint64_t)a * slot : part[w];
+            for (uint32_t i = a; i < e; ++i) {   // only [0, span) of a frame is ever read
+                const uint32_t len = lens[lo + i];
+                const uint32_t k = std::min(len, span);
+                if (len > 0xFFFFu) bad[w] = std::min(bad[w], lo + i);
+                else if (k) std::memcpy(h + p, frames[lo + i], k);
+                d[i] = BT_DESC(p, len & 0xFFFFu);
+                p += fixed ? slot : (k + 15u) & ~15u;
+            }
+        });
+        const uint32_t first_bad = *std::min_element(bad.begin(), bad.end());
+        if (first_bad != UINT32_MAX) return fail(BT_E_INVALID_ARGUMENT, "frame %u longer than 65535 bytes", first_bad);
         HIP_TRY(hipMemcpyAsync(c->ex_d, h, in_b, hipMemcpyHostToDevice, c->stream));
         bt_batch b{};
         b.base = c->ex_d;
@@ -1834,10 +1857,15 @@ int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, ui
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(hout, dout, out_b, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (status) std::memcpy(status + lo, hout, m);
-        for (uint32_t k = 0; values && k < n_fields; ++k)
-            std::memcpy(values + (size_t)k * n + lo, hout + st_b + (size_t)k * m * 8, (size_t)m * 8);
-        if (image && span) std::memcpy(image + (size_t)lo * span, hout + st_b + val_b, img_b);
+        pipeline_run(c, m, T, [&](unsigned w) {
+            const uint32_t a = (uint32_t)((uint64_t)m * w / T), e = (uint32_t)((uint64_t)m * (w + 1) / T);
+            if (a >= e) return;
+            if (status) std::memcpy(status + lo + a, hout + a, e - a);
+            for (uint32_t k = 0; values && k < n_fields; ++k)
+                std::memcpy(values + (size_t)k * n + lo + a, hout + st_b + ((size_t)k * m + a) * 8, (size_t)(e - a) * 8);
+            if (image && span) std::memcpy(image + ((size_t)lo + a) * span, hout + st_b + val_b + (size_t)a * span,
+                                           (size_t)(e - a) * span);
+        });
     }
     return BT_OK;
 }

@@ -270,28 +270,44 @@ std::string GpuParsedBatch::format(uint32_t fmt) const {
     return format_recs(ctx_, recs_.data(), (uint32_t)recs_.size(), fmt);
 }
 
+void detail::BatchStore::give(std::vector<const uint8_t*>& f, std::vector<uint32_t>& l, Keep& k) {
+    // under mu (the caller's lock); the parser's destructor waits for it
+    if (k.size() >= 65536 && ctx) {   // release the frames' references on the host threads
+        auto release = [](void* x, uint32_t w, uint32_t T) {
+            auto& v = *static_cast<Keep*>(x);
+            for (size_t i = v.size() * w / T; i < v.size() * (w + 1) / T; ++i) v[i].reset();
+        };
+        if (bt_host_parallel(ctx, release, &k) != BT_OK) k.clear();
+    }
+    k.clear();
+    f.clear();
+    l.clear();
+    auto keep_for_reuse = [](auto& pool, auto& v, size_t cap) {
+        if (v.capacity() && pool.size() < cap) pool.push_back(std::move(v));
+    };
+    keep_for_reuse(frames, f, kSets);
+    keep_for_reuse(lens, l, kSets);
+    keep_for_reuse(keep, k, kSets);
+}
+
 GpuParsedBatch::~GpuParsedBatch() {
     if (!store_) return;
-    detail::BatchStore& st = *store_;
-    std::lock_guard<std::mutex> lk(st.mu);   // the parser's destructor waits for this one
-    if (keep_.size() >= 65536 && st.ctx) {    // release the frames' references on the host threads
-        auto release = [](void* x, uint32_t w, uint32_t T) {
-            auto& k = *static_cast<detail::BatchStore::Keep*>(x);
-            for (size_t i = k.size() * w / T; i < k.size() * (w + 1) / T; ++i) k[i].reset();
-        };
-        if (bt_host_parallel(st.ctx, release, &keep_) != BT_OK) keep_.clear();
-    }
-    keep_.clear();
-    frames_.clear();
-    lens_.clear();
+    std::lock_guard<std::mutex> lk(store_->mu);
+    store_->give(frames_, lens_, keep_);
     recs_.clear();
-    auto give = [](auto& pool, auto& v) {
-        if (v.capacity() && pool.size() < detail::BatchStore::kSets) pool.push_back(std::move(v));
-    };
-    give(st.recs, recs_);
-    give(st.frames, frames_);
-    give(st.lens, lens_);
-    give(st.keep, keep_);
+    if (recs_.capacity() && store_->recs.size() < detail::BatchStore::kSets) store_->recs.push_back(std::move(recs_));
+}
+
+GpuFieldBatch::~GpuFieldBatch() {
+    if (!store_) return;
+    std::lock_guard<std::mutex> lk(store_->mu);
+    store_->give(frames_, lens_, keep_);
+    for (auto* v : {&status_, &image_}) {
+        v->clear();
+        if (v->capacity() && store_->bytes.size() < 2 * detail::BatchStore::kSets) store_->bytes.push_back(std::move(*v));
+    }
+    values_.clear();
+    if (values_.capacity() && store_->words.size() < detail::BatchStore::kSets) store_->words.push_back(std::move(values_));
 }
 
 namespace {
@@ -311,6 +327,17 @@ void GpuProtocolParser::newBatch(GpuParsedBatch& b) {
     b.store_ = store_;
     std::lock_guard<std::mutex> lk(store_->mu);
     b.recs_ = take_from(store_->recs);
+    b.frames_ = take_from(store_->frames);
+    b.lens_ = take_from(store_->lens);
+    b.keep_ = take_from(store_->keep);
+}
+
+void GpuProtocolParser::newBatch(GpuFieldBatch& b) {
+    b.store_ = store_;
+    std::lock_guard<std::mutex> lk(store_->mu);
+    b.image_ = take_from(store_->bytes);   // the larger byte column first
+    b.status_ = take_from(store_->bytes);
+    b.values_ = take_from(store_->words);
     b.frames_ = take_from(store_->frames);
     b.lens_ = take_from(store_->lens);
     b.keep_ = take_from(store_->keep);
@@ -807,13 +834,20 @@ void GpuProtocolParser::extract(GpuFieldBatch& b) {
     const uint32_t n = (uint32_t)b.frames_.size();
     b.span_ = span > 0xFFFFu ? 0 : span;
     b.validate_ = config_.enableValidation;
-    b.status_.assign(n, 0);
-    b.values_.assign((size_t)table.size() * n, 0);
-    b.image_.assign((size_t)n * b.span_, 0);
+    // bt_extract writes every status, value and image byte; bt_extract_host gets zeroed columns
+    const bool on_host = n && n < hostBelow_;
+    b.status_.resize(n);
+    b.values_.resize((size_t)table.size() * n);
+    b.image_.resize((size_t)n * b.span_);
+    if (on_host) {
+        std::fill(b.status_.begin(), b.status_.end(), 0);
+        std::fill(b.values_.begin(), b.values_.end(), 0);
+        std::fill(b.image_.begin(), b.image_.end(), 0);
+    }
     const auto t0 = std::chrono::steady_clock::now();
     // a small batch (parsePacket's one packet) on this thread: the device's round trip costs more
     int rc = BT_OK;
-    if (n && n < hostBelow_)
+    if (on_host)
         rc = bt_extract_host(b.frames_.data(), b.lens_.data(), n, table.data(), (uint32_t)table.size(), b.status_.data(),
                              table.empty() ? nullptr : b.values_.data(), b.span_ ? b.image_.data() : nullptr);
     else if (n)
@@ -874,6 +908,7 @@ std::vector<GpuProtocolParser::DefPtr> GpuProtocolParser::allProtocols() const {
 
 GpuFieldBatch GpuProtocolParser::batchOf(const std::vector<Packet>& packets, DefPtr def) {
     GpuFieldBatch b;
+    newBatch(b);
     b.def_ = std::move(def);
     adopt(ctx_, packets, b);
     extract(b);

@@ -89,6 +89,8 @@ namespace detail {
 // while the parser lives (ctx is null once it is gone).
 struct BatchStore {
     using Recs = std::vector<bt_rec, UninitAllocator<bt_rec>>;
+    using Bytes = std::vector<uint8_t, UninitAllocator<uint8_t>>;
+    using Words = std::vector<uint64_t, UninitAllocator<uint64_t>>;
     using Keep = std::vector<std::shared_ptr<const uint8_t[]>>;
     static constexpr size_t kSets = 2;   // sets of arrays kept for reuse
     std::mutex mu;
@@ -97,12 +99,19 @@ struct BatchStore {
     std::vector<std::vector<const uint8_t*>> frames;
     std::vector<std::vector<uint32_t>> lens;
     std::vector<Keep> keep;
+    std::vector<Bytes> bytes;   // a field batch's status and image columns
+    std::vector<Words> words;   // its value columns
     BatchStore() {   // a destructor hands arrays back without allocating
         recs.reserve(kSets);
         frames.reserve(kSets);
         lens.reserve(kSets);
         keep.reserve(kSets);
+        bytes.reserve(2 * kSets);
+        words.reserve(kSets);
     }
+    // A destroyed batch's arrays: the frames' references released (on the parser's host
+    // threads for a large batch while the parser lives), the arrays kept for reuse.
+    void give(std::vector<const uint8_t*>& f, std::vector<uint32_t>& l, Keep& k);
 };
 }  // namespace detail
 
@@ -150,6 +159,13 @@ private:
 // numeric field, the [0, span) bytes of each packet) and ParseResult on demand.
 class GpuFieldBatch {
 public:
+    GpuFieldBatch() = default;
+    GpuFieldBatch(const GpuFieldBatch&) = default;
+    GpuFieldBatch(GpuFieldBatch&&) noexcept = default;
+    GpuFieldBatch& operator=(const GpuFieldBatch&) = default;
+    GpuFieldBatch& operator=(GpuFieldBatch&&) noexcept = default;
+    ~GpuFieldBatch();
+
     size_t size() const { return lens_.size(); }
     const parser::ProtocolDefinition& protocol() const {
         static const parser::ProtocolDefinition kNone{};   // a default-constructed batch
@@ -176,12 +192,13 @@ private:
     std::shared_ptr<const parser::ProtocolDefinition> def_;   // the registered definition, shared
     bool validate_ = true;
     uint64_t span_ = 0;
-    std::vector<uint8_t> status_;
-    std::vector<uint64_t> values_;     // field-major, column stride size()
-    std::vector<uint8_t> image_;       // size() x span_
+    detail::BatchStore::Bytes status_;
+    detail::BatchStore::Words values_;   // field-major, column stride size()
+    detail::BatchStore::Bytes image_;    // size() x span_
     std::vector<const uint8_t*> frames_;
     std::vector<uint32_t> lens_;
     std::vector<std::shared_ptr<const uint8_t[]>> keep_;
+    std::shared_ptr<detail::BatchStore> store_;   // where the arrays go when the batch is destroyed
 };
 
 class GpuProtocolParser {
@@ -280,6 +297,7 @@ private:
     template <class Batch>
     static void adopt(bt_ctx* ctx, const std::vector<Packet>& packets, Batch& b);
     void newBatch(GpuParsedBatch& b);   // arrays from the store, ready for reuse
+    void newBatch(GpuFieldBatch& b);
     void run(GpuParsedBatch& b);
     void extract(GpuFieldBatch& b);
     using DefPtr = std::shared_ptr<const parser::ProtocolDefinition>;

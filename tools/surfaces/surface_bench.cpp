@@ -2,7 +2,7 @@
 // to the reference's own PacketFilter on the same host CPUs (VERDICT r02 "time what an
 // integrator calls").
 //
-//   surface_bench [all|filter|ref|mt|parser|sizes|single|group|plugin|plugin-hot] [--packets N] [--seconds S] [--threads T]
+//   surface_bench [all|filter|ref|mt|parser|usertable|sizes|single|group|plugin|plugin-hot] [--packets N] [--seconds S] [--threads T]
 //                 [--plugin SO] [--chunks 16384,65536] [--members 1,2,4] [--data-node none|auto|N]
 //
 // For C2 (64-B Eth/IPv4/UDP) and C3 (IMIX) frames held as std::vector<beatrice::Packet>
@@ -19,6 +19,8 @@
 //             on its own shard in chunks (the reference's pattern above, one instance);
 //   parser    ProtocolParser::parsePacket per walked layer against GpuProtocolParser::parseBatch
 //             (records, ParseResults on demand, JSON text): bench_parser below;
+//   usertable parser_example's user protocol table (BASELINE configs[0]) over the C2 frames:
+//             parsePacket(frame, definition) against parseBatch(packets, definition);
 //   single    one packet per call (applyFilters(const Packet&), parsePacket(slice, name)) and small
 //             classify() batches, host branch against device branch: bench_single below;
 //   group     one GpuPacketFilter over a device group of 1 / 2 / 4 members: bench_group below;
@@ -396,6 +398,85 @@ void bench_parser(const Capture& c, int threads, double seconds) {
     timed("GpuProtocolParser::parseBatch + format(BT_FMT_JSON) of the batch", 2);
 }
 
+// BASELINE configs[0]'s path through the C++ API: parser_example's CUSTOM_PROTO table
+// (examples/parser_example.cpp:18-22: header u32 @0, version u8 @4, length u16 @5, data
+// BYTES[10] @7) over every frame. The reference: ProtocolParser::parsePacket(frame, definition)
+// per packet on T threads, a parser each (metrics off, as oracle/ref_harness.cpp); against it
+// GpuProtocolParser::parseBatch(packets, definition) (the GPU's status / value / byte columns),
+// alone and with result(i) — the reference's ParseResult — for every packet on T threads.
+void bench_usertable(const Capture& c, int threads, double seconds) {
+    using namespace beatrice::parser;
+    ProtocolDefinition def("CUSTOM_PROTO", "1.0");
+    def.addField(FieldFactory::createUInt32Field("header", 0, Endianness::NETWORK, true, "Protocol header"));
+    def.addField(FieldFactory::createUInt8Field("version", 4, true, "Protocol version"));
+    def.addField(FieldFactory::createUInt16Field("length", 5, Endianness::NETWORK, true, "Data length"));
+    def.addField(FieldFactory::createBytesField("data", 7, 10, "Payload data"));
+    const size_t n = std::min<size_t>(c.packets.size(), 1u << 20);
+    const std::vector<Packet> pk(c.packets.begin(), c.packets.begin() + n);
+    {
+        std::atomic<uint64_t> done{0};
+        std::atomic<bool> stop{false};
+        std::vector<std::thread> th;
+        const auto t0 = Clock::now();
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                ProtocolParser::ParserConfig cfg;
+                cfg.enablePerformanceMetrics = false;
+                ProtocolParser rp(cfg);
+                const size_t lo = n * t / threads, hi = n * (t + 1) / threads;
+                uint64_t mine = 0;
+                for (size_t i = lo; !stop.load(std::memory_order_relaxed); i = i + 1 < hi ? i + 1 : lo) {
+                    const std::vector<uint8_t> frame(pk[i].data(), pk[i].data() + pk[i].length());
+                    const ParseResult r = rp.parsePacket(frame, def);
+                    (void)r;
+                    ++mine;
+                    if (t == 0 && (mine & 1023) == 0 && secs(t0, Clock::now()) > seconds) stop = true;
+                }
+                done += mine;
+            });
+        for (auto& x : th) x.join();
+        const double el = secs(t0, Clock::now());
+        char extra[64];
+        std::snprintf(extra, sizeof(extra), "\"seconds\": %.3f", el);
+        line("ref ProtocolParser::parsePacket(frame, CUSTOM_PROTO definition)", c, threads, done / el, extra);
+    }
+    ProtocolParser::ParserConfig cfg;
+    cfg.enablePerformanceMetrics = false;
+    beatrice::gpu::GpuProtocolParser gp(cfg, 0);
+    (void)gp.parseBatch(pk, def);   // warm-up
+    for (int mode = 0; mode < 2; ++mode) {
+        uint64_t done = 0;
+        double dev_s = 0, post_s = 0;
+        const auto t0 = Clock::now();
+        while (secs(t0, Clock::now()) < seconds) {
+            const auto a = Clock::now();
+            const auto b = gp.parseBatch(pk, def);
+            const auto m = Clock::now();
+            if (mode == 1) {
+                std::vector<std::thread> th;
+                for (int t = 0; t < threads; ++t)
+                    th.emplace_back([&, t] {
+                        for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+                            const ParseResult r = b.result(i);
+                            (void)r;
+                        }
+                    });
+                for (auto& x : th) x.join();
+            }
+            dev_s += secs(a, m);
+            post_s += secs(m, Clock::now());
+            done += n;
+        }
+        const double el = secs(t0, Clock::now());
+        char extra[160];
+        std::snprintf(extra, sizeof(extra), "\"parse_batch_s\": %.4f, \"host_post_s\": %.4f, \"seconds\": %.3f", dev_s,
+                      post_s, el);
+        line(mode ? "GpuProtocolParser::parseBatch(packets, CUSTOM_PROTO) + result(i) ParseResult for every packet"
+                  : "GpuProtocolParser::parseBatch(packets, CUSTOM_PROTO) -> status / value / byte columns",
+             c, mode ? threads : 0, done / el, extra);
+    }
+}
+
 // Single-packet calls and small batches (VERDICT r03 "stop charging single-packet callers a
 // device round trip"): the reference's per-packet entries on one thread against the drop-in's
 // host branch (the compiled program / extractor on the calling thread) and its device branch
@@ -711,6 +792,7 @@ int main(int argc, char** argv) {
             }
         }
         if (what == "all" || what == "parser") bench_parser(c, threads, seconds);
+        if ((what == "all" || what == "usertable") && c.name == std::string("c2")) bench_usertable(c, threads, seconds);
         if (what == "all" || what == "sizes") bench_call_sizes(c, seconds);
         if (what == "all" || what == "single") bench_single(c, seconds);
         if (what == "all" || what == "group") bench_group(c, threads, seconds, members);
