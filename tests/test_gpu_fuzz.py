@@ -48,14 +48,50 @@ def _check(out, dec, n, npass, where):
         assert out["n_pass"] == npass == len(exp) and np.array_equal(out["pass_idx"], exp), f"{where}: pass list"
 
 
-def _mapped(grp, data, desc, n, records):
+class Arena:
+    """A group's registered host buffers, registered once for the whole sweep (as a
+    deployment registers its UMEM or ring once) and refilled every round: the capture is copied
+    in, the outputs are poisoned (0xFF) so that a byte the device did not write shows up.
+    BT_FUZZ_REGISTER_EACH=1 instead registers and unregisters each round's own arrays (the
+    round-5 sweeps' form; see DESIGN.md §5 for the one difference it showed)."""
+    DATA = 128 << 20
+    N = 70000
+
+    def __init__(self, grp):
+        self.grp = grp
+        tiles = (self.N + 63) // 64
+        self.data = np.zeros(self.DATA, np.uint8)
+        self.desc = np.zeros(self.N, np.uint64)
+        self.rec = np.zeros(tiles * 6144, np.uint8)
+        self.dec = np.zeros(tiles * 64, np.uint8)
+        self.ver = np.zeros(tiles, np.uint64)
+        self.held = [self.data, self.desc, self.rec, self.dec, self.ver]
+        for a in self.held:
+            grp.register(a)
+
+    def close(self):
+        for a in self.held:
+            self.grp.unregister(a)
+
+
+def _mapped(grp, data, desc, n, records, arena=None):
     tiles = max(1, (n + 63) // 64)
-    h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64)
     pidx = np.zeros(max(n, 1), np.uint32)
     npass = np.zeros(1, np.uint32)
-    held = [a for a in (data, desc, h_rec, h_dec, h_ver) if a is not None]
+    if arena is not None and data.nbytes <= Arena.DATA and n <= Arena.N:
+        arena.data[:data.nbytes] = data
+        arena.desc[:n] = desc[:n]
+        arena.dec.fill(0xFF)
+        arena.ver.fill(0xFFFFFFFFFFFFFFFF)
+        data, desc = arena.data[:data.nbytes], arena.desc
+        h_rec = arena.rec[:tiles * 6144] if records else None
+        h_dec, h_ver = arena.dec[:tiles * 64], arena.ver[:tiles]
+        held = []
+    else:
+        h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
+        h_dec = np.zeros(tiles * 64, np.uint8)
+        h_ver = np.zeros(tiles, np.uint64)
+        held = [a for a in (data, desc, h_rec, h_dec, h_ver) if a is not None]
     for a in held:
         grp.register(a)
     try:
@@ -65,8 +101,16 @@ def _mapped(grp, data, desc, n, records):
     finally:
         for a in held:
             grp.unregister(a)
-    return {"decide": h_dec[:n], "verdict": h_ver, "pass_idx": pidx[:int(npass[0])], "n_pass": int(npass[0]),
-            "records": abi.untile_records(h_rec, n) if records else None}
+    return {"decide": h_dec[:n].copy(), "verdict": h_ver.copy(), "pass_idx": pidx[:int(npass[0])],
+            "n_pass": int(npass[0]), "records": abi.untile_records(h_rec, n) if records else None}
+
+
+def _arena(arenas, key, grp):
+    if os.environ.get("BT_FUZZ_REGISTER_EACH", "0") not in ("", "0"):
+        return None
+    if key not in arenas:
+        arenas[key] = Arena(grp)
+    return arenas[key]
 
 
 def test_randomized_parity_sweep():
@@ -76,6 +120,7 @@ def test_randomized_parity_sweep():
     print(f"fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
     ctx = abi.Context(0)
     groups = {}
+    arenas = {}
     t_end = time.time() + seconds
     rounds = 0
     try:
@@ -116,7 +161,8 @@ def test_randomized_parity_sweep():
                     groups[m] = abi.Group([0] * m, flags=abi.OPT_GROUP_SHARED_DEVICE if m > 1 else 0)
                 grp = groups[m]
                 grp.compile(prog)
-                out = _mapped(grp, data, desc, n, records) if form == "mapped" else grp.run_host(data, desc, records=records)
+                out = (_mapped(grp, data, desc, n, records, _arena(arenas, m, grp)) if form == "mapped"
+                       else grp.run_host(data, desc, records=records))
             _check(out, dec, n, npass, where)
             if records:
                 bad = np.nonzero((out["records"][:n] != rec).any(axis=1))[0]
@@ -124,6 +170,8 @@ def test_randomized_parity_sweep():
             rounds += 1
             print(f"ok round {rounds} {form} cfg {cfg} n {n} filters {len(prog)} records {records}", flush=True)
     finally:
+        for a in arenas.values():
+            a.close()
         for g in groups.values():
             g.close()
         ctx.close()
@@ -146,6 +194,7 @@ def test_randomized_payload_programs_vs_reference():
     print(f"payload fuzz seed {seed0:#x}, {seconds:.0f} s", flush=True)
     ctx = abi.Context(0)
     grp = abi.Group([0, 0], flags=abi.OPT_GROUP_SHARED_DEVICE)
+    arenas = {}
     t_end = time.time() + seconds
     rounds = 0
     try:
@@ -164,7 +213,7 @@ def test_randomized_payload_programs_vs_reference():
             where = f"payload round {rounds} form {form} cfg {cfg} n {n} program {prog}"
             if form == "mapped":
                 grp.compile(prog)
-                out = _mapped(grp, data, desc, n, False)
+                out = _mapped(grp, data, desc, n, False, _arena(arenas, 2, grp))
             else:
                 ctx.compile(prog)
                 if form == "host":
@@ -179,5 +228,7 @@ def test_randomized_payload_programs_vs_reference():
             rounds += 1
             print(f"ok payload round {rounds} {form} cfg {cfg} n {n} filters {len(prog)}", flush=True)
     finally:
+        for a in arenas.values():
+            a.close()
         grp.close()
         ctx.close()
