@@ -407,7 +407,9 @@ int  bt_parse_filter_device_async(bt_ctx* ctx, const bt_batch* batch, const bt_o
 
 /* Host batch: borrows base/desc for the call, copies through pinned staging in
  * chunks (H2D, kernels, D2H double-buffered on two streams), fills host outputs,
- * returns when done. Output pointers are host memory (records in bt_rec AoS). */
+ * returns when done. Output pointers are host memory (records in bt_rec AoS). Records
+ * that lie inside a range registered with bt_host_register on this context are written
+ * in place by the D2H copies (no pass through the staging). */
 int  bt_parse_filter(bt_ctx* ctx, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n,
                      bt_rec* records, uint64_t* verdict, uint8_t* decide,
                      uint32_t* pass_idx, uint32_t* n_pass);

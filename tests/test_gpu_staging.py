@@ -103,3 +103,40 @@ def test_lean_staging_equals_full_prefixes(cap):
     finally:
         lean.close()
         full.close()
+
+
+@pytest.mark.parametrize("cap", ["c3", "c4", "edge"])
+@pytest.mark.parametrize("records", [False, True])
+def test_registered_outputs_are_written_in_place(cap, records):
+    """Host batch outputs inside a range registered with bt_host_register are copied D2H in
+    place (no staging drain); the results equal the reference fixture and the staged form, also
+    with several chunks (host_chunk_packets 1024) and with only some outputs registered."""
+    g, man = load_golden(cap)
+    filters = man["filter_sets"]["c3"]
+    n = len(g["desc"])
+    ctx = abi.Context(0, host_chunk_packets=1024)
+    try:
+        ctx.compile(filters)
+        want = ctx.run_host(g["data"], g["desc"], records=records)
+        def own_pages(a):   # each array on pages of its own (registrations may not share a page)
+            import mmap
+            m = mmap.mmap(-1, (a.nbytes + 4095) // 4096 * 4096 or 4096)
+            return np.frombuffer(m, a.dtype, count=a.size).reshape(a.shape)
+
+        for which in (("records", "decide", "verdict"), ("decide",), ("verdict",)):
+            outs = {k: None if v is None else own_pages(v) for k, v in abi.host_outputs(n, records=records).items()}
+            regs = [outs[k] for k in which if outs.get(k) is not None]
+            for a in regs:
+                ctx.register(a)
+            try:
+                got = ctx.run_host(g["data"], g["desc"], records=records, outs=outs)
+            finally:
+                for a in regs:
+                    ctx.unregister(a)
+            compare_decisions(got["decide"], g["code__c3"], g["src__c3"], filters, where=f"registered {which}/{cap}")
+            for k in ("decide", "verdict", "pass_idx"):
+                assert np.array_equal(got[k], want[k]), f"{cap} {which}: {k} differs from the staged form"
+            if records:
+                assert np.array_equal(got["records"], want["records"]), f"{cap} {which}: records differ"
+    finally:
+        ctx.close()
