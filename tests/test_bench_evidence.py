@@ -229,7 +229,7 @@ def test_group_ingest_entry():
         assert "skipped" in r["configs"]["zero_copy_group"]
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_r05_lines_carry_cpu_baseline_and_aggregate_roofline_at_every_n(n):
     """Round 5's rule: at every GPU count the line carries the reference CPU
     baseline, timed on rank 0 in the same run, and the roofline over all N devices."""
@@ -281,3 +281,11 @@ def test_r03_rank_lines_come_from_the_self_spawning_launcher():
         c = d["config"]
         assert c["rehearsal_one_device"] is True and c["devices_distinct"] == 1   # distinct devices used
         assert len(c["pci_bus_ids"]) == n and len(set(c["pci_bus_ids"])) == 1
+
+
+def test_r05_rank_lines_are_alone_on_stdout_after_the_gloo_change():
+    """The 8-rank rehearsal ran after bench.py moved gloo's connection lines to stderr: its
+    stdout (the committed file) is the JSON line alone, as the driver reads it."""
+    with open(os.path.join(ROOT, "profiles", "r05", "bench_8rank_one_gpu.json")) as fh:
+        lines = [x for x in fh.read().splitlines() if x.strip()]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 8
