@@ -174,6 +174,7 @@ EXPORTS = [
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records", "bt_format_records_to",
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3", "bt_ring_gather_dense_tpv3",
+    "bt_ring_gather_lean_tpv3",
     "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
     "bt_group_split_cost", "bt_group_cost", "bt_group_thread_budget", "bt_group_host_register",
@@ -249,6 +250,8 @@ def lib() -> ctypes.CDLL:
         "bt_ring_gather_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, u32,
                                                ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_ring_gather_dense_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, vp, u32,
+                                                     ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+        "bt_ring_gather_lean_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, vp, u32,
                                                      ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
@@ -729,29 +732,33 @@ def ring_walk_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, first: int 
 
 PREFIX_SLOT = 128
 BATCH_PREFIXES = 0x1
+BATCH_LEAN = 0x2
 
 
 def ring_gather_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, slots: np.ndarray, out: np.ndarray,
                      first: int = 0, max_blocks: int | None = None, ctx: "Context | None" = None,
-                     slot_base: int = 0, dense: bool = False, ring_out: np.ndarray | None = None):
+                     slot_base: int = 0, dense: bool = False, ring_out: np.ndarray | None = None,
+                     lean: bool = False):
     """bt_ring_gather_tpv3: the walk of ring_walk_tpv3, plus every frame's header prefix
     copied into slots[(slot_base + i) * PREFIX_SLOT ...]; descriptors (written to
     out[slot_base:]) point into `slots`. dense=True: bt_ring_gather_dense_tpv3 (each block's
     prefixes back to back from its first slot; ring_out[slot_base:] gets the ring descriptors).
-    Returns (desc view, blocks taken)."""
+    lean=True: bt_ring_gather_lean_tpv3 (filter-only: each frame's bytes 12..43, packed after a
+    16-B pad; run the batch with BATCH_PREFIXES | BATCH_LEAN). Returns (desc view, blocks taken)."""
     if slots.dtype != np.uint8 or not slots.flags.c_contiguous or out.dtype != np.uint64:
         raise ValueError("slots must be contiguous uint8, out uint64")
-    if ring_out is not None and (not dense or ring_out.dtype != np.uint64 or len(ring_out) < len(out)):
-        raise ValueError("ring_out: uint64, as long as out, dense gather only")
+    if ring_out is not None and (not (dense or lean) or ring_out.dtype != np.uint64 or len(ring_out) < len(out)):
+        raise ValueError("ring_out: uint64, as long as out, dense or lean gather only")
     cap = min(len(out) - slot_base, len(slots) // PREFIX_SLOT - slot_base)
     r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
     nd, nb = ctypes.c_uint32(), ctypes.c_uint32()
     args = (ctx.h if ctx else None, ctypes.byref(r), first, n_blocks if max_blocks is None else max_blocks,
             slots.ctypes.data + slot_base * PREFIX_SLOT, out.ctypes.data + 8 * slot_base)
     tail = (cap, ctypes.byref(nd), ctypes.byref(nb))
-    if dense:
+    if dense or lean:
         rd = None if ring_out is None else ring_out.ctypes.data + 8 * slot_base
-        _check(lib().bt_ring_gather_dense_tpv3(*args, rd, *tail))
+        fn = lib().bt_ring_gather_lean_tpv3 if lean else lib().bt_ring_gather_dense_tpv3
+        _check(fn(*args, rd, *tail))
     else:
         _check(lib().bt_ring_gather_tpv3(*args, *tail))
     return out[slot_base:slot_base + nd.value], nb.value

@@ -69,7 +69,14 @@ struct Chain {
 };
 
 // What the walk does with each frame besides its descriptor.
-enum WalkMode { kWalkOnly, kGatherSlots, kGatherDense };
+enum WalkMode { kWalkOnly, kGatherSlots, kGatherDense, kGatherLean };
+
+// Lean gather (filter-only batches): each frame's bytes [kLeanFrom, kLeanFrom + 32), the 16-B
+// chunk pair holding what every filter gate reads (12..37), packed like the dense gather
+// after a 16-B pad at the block's first slot; a descriptor points kLeanFrom bytes before its
+// frame's chunks.
+constexpr uint32_t kLeanFrom = 12;
+constexpr bool packs(WalkMode m) { return m == kGatherDense || m == kGatherLean; }
 
 inline uint8_t* dense_at(const Chain& ch) { return ch.line + 16u * ch.fill; }
 
@@ -124,6 +131,20 @@ inline uint32_t prefix_len(const uint8_t* f, uint32_t len) {
 // streamed as whole lines.
 template <WalkMode MODE>
 inline void copy_prefix(Chain& ch) {
+    if (MODE == kGatherLean) {   // two chunks, zero past the frame (whose end may end the mapping)
+        const uint32_t len = ch.pend_len;
+        if (len >= kLeanFrom + 32u) {
+            push16(ch, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + kLeanFrom)));
+            push16(ch, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ch.pend + kLeanFrom + 16)));
+        } else {
+            alignas(16) uint8_t t[32] = {};
+            if (len > kLeanFrom) std::memcpy(t, ch.pend + kLeanFrom, len - kLeanFrom);
+            push16(ch, _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
+            push16(ch, _mm_load_si128(reinterpret_cast<const __m128i*>(t + 16)));
+        }
+        ch.pend = nullptr;
+        return;
+    }
     const uint32_t m = prefix_len(ch.pend, ch.pend_len);
     if (MODE == kGatherDense) {
         const uint32_t full = m & ~15u;
@@ -180,7 +201,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
             ch.block = b;
             ch.first = start[k];
             ch.pend = nullptr;
-            ch.line = slots ? slots + (uint64_t)start[k] * BT_PREFIX_SLOT : nullptr;
+            ch.line = slots ? slots + (uint64_t)start[k] * BT_PREFIX_SLOT + (MODE == kGatherLean ? 16u : 0u) : nullptr;
             ch.fill = 0;
             if (ch.n) {
                 __builtin_prefetch(ch.blk + ch.off);
@@ -204,8 +225,9 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                 if (mac + snap > bs) return ch.block;
                 if (MODE != kWalkOnly) {
                     const uint64_t i = ch.first + ch.j;
-                    ch.pend_slot = MODE == kGatherDense ? dense_at(ch) : slots + i * BT_PREFIX_SLOT;
-                    ch.out[ch.j] = BT_DESC((uint64_t)(ch.pend_slot - slots), std::min<uint32_t>(snap, kDescLenMax));
+                    ch.pend_slot = packs(MODE) ? dense_at(ch) : slots + i * BT_PREFIX_SLOT;
+                    ch.out[ch.j] = BT_DESC((uint64_t)(ch.pend_slot - slots) - (MODE == kGatherLean ? kLeanFrom : 0u),
+                                           std::min<uint32_t>(snap, kDescLenMax));
                     if (ch.rout) ch.rout[ch.j] = BT_DESC(ch.base_off + mac, std::min<uint32_t>(snap, kDescLenMax));
                     ch.pend = ch.blk + mac;
                     ch.pend_len = snap;
@@ -216,7 +238,7 @@ int64_t walk_blocks(const bt_tpv3_ring* r, const uint32_t* blocks, const uint32_
                 }
                 if (++ch.j == ch.n) {          // chain done: swap in the last live one
                     if (MODE != kWalkOnly && ch.pend) copy_prefix<MODE>(ch);
-                    if (MODE == kGatherDense) flush_stage(ch);
+                    if (packs(MODE)) flush_stage(ch);
                     c[g] = c[--live];
                     continue;
                 }
@@ -237,7 +259,7 @@ extern "C" {
 namespace {
 
 int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks, uint8_t* slots,
-              bool dense, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap, uint32_t* n_desc,
+              WalkMode mode, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap, uint32_t* n_desc,
               uint32_t* n_blocks_taken) {
     if (!ring || !ring->base || !n_desc || !n_blocks_taken || (cap && !desc))
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3: null argument");
@@ -268,10 +290,12 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
     auto work = [&](unsigned w, unsigned T) {
         const uint32_t a = (uint32_t)((uint64_t)nb * w / T), b = (uint32_t)((uint64_t)nb * (w + 1) / T);
         if (a >= b) return;
-        const int64_t e =
-            !slots ? walk_blocks<kWalkOnly>(ring, blocks.data() + a, start.data() + a, b - a, desc, nullptr, nullptr)
-            : dense ? walk_blocks<kGatherDense>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots, ring_desc)
-                    : walk_blocks<kGatherSlots>(ring, blocks.data() + a, start.data() + a, b - a, desc, slots, nullptr);
+        const uint32_t* bl = blocks.data() + a;
+        const uint32_t* st = start.data() + a;
+        const int64_t e = mode == kWalkOnly ? walk_blocks<kWalkOnly>(ring, bl, st, b - a, desc, nullptr, nullptr)
+                        : mode == kGatherDense ? walk_blocks<kGatherDense>(ring, bl, st, b - a, desc, slots, ring_desc)
+                        : mode == kGatherLean ? walk_blocks<kGatherLean>(ring, bl, st, b - a, desc, slots, ring_desc)
+                                              : walk_blocks<kGatherSlots>(ring, bl, st, b - a, desc, slots, nullptr);
         if (slots) _mm_sfence();   // this worker's streaming stores land before the join
         if (e >= 0) bad.store(e);
     };
@@ -289,14 +313,14 @@ int ring_walk(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint3
 
 int bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                       bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc, uint32_t* n_blocks_taken) {
-    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, false, desc, nullptr, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, nullptr, kWalkOnly, desc, nullptr, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                         uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
                         uint32_t* n_blocks_taken) {
     if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_tpv3: null slots");
-    return ring_walk(ctx, ring, first_block, max_blocks, slots, false, desc, nullptr, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, kGatherSlots, desc, nullptr, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
@@ -305,7 +329,16 @@ int bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t fi
     if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: null slots");
     if ((uintptr_t)slots & 15u)
         return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_dense_tpv3: slots not 16-B aligned");
-    return ring_walk(ctx, ring, first_block, max_blocks, slots, true, desc, ring_desc, cap, n_desc, n_blocks_taken);
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, kGatherDense, desc, ring_desc, cap, n_desc, n_blocks_taken);
+}
+
+int bt_ring_gather_lean_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                             uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
+                             uint32_t* n_desc, uint32_t* n_blocks_taken) {
+    if (!slots && cap) return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_lean_tpv3: null slots");
+    if ((uintptr_t)slots & 15u)
+        return bt::set_error(BT_E_INVALID_ARGUMENT, "bt_ring_gather_lean_tpv3: slots not 16-B aligned");
+    return ring_walk(ctx, ring, first_block, max_blocks, slots, kGatherLean, desc, ring_desc, cap, n_desc, n_blocks_taken);
 }
 
 int bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count) {

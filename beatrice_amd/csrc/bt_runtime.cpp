@@ -456,6 +456,8 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
         c->ws_next ^= 1;
     }
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
+    if ((b->flags & BT_BATCH_LEAN) && o->records)
+        return fail(BT_E_INVALID_ARGUMENT, "a BT_BATCH_LEAN batch holds frame bytes 12..43 only: no records");
     // The readable range of base is part of the contract: descriptor batches must state it
     // (a descriptor past it then reads zeros instead of arbitrary memory); fixed-stride
     // batches default to n * stride.
@@ -472,7 +474,7 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     a.base = b->base;
     a.desc = static_cast<const uint64_t*>(b->desc);
     a.desc_words = b->desc_format == BT_DESC_XDP ? 2u : 1u;
-    a.prefixes = (b->flags & BT_BATCH_PREFIXES) ? 1u : 0u;
+    a.prefixes = (b->flags & (BT_BATCH_PREFIXES | BT_BATCH_LEAN)) ? 1u : 0u;
     a.stride = b->stride;
     a.n = b->n;
     a.ntiles = (b->n + 63) / 64;
@@ -1653,6 +1655,8 @@ int run_extract(bt_ctx* c, const bt_batch* b, const ExTable& t, bool never, cons
     if (!b->desc && b->stride == 0 && b->n) return fail(BT_E_INVALID_ARGUMENT, "fixed-stride mode needs stride > 0");
     if (o->values && o->n_cap < b->n) return fail(BT_E_INVALID_ARGUMENT, "values n_cap %u < n %u", o->n_cap, b->n);
     if (b->desc_format > BT_DESC_XDP) return fail(BT_E_INVALID_ARGUMENT, "unknown desc_format %u", b->desc_format);
+    if (b->flags & BT_BATCH_LEAN)
+        return fail(BT_E_INVALID_ARGUMENT, "a BT_BATCH_LEAN batch holds frame bytes 12..43 only: no user-table extraction");
     if (!b->n) return BT_OK;
     uint64_t bytes = b->bytes;   // as run_device: mandatory with descriptors
     if (b->desc) {

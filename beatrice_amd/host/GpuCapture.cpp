@@ -287,8 +287,9 @@ const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds ti
     uint32_t n = 0;
     const bool gathered = opts_.gather && !(opts_.inPlaceEvery && polls_ % opts_.inPlaceEvery == opts_.inPlaceEvery - 1);
     ++polls_;
+    const bool lean = gathered && opts_.lean && !opts_.records;
     auto taken = gathered ? ring_.takeGathered(filter_.context(), opts_.maxBlocks, slots_.data(), slotDesc_.data(),
-                                               desc_.data(), opts_.maxPackets, &n)
+                                               desc_.data(), opts_.maxPackets, &n, lean)
                           : ring_.take(filter_.context(), opts_.maxBlocks, desc_.data(), opts_.maxPackets, &n);
     if (taken.isError()) throw std::runtime_error("GpuTpacketStage: " + taken.getErrorMessage());
     batch_.blocks = taken.getValue();
@@ -306,7 +307,7 @@ const GpuTpacketStage::Batch& GpuTpacketStage::poll(std::chrono::milliseconds ti
     b.n = n;
     b.bytes = gathered ? slots_.size() : ring_.bytes();
     b.desc_format = BT_DESC_PACKED;
-    b.flags = gathered ? BT_BATCH_PREFIXES : 0u;   // PAYLOAD slots: resolved on the host from the frame
+    b.flags = (gathered ? BT_BATCH_PREFIXES : 0u) | (lean ? BT_BATCH_LEAN : 0u);   // PAYLOAD: on the host, from the frame
     bt_outputs o{};
     o.records = opts_.records ? records_.data() : nullptr;
     o.n_cap = opts_.maxPackets;

@@ -110,6 +110,10 @@ public:
         // place, sharing the work between the host's copy and the GPU's PCIe reads.
         bool gather = false;
         uint32_t inPlaceEvery = 0;
+        // Gathered batches that ask for no records pack only frame bytes 12..43
+        // (bt_ring_gather_lean_tpv3, BT_BATCH_LEAN): the ring's e2e verdicts +17..45 % over the
+        // full prefixes with inPlaceEvery = 2. false: the full prefixes.
+        bool lean = true;
     };
     // One batch of ring blocks, owned by the caller until release().
     struct Batch {

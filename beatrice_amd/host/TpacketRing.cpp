@@ -122,11 +122,12 @@ Result<uint32_t> TpacketV3Ring::take(bt_ctx* ctx, uint32_t maxBlocks, bt_pkt_des
 }
 
 Result<uint32_t> TpacketV3Ring::takeGathered(bt_ctx* ctx, uint32_t maxBlocks, uint8_t* slots, bt_pkt_desc* slotDesc,
-                                             bt_pkt_desc* ringDesc, uint32_t cap, uint32_t* n) {
+                                             bt_pkt_desc* ringDesc, uint32_t cap, uint32_t* n, bool lean) {
     const bt_tpv3_ring r = ring();
     uint32_t blocks = 0;
     *n = 0;
-    if (bt_ring_gather_dense_tpv3(ctx, &r, cursor_, maxBlocks, slots, slotDesc, ringDesc, cap, n, &blocks) != BT_OK)
+    auto gather = lean ? bt_ring_gather_lean_tpv3 : bt_ring_gather_dense_tpv3;
+    if (gather(ctx, &r, cursor_, maxBlocks, slots, slotDesc, ringDesc, cap, n, &blocks) != BT_OK)
         return Result<uint32_t>::error(ErrorCode::INVALID_ARGUMENT, err_ = bt_last_error());
     return Result<uint32_t>::success(blocks);
 }

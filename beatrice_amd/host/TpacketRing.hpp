@@ -62,9 +62,10 @@ public:
     // host pool; ctx may be null); desc receives ring-relative descriptors
     Result<uint32_t> take(bt_ctx* ctx, uint32_t maxBlocks, bt_pkt_desc* desc, uint32_t cap, uint32_t* n);
     // the same walk, with each frame's header prefix packed into `slots` (bt_ring_gather_dense_tpv3:
-    // slotDesc points into slots, ringDesc at the frames)
+    // slotDesc points into slots, ringDesc at the frames); lean: only frame bytes 12..43 for
+    // filter-only batches (bt_ring_gather_lean_tpv3, run with BT_BATCH_LEAN)
     Result<uint32_t> takeGathered(bt_ctx* ctx, uint32_t maxBlocks, uint8_t* slots, bt_pkt_desc* slotDesc,
-                                  bt_pkt_desc* ringDesc, uint32_t cap, uint32_t* n);
+                                  bt_pkt_desc* ringDesc, uint32_t cap, uint32_t* n, bool lean = false);
     // hands `blocks` blocks back to the kernel starting at the cursor and advances it
     void release(uint32_t blocks);
     Stats statistics();

@@ -334,6 +334,8 @@ typedef struct bt_batch {          /* input; device memory or host memory mapped
 #define BT_BATCH_PREFIXES 0x1u     /* base holds header prefixes (bt_ring_gather_tpv3), not
                                       whole frames: PAYLOAD slots, which read past the
                                       headers, are left to the host (BT_DECIDE_HOST)     */
+#define BT_BATCH_LEAN 0x2u         /* with BT_BATCH_PREFIXES: frame bytes 12..43 only
+                                      (bt_ring_gather_lean_tpv3); records refused        */
 
 typedef struct bt_outputs {        /* any pointer may be NULL = not produced            */
     void*     records;             /* ceil(n/64) * 6144 bytes, tiled slabs (see above)  */
@@ -511,6 +513,14 @@ int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_b
 int  bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                                uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
                                uint32_t* n_desc, uint32_t* n_blocks_taken);
+/* The same walk for filter-only batches: each frame's bytes 12..43 (the 16-B chunk pair
+ * holding what every built-in filter reads, zeros past the frame) packed back to back after a
+ * 16-B pad at the block's first slot (j_k * BT_PREFIX_SLOT + 16), 32 B per frame;
+ * desc[i] = BT_DESC(offset of frame i's 32 B - 12, min(tp_snaplen, 65535)). Run the batch
+ * with flags BT_BATCH_PREFIXES | BT_BATCH_LEAN: a call that asks for records is refused. */
+int  bt_ring_gather_lean_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
+                              uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
+                              uint32_t* n_desc, uint32_t* n_blocks_taken);
 /* The walk with the frame chains followed on the GPU. The host reads only the taken blocks'
  * headers (block_status, num_pkts, offset_to_first_pkt: one line per block) and a kernel on
  * `stream` walks every chain through ring_dev (the ring's device-visible alias, e.g. from

@@ -107,14 +107,15 @@ def test_cpp_stage_per_gpu_fanout_rings():
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
 
 
-def _run_gathered(ctx, ring, bs, nb, filters, dense=False):
-    """bt_ring_gather_tpv3 (dense: bt_ring_gather_dense_tpv3) -> device run over the prefix
-    slots (BT_BATCH_PREFIXES), slots and outputs in registered host memory."""
+def _run_gathered(ctx, ring, bs, nb, filters, dense=False, lean=False):
+    """bt_ring_gather_tpv3 (dense: bt_ring_gather_dense_tpv3; lean: bt_ring_gather_lean_tpv3,
+    filter-only, BT_BATCH_LEAN, no records) -> device run over the prefix slots
+    (BT_BATCH_PREFIXES), slots and outputs in registered host memory."""
     wdesc, _ = abi.ring_walk_tpv3(ring, bs, nb, ctx=ctx)
     n = len(wdesc)
     slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)   # poison past each prefix
     gd = np.zeros(n, np.uint64)
-    desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx, dense=dense)
+    desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx, dense=dense, lean=lean)
     assert taken == nb and len(desc) == n
     tiles = (n + 63) // 64
     h_rec = np.zeros(tiles * 6144, np.uint8)
@@ -124,13 +125,41 @@ def _run_gathered(ctx, ring, bs, nb, filters, dense=False):
     held = [slots, gd, h_dec, h_ver, h_rec]
     dev = [ctx.register(a) for a in held]
     try:
-        batch = abi.Batch(dev[0], dev[1], 0, n, slots.nbytes, abi.DESC_PACKED, abi.BATCH_PREFIXES)
-        ctx.run_device(batch, abi.Outputs(dev[4], n, dev[3], dev[2], None, None))
+        batch = abi.Batch(dev[0], dev[1], 0, n, slots.nbytes, abi.DESC_PACKED,
+                          abi.BATCH_PREFIXES | (abi.BATCH_LEAN if lean else 0))
+        ctx.run_device(batch, abi.Outputs(None if lean else dev[4], n, dev[3], dev[2], None, None))
         ctx.synchronize()
     finally:
         for a in held:
             ctx.unregister(a)
-    return wdesc, abi.untile_records(h_rec, n), h_dec[:n]
+    return wdesc, None if lean else abi.untile_records(h_rec, n), h_dec[:n]
+
+
+def test_lean_gather_decides_as_the_reference(gpu_ctx):
+    """bt_ring_gather_lean_tpv3 + BT_BATCH_LEAN: the kernels read frame bytes 12..43 only and
+    decide as the reference on the kernel-written ring (every filter set without PAYLOAD) and
+    as the oracle on 1M-frame C3 / C4 / fuzz rings; asking such a batch for records, or
+    extracting a user table from it, is refused."""
+    g = np.load(os.path.join(GOLDEN, "ring_lo.npz"))
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    bs, nb = (int(x) for x in g["geometry"])
+    for s in man["rings"]["ring_lo"]["filter_sets"]:
+        filters = man["filter_sets"][s]
+        if any(f["type"] == abi.PAYLOAD for f in filters):
+            continue
+        desc, _, dec = _run_gathered(gpu_ctx, g["ring"].copy(), bs, nb, filters, lean=True)
+        assert np.array_equal(desc, g["desc"])
+        compare_decisions(dec, g[f"code__{s}"], g[f"src__{s}"], filters, where=f"ring_lo/{s} lean")
+    for cfg in (synth.C3, synth.C4, synth.FUZZ):
+        data, desc0 = synth.capture(cfg, 1 << 20, seed=29)
+        ring, _, used = synth.tpv3_ring(data, desc0)
+        desc, _, dec = _run_gathered(gpu_ctx, ring, synth.TPV3_BLOCK, used, C3_SET, lean=True)
+        _, odec, _ = ol.oracle_run(ring, desc, len(desc), C3_SET, parse=False)
+        assert np.array_equal(dec, odec), cfg
+    buf = gpu_ctx.alloc(4096)
+    batch = abi.Batch(buf.ptr, buf.ptr + 2048, 0, 1, 2048, abi.DESC_PACKED, abi.BATCH_PREFIXES | abi.BATCH_LEAN)
+    with pytest.raises(abi.BtError):
+        gpu_ctx.run_device(batch, abi.Outputs(buf.ptr + 3072, 1, None, None, None, None))
 
 
 @pytest.mark.parametrize("dense", [False, True])

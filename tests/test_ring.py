@@ -341,3 +341,45 @@ def test_dense_gather_packs_each_block(which):
         k = int(min(room[i], lens[i], 38))
         assert np.array_equal(slots[goff[i]:goff[i] + k], ring[woff[i]:woff[i] + k]), i
     _same_as_ring(ring, wdesc, slots, gdesc, man)
+
+
+@pytest.mark.parametrize("which", ["kernel_ring", "c2", "c3", "c4", "fuzz"])
+def test_lean_gather_packs_the_filter_bytes(which):
+    """bt_ring_gather_lean_tpv3 (filter-only batches): 32 B per frame, each block's frames back
+    to back after a 16-B pad at its first slot; frame i's descriptor points 12 B before its 32
+    B, which hold the frame's bytes 12..43 (zeros past the frame); the oracle's decisions over
+    them equal its decisions over the ring for the reference's filter sets."""
+    import json
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    if which == "kernel_ring":
+        g, bs, nb = _fixture()
+        ring, used = g["ring"].copy(), nb
+    else:
+        cfg = {"c2": synth.C2, "c3": synth.C3, "c4": synth.C4, "fuzz": synth.FUZZ}[which]
+        data, desc = synth.capture(cfg, 6000, seed=12)
+        bs = 1 << 16
+        ring, _, used = synth.tpv3_ring(data, desc, block_size=bs)
+    wdesc, taken = abi.ring_walk_tpv3(ring, bs, used)
+    n = len(wdesc)
+    slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)
+    out, rout = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    gdesc, gtaken = abi.ring_gather_tpv3(ring, bs, used, slots, out, lean=True, ring_out=rout)
+    assert gtaken == taken and len(gdesc) == n and np.array_equal(rout, wdesc)
+    assert np.array_equal(synth.desc_len(gdesc), synth.desc_len(wdesc))
+    goff = synth.desc_off(gdesc).astype(np.int64) + 12   # where each frame's 32 B start
+    woff = synth.desc_off(wdesc).astype(np.int64)
+    lens = synth.desc_len(wdesc).astype(np.int64)
+    blk = woff // bs
+    first = np.r_[True, blk[1:] != blk[:-1]]
+    assert np.array_equal(goff[first], np.flatnonzero(first) * abi.PREFIX_SLOT + 16)
+    assert np.all(np.diff(goff)[~first[1:]] == 32)
+    for i in range(n):
+        want = np.zeros(32, np.uint8)
+        k = int(max(0, min(lens[i] - 12, 32)))
+        want[:k] = ring[woff[i] + 12:woff[i] + 12 + k]
+        assert np.array_equal(slots[goff[i]:goff[i] + 32], want), i
+    for s in ("c3", "mixed", "throw_after", "bpf_1", "port_range_1", "ip_range_1"):
+        filters = man["filter_sets"][s]
+        _, dw, _ = ol.oracle_run(ring, wdesc, n, filters, parse=False)
+        _, dg, _ = ol.oracle_run(slots, gdesc, n, filters, parse=False)
+        assert np.array_equal(dg, dw), s

@@ -32,6 +32,9 @@ ap.add_argument("--gather", action="store_true",
                      "slots (bt_ring_gather_tpv3) and the kernels read the slots (BT_BATCH_PREFIXES)")
 ap.add_argument("--dense", action="store_true",
                 help="with --gather: each block's prefixes packed back to back (bt_ring_gather_dense_tpv3)")
+ap.add_argument("--lean", action="store_true",
+                help="with --gather: each frame's bytes 12..43 packed back to back (bt_ring_gather_lean_tpv3, "
+                     "BT_BATCH_LEAN): verdict rows only")
 ap.add_argument("--mix", type=int, default=0,
                 help="with --gather: every N-th batch is walked and read in place instead (the host "
                      "gathers, the GPU reads the other batches' frames over PCIe itself)")
@@ -160,7 +163,7 @@ if a.tpacket:
         d_slots = ctx.register(slots)
     if a.gpu_walk:
         g_desc = ctx.alloc(8 * (n + 64))
-    for mode in ("verdicts", "records+verdicts"):
+    for mode in ("verdicts",) if a.lean else ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
         tiles = (n + 63) // 64 + nbat + 1          # each batch starts its outputs on a fresh tile
         h_dec = np.zeros(tiles * 64, np.uint8)
@@ -179,7 +182,7 @@ if a.tpacket:
                 if walk and gathered:
                     got, taken = abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B,
                                                       max_blocks=min(B, used - k * B), ctx=ctx, slot_base=start,
-                                                      dense=a.dense)
+                                                      dense=a.dense, lean=a.lean)
                     cnt = len(got)
                     if len(counts) < nbat:
                         counts.append(cnt)
@@ -207,7 +210,8 @@ if a.tpacket:
                     continue
                 if gathered:
                     batch = abi.Batch(d_slots + abi.PREFIX_SLOT * start, d_desc + 8 * start, 0, cnt,
-                                      abi.PREFIX_SLOT * cnt, abi.DESC_PACKED, abi.BATCH_PREFIXES)
+                                      abi.PREFIX_SLOT * cnt, abi.DESC_PACKED,
+                                      abi.BATCH_PREFIXES | (abi.BATCH_LEAN if a.lean else 0))
                 else:
                     dd = g_desc.ptr if a.gpu_walk else d_desc
                     batch = abi.Batch(d_ring, dd + 8 * start, 0, cnt, ring.nbytes, abi.DESC_PACKED, 0)
@@ -238,7 +242,7 @@ if a.tpacket:
                 continue
             if a.gather and not (a.mix and k % a.mix == a.mix - 1):
                 abi.ring_gather_tpv3(ring, bs, used, slots, h_desc, first=k * B, max_blocks=min(B, used - k * B),
-                                     ctx=ctx, dense=a.dense)
+                                     ctx=ctx, dense=a.dense, lean=a.lean)
             else:
                 abi.ring_walk_tpv3(ring, bs, used, first=k * B, max_blocks=min(B, used - k * B), ctx=ctx,
                                    out=h_desc[:])
@@ -247,6 +251,9 @@ if a.tpacket:
         lens = synth.desc_len(rdesc)
         pcie = float(np.minimum(lens, 64).sum() + 8 * n)
         how = "tpacket_v3 ring, walk then host gather (bt_parse_filter), " if a.host_gather else \
+            f"tpacket_v3 ring, lean gather (bytes 12..43) per block, every {a.mix}th batch in place, zero-copy, " \
+            if a.gather and a.lean and a.mix else \
+            "tpacket_v3 ring, lean gather (bytes 12..43) per block, zero-copy, " if a.gather and a.lean else \
             f"tpacket_v3 ring, header gather packed per block, every {a.mix}th batch in place, zero-copy, " \
             if a.gather and a.dense and a.mix else \
             "tpacket_v3 ring, header gather packed per block, zero-copy, " if a.gather and a.dense else \
