@@ -1819,12 +1819,13 @@ int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, ui
     (void)pool_of(c);
     // chunks of at most 1M packets: [prefixes | descriptors] in, [status | values | image] out.
     // The gather and the drain run on the context's host threads (a serial gather, length
-    // check and drain were most of a 1M-packet call). Tables up to 256 B give every frame one
-    // slot of round_up(span, 16) bytes, so the gather needs no prefix pass; wider ones pack
-    // each frame's round_up(min(len, span), 16) bytes after a per-worker count and scan.
+    // check and drain were most of a 1M-packet call). Tables up to 64 B (no frame is shorter
+    // than an Ethernet minimum's worth of slot) give every frame one slot of round_up(span, 16)
+    // bytes, so the gather needs no prefix pass; wider ones pack each frame's
+    // round_up(min(len, span), 16) bytes after a per-worker count and scan.
     const uint32_t chunk = 1u << 20;
     const size_t slot = ((size_t)span + 15u) & ~(size_t)15u;
-    const bool fixed = slot <= 256;
+    const bool fixed = slot <= 64;
     for (uint32_t lo = 0; lo < n; lo += chunk) {
         const uint32_t m = std::min(chunk, n - lo);
         const unsigned T = pipeline_share(c);
