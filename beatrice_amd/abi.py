@@ -546,14 +546,38 @@ class Context:
         return out
 
 
+PAGE = 4096
+
+
+def host_array(shape, dtype=np.uint8) -> np.ndarray:
+    """A zeroed array on pages of its own: an anonymous mapping, page-aligned and padded to
+    whole pages, that lives as long as the array. Registration (Context.register,
+    Group.register) is in whole pages and refuses a range that shares only some of its pages
+    with a live registration, so buffers registered side by side (a capture, its
+    descriptors, the outputs) are allocated this way, as a UMEM or a ring is."""
+    import mmap
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    m = mmap.mmap(-1, max(PAGE, (n + PAGE - 1) // PAGE * PAGE))
+    return np.frombuffer(m, dtype=dt, count=n // dt.itemsize).reshape(shape)
+
+
+def host_copy(arr: np.ndarray) -> np.ndarray:
+    """host_array holding a copy of arr."""
+    out = host_array(arr.shape, arr.dtype)
+    np.copyto(out, arr)
+    return out
+
+
 def host_outputs(n: int, records=True, filters=True) -> dict:
     """Output arrays for run_host calls of n packets, allocated and touched once (a capture
-    loop reuses its outputs; fresh arrays would fault their pages in inside every call)."""
-    o = {"records": np.zeros((n, BT_REC_BYTES), dtype=np.uint8) if records else None,
-         "verdict": np.zeros((n + 63) // 64, dtype=np.uint64) if filters else None,
-         "decide": np.zeros(n, dtype=np.uint8) if filters else None,
-         "pass_idx": np.zeros(max(n, 1), dtype=np.uint32) if filters else None,
-         "n_pass": np.zeros(1, dtype=np.uint32) if filters else None}
+    loop reuses its outputs; fresh arrays would fault their pages in inside every call), each
+    on pages of its own (host_array), so any of them may be registered."""
+    o = {"records": host_array((n, BT_REC_BYTES), np.uint8) if records else None,
+         "verdict": host_array((n + 63) // 64, np.uint64) if filters else None,
+         "decide": host_array(n, np.uint8) if filters else None,
+         "pass_idx": host_array(max(n, 1), np.uint32) if filters else None,
+         "n_pass": host_array(1, np.uint32) if filters else None}
     for a in o.values():
         if a is not None:
             a.fill(0)   # first touch now, outside any timed call
@@ -580,7 +604,7 @@ def _host_outputs(n, records, filters, outs):
                 raise ValueError(f"outs[{k!r}]: need a writable contiguous {np.dtype(dt).name} array of at least "
                                  f"{size} elements, got {a.dtype} x {a.size}")
         # views of this call's part (arrays sized for a larger batch are reused as they are)
-        outs = {k: None if outs[k] is None else outs[k].reshape(-1)[:size] for k, (_, _, size) in need.items()}
+        outs = {k: None if outs.get(k) is None else outs[k].reshape(-1)[:size] for k, (_, _, size) in need.items()}
         if outs["records"] is not None:
             outs["records"] = outs["records"].reshape(n, BT_REC_BYTES)
     return outs["records"], outs["verdict"], outs["decide"], outs["pass_idx"], outs["n_pass"]

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "bt_device.h"
+#include "bt_hip_util.h"
 #include "bt_host.h"
 #include "bt_host_pool.h"
 
@@ -79,10 +80,6 @@ struct bt_group {
     std::unique_ptr<std::atomic<uint32_t>[]> busy;   // per member: call parts running on it
     std::atomic<uint32_t> rr{0};
     uint32_t route_below = 0;
-    // the host batches' staged window per frame without / with records (the bytes the host
-    // pipeline copies for the installed program: 32 / 112 / 176), cached when a program is installed so that a split reads it
-    // without taking member 0's context lock (which a host batch in flight holds)
-    std::atomic<uint32_t> stage_window[2] = {{0u}, {0u}};
 };
 
 namespace {
@@ -261,33 +258,12 @@ uint8_t* alias_of(const bt_group* g, uint32_t k, const void* p, uint64_t need) {
     return nullptr;
 }
 
-int alias_all(bt_group* g, void* host, std::vector<uint8_t*>* dev) {
-    const uint32_t m = (uint32_t)g->members.size();
-    dev->assign(m, nullptr);
-    for (uint32_t k = 0; k < m; ++k) {
-        void* d = nullptr;
-        if (hipSetDevice(bt::ctx_device(g->members[k])) != hipSuccess ||
-            hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
-            const hipError_t e = hipGetLastError();
-            return bt::set_error(BT_E_INTERNAL, "hipHostGetDevicePointer on member %u (device %d): %s", k,
-                                 bt::ctx_device(g->members[k]), hipGetErrorString(e));
-        }
-        (*dev)[k] = static_cast<uint8_t*>(d);
-    }
-    return BT_OK;
-}
-
-// Every member's device has finished what it queued (before a registered range goes away).
-int sync_devices(bt_group* g) {
-    std::vector<int> done;
-    for (bt_ctx* c : g->members) {
-        const int d = bt::ctx_device(c);
-        if (std::find(done.begin(), done.end(), d) != done.end()) continue;
-        done.push_back(d);
-        if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-            return bt::set_error(BT_E_INTERNAL, "device %d: %s", d, hipGetErrorString(hipGetLastError()));
-    }
-    return BT_OK;
+// The members' devices, in member order (bt::pin_acquire's device list: member k's alias of
+// a registered range is aliases[k], taken on its own device).
+std::vector<int> member_devices(const bt_group* g) {
+    std::vector<int> d;
+    for (bt_ctx* c : g->members) d.push_back(bt::ctx_device(c));
+    return d;
 }
 
 // Indices of the set bits of verdict words [w0, w1) whose packet index is < n, written
@@ -383,6 +359,7 @@ int bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested
 static int group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out);
 
 int bt_group_create(const int* devices, uint32_t n_devices, const bt_opts* opts, bt_group** out) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!out || !devices || !n_devices) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / no devices");
     try {
         return group_create(devices, n_devices, opts, out);
@@ -435,7 +412,6 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
         g->route_below = rb ? (uint32_t)strtoul(rb, nullptr, 10) : (1u << 20);
         g->busy = std::make_unique<std::atomic<uint32_t>[]>(n_devices);
         for (uint32_t i = 0; i < n_devices; ++i) g->busy[i].store(0, std::memory_order_relaxed);
-        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::staged_bytes_of(g->members[0], r != 0));
     }
     if (n_devices > 1) {
         std::vector<const cpu_set_t*> pins;
@@ -456,12 +432,13 @@ static int group_create(const int* devices, uint32_t n_devices, const bt_opts* o
 }
 
 void bt_group_destroy(bt_group* g) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g) return;
     g->threads.reset();
-    if (!g->regions.empty() || g->scratch) (void)sync_devices(g);
-    for (const Region& r : g->regions) (void)hipHostUnregister(r.host);
+    // the group's references on its registered pages (the last one waits for the devices)
+    for (const Region& r : g->regions) (void)bt::pin_release(r.host, r.bytes);
     if (g->scratch) {
-        (void)hipHostUnregister(g->scratch);
+        (void)bt::pin_release(g->scratch, g->scratch_words * 8);
         free(g->scratch);
     }
     for (bt_ctx* c : g->members) bt_destroy(c);
@@ -475,13 +452,13 @@ bt_ctx* bt_group_member(bt_group* g, uint32_t k) {
 }
 
 int bt_group_filter_compile(bt_group* g, const bt_filter_desc* filters, uint32_t n) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
     try {
         std::unique_lock<std::shared_mutex> lk(g->prog_mu);
         bt::CompiledProgram p;   // compiled once, installed on every device
         if (int rc = bt::compile_program(filters, n, bt::ctx_flags(g->members[0]), &p)) return rc;
         const int rc = run_members(g, [&](uint32_t k) { return bt::install_program(g->members[k], p); });
-        for (int r = 0; r < 2; ++r) g->stage_window[r].store(bt::staged_bytes_of(g->members[0], r != 0));
         return rc;
     } catch (const std::exception& e) {
         return bt::set_error(BT_E_INTERNAL, "bt_group_filter_compile: %s", e.what());
@@ -500,7 +477,10 @@ int bt_group_cost(bt_group* g, int mapped, int records, int filters, uint32_t de
         out->window = records ? 128u : kLeanWindow;
         out->fixed = desc_bytes + (records ? 64u : 0u) + (filters ? 1u : 0u);
     } else {
-        out->window = g->stage_window[records != 0].load(std::memory_order_relaxed);
+        // the bytes the host pipeline copies per frame for member 0's installed program (32 /
+        // 112 / 176), published by the context at install time: a program compiled on a member
+        // directly (bt_group_member + bt_filter_compile) is seen too, and no member lock is taken
+        out->window = bt::staged_window(g->members[0], records != 0);
         out->fixed = desc_bytes + (records ? (uint32_t)BT_REC_BYTES : 0u) + (filters ? 1u : 0u);
     }
     return BT_OK;
@@ -508,6 +488,7 @@ int bt_group_cost(bt_group* g, int mapped, int records, int filters, uint32_t de
 
 int bt_group_parse_filter(bt_group* g, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n, bt_rec* records,
                           uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
     if (n && (!base || !desc)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
     try {
@@ -524,6 +505,7 @@ int bt_group_parse_filter(bt_group* g, const uint8_t* base, const bt_pkt_desc* d
 int bt_group_parse_filter_ptrs(bt_group* g, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                                bt_rec* records, uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx,
                                uint32_t* n_pass) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g) return bt::set_error(BT_E_INVALID_ARGUMENT, "null group");
     if (n && (!frames || !lens)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
     try {
@@ -554,6 +536,7 @@ int bt_group_host_parallel(bt_group* g, void (*fn)(void*, uint32_t, uint32_t), v
 }
 
 int bt_group_host_register(bt_group* g, void* host, uint64_t bytes) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g || !host || !bytes) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument / empty range");
     try {
         std::unique_lock<std::shared_mutex> lk(g->reg_mu);
@@ -562,16 +545,14 @@ int bt_group_host_register(bt_group* g, void* host, uint64_t bytes) {
             if (a < r.host + r.bytes && r.host < a + bytes)
                 return bt::set_error(BT_E_INVALID_ARGUMENT, "range %p + %llu overlaps a registered range", host,
                                      (unsigned long long)bytes);
-        if (hipSetDevice(bt::ctx_device(g->members[0])) != hipSuccess ||
-            hipHostRegister(host, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess)
-            return bt::set_error(BT_E_INTERNAL, "hipHostRegister: %s", hipGetErrorString(hipGetLastError()));
+        // whole pages, in the process's one table (bt_pin.h): pages a context or another group
+        // already holds in full are shared, a range that holds only some of them is refused
+        const std::vector<int> devs = member_devices(g);
         Region r;
         r.host = static_cast<uint8_t*>(host);
         r.bytes = bytes;
-        if (int rc = alias_all(g, host, &r.dev)) {
-            (void)hipHostUnregister(host);
-            return rc;
-        }
+        r.dev.assign(devs.size(), nullptr);
+        if (int rc = bt::pin_acquire(host, bytes, devs.data(), (uint32_t)devs.size(), r.dev.data())) return rc;
         g->regions.push_back(std::move(r));
         return BT_OK;
     } catch (const std::exception& e) {
@@ -580,20 +561,21 @@ int bt_group_host_register(bt_group* g, void* host, uint64_t bytes) {
 }
 
 int bt_group_host_unregister(bt_group* g, void* host) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g || !host) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
     std::unique_lock<std::shared_mutex> lk(g->reg_mu);
     auto it = std::find_if(g->regions.begin(), g->regions.end(), [&](const Region& r) { return r.host == host; });
     if (it == g->regions.end()) return bt::set_error(BT_E_INVALID_ARGUMENT, "%p is not a registered range", host);
-    // every queued kernel of every member that may read or write the range has finished
-    if (int rc = sync_devices(g)) return rc;
-    if (hipHostUnregister(host) != hipSuccess)
-        return bt::set_error(BT_E_INTERNAL, "hipHostUnregister: %s", hipGetErrorString(hipGetLastError()));
+    // the last reference on the pages waits for every device that holds an alias of them (the
+    // queued kernels of every member that may read or write the range) before unregistering
+    if (int rc = bt::pin_release(it->host, it->bytes)) return rc;
     g->regions.erase(it);
     for (bt_ctx* c : g->members) bt::ctx_forget_base(c);   // the address may come back as another kind
     return BT_OK;
 }
 
 int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_outputs* o) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!g || !b || !o) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
     const uint32_t n = b->n;
     if (n && !b->base) return bt::set_error(BT_E_INVALID_ARGUMENT, "null packet buffer");
@@ -653,26 +635,22 @@ int bt_group_parse_filter_mapped(bt_group* g, const bt_batch* b, const bt_output
             slk.lock();
             if (g->scratch_words < words) {
                 if (g->scratch) {
-                    (void)hipHostUnregister(g->scratch);
+                    if (int rc = bt::pin_release(g->scratch, g->scratch_words * 8)) return rc;
                     free(g->scratch);
                     g->scratch = nullptr;
                     g->scratch_words = 0;
+                    g->scratch_dev.clear();
                 }
                 const size_t bytes = ((size_t)words * 8 + 4095) & ~(size_t)4095;
                 void* p = nullptr;
                 if (posix_memalign(&p, 4096, bytes) != 0) return bt::set_error(BT_E_RESOURCE, "scratch verdict words");
-                if (hipSetDevice(bt::ctx_device(g->members[0])) != hipSuccess ||
-                    hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
-                    free(p);
-                    return bt::set_error(BT_E_INTERNAL, "hipHostRegister (scratch): %s",
-                                         hipGetErrorString(hipGetLastError()));
-                }
-                if (int rc = alias_all(g, p, &g->scratch_dev)) {   // no half-made scratch for later calls
-                    (void)hipHostUnregister(p);
-                    free(p);
-                    g->scratch_dev.clear();
+                const std::vector<int> devs = member_devices(g);
+                std::vector<uint8_t*> al(devs.size(), nullptr);
+                if (int rc = bt::pin_acquire(p, bytes, devs.data(), (uint32_t)devs.size(), al.data())) {
+                    free(p);   // no half-made scratch for later calls
                     return rc;
                 }
+                g->scratch_dev = std::move(al);
                 g->scratch = static_cast<uint64_t*>(p);
                 g->scratch_words = bytes / 8;
             }

@@ -26,6 +26,7 @@
 
 #include "beatrice_gpu_bench.h"
 #include "bt_device.h"
+#include "bt_hip_util.h"
 #include "bt_host_pool.h"
 #include "bt_host.h"
 
@@ -90,6 +91,10 @@ struct bt_ctx {
     std::vector<bt_filter_slot> slots;
     DevProgram prog{};
     std::vector<uint8_t> dfa_pool;     // BT_K_PAYLOAD tables of the current program
+    // the host batches' staged bytes per frame without / with records for the installed
+    // program (stage_bytes / staged_bytes_of below), published by install_program so that a
+    // group's split reads them without this context's lock (a host batch in flight holds it)
+    std::atomic<uint32_t> staged_window[2] = {{0u}, {0u}};
     // PAYLOAD DFA pools, double-buffered: a recompile writes the buffer no queued launch
     // uses. Every stream that launched a kernel reading dfa_dev[k] has its own event in
     // dfa_readers[k], recorded right after that launch; a recompile that reuses buffer k
@@ -182,6 +187,7 @@ struct bt_ctx {
 };
 
 namespace bt {
+void publish_staged_window(bt_ctx* c);   // defined with the host pipeline
 
 int set_error(int code, const char* fmt, ...) {
     char buf[512];
@@ -745,6 +751,7 @@ int bt_device_count(int* out) {
 }
 
 int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!out) return fail(BT_E_INVALID_ARGUMENT, "null out");
     *out = nullptr;
     int n = 0;
@@ -771,6 +778,7 @@ int bt_create(int device, const bt_opts* opts, bt_ctx** out) {
     c->grid = c->opts.grid_waves ? (int)((c->opts.grid_waves + kWavesPerBlock - 1) / kWavesPerBlock)
                                  : device_grid_blocks(device);
     to_device_program(nullptr, 0, &c->prog);
+    bt::publish_staged_window(c);
     place_ctx(c);
     *out = c;
     return BT_OK;
@@ -818,9 +826,13 @@ int bt_node_cpus(int node, int32_t* cpus, uint32_t cap, uint32_t* n) {
 uint32_t bt_usable_cpus(void) { return bt::usable_cpus(); }
 
 void bt_destroy(bt_ctx* c) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
+    for (const auto& r : c->host_regs)   // registrations the caller left: this context's references
+        (void)bt::pin_release(reinterpret_cast<const void*>(r.first), r.second);
+    c->host_regs.clear();
     free_host(c);
     c->pool.reset();
     if (c->tgraph) (void)hipGraphExecDestroy(c->tgraph);
@@ -927,6 +939,7 @@ int install_program(bt_ctx* c, const CompiledProgram& p) {
     c->dfa_pool = p.dfa_pool;
     c->slots = p.slots;
     to_device_program(c->slots.data(), (uint32_t)c->slots.size(), &c->prog);
+    publish_staged_window(c);
     return BT_OK;
 }
 
@@ -938,12 +951,16 @@ void ctx_forget_base(bt_ctx* c) {
     c->last_base = nullptr;
 }
 uint32_t stage_bytes_of(bt_ctx* c, bool records);   // defined with the host pipeline
+uint32_t staged_window(const bt_ctx* c, bool records) {
+    return c->staged_window[records ? 1 : 0].load(std::memory_order_acquire);
+}
 
 }  // namespace bt
 
 extern "C" {
 
 int bt_filter_compile(bt_ctx* c, const bt_filter_desc* f, uint32_t n) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     CompiledProgram p;
     if (int rc = compile_program(f, n, c->opts.flags, &p)) return rc;
@@ -958,12 +975,14 @@ int bt_filter_program(const bt_ctx* c, bt_filter_slot* out, uint32_t cap, uint32
 }
 
 int bt_reserve(bt_ctx* c, uint32_t n) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     return ensure_ws(c, n);
 }
 
 int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, void* stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
@@ -973,6 +992,7 @@ int bt_parse_filter_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, vo
 
 int bt_parse_filter_device_async(bt_ctx* c, const bt_batch* b, const bt_outputs* o, void* stream,
                                  void* done_event) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = ensure_cstream(c)) return rc;
@@ -1050,6 +1070,7 @@ static int ensure_timing_events(bt_ctx* c, uint32_t iters) {
 
 int bt_time_device2(bt_ctx* c, const bt_batch* b, const bt_outputs* outs, uint32_t n_out, uint32_t iters,
                     uint32_t mode, bt_timing* t) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !b || !outs || !n_out || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
     if (mode & ~(uint32_t)(BT_TIME_KERNEL_EVENTS | BT_TIME_PIPELINED)) return fail(BT_E_INVALID_ARGUMENT, "unknown mode");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1117,12 +1138,14 @@ int bt_time_device2(bt_ctx* c, const bt_batch* b, const bt_outputs* outs, uint32
 }
 
 int bt_time_device_ex(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, bt_timing* t) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     const uint32_t mode = BT_TIME_KERNEL_EVENTS | ((c && (c->opts.flags & BT_OPT_PIPELINE)) ? BT_TIME_PIPELINED : 0u);
     return bt_time_device2(c, b, o, 1, iters, mode, t);
 }
 
 int bt_time_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, uint32_t iters, float* ms_per_iter,
                    float* main_ms) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     bt_timing t{};
     const int rc = bt_time_device_ex(c, b, o, iters, &t);
     if (rc) return rc;
@@ -1151,10 +1174,16 @@ uint32_t stage_bytes_of(bt_ctx* c, bool records) {
     std::lock_guard<std::mutex> lk(c->mu);
     return stage_bytes(c, records);
 }
-uint32_t staged_bytes_of(bt_ctx* c, bool records) {
-    std::lock_guard<std::mutex> lk(c->mu);
+uint32_t staged_bytes_locked(const bt_ctx* c, bool records) {
     const uint32_t w = stage_bytes(c, records);
     return w == kHostSlotFilter && !(c->opts.flags & BT_OPT_NO_LEAN_HOST) ? kHostLeanWidth : w;
+}
+uint32_t staged_bytes_of(bt_ctx* c, bool records) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    return staged_bytes_locked(c, records);
+}
+void publish_staged_window(bt_ctx* c) {   // under c->mu, after the program changed
+    for (int r = 0; r < 2; ++r) c->staged_window[r].store(staged_bytes_locked(c, r != 0), std::memory_order_release);
 }
 }  // namespace bt
 
@@ -1339,6 +1368,7 @@ extern "C" {
 
 int bt_parse_filter(bt_ctx* c, const uint8_t* base, const bt_pkt_desc* desc, uint32_t n, bt_rec* records,
                     uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (n && (!base || !desc)) return fail(BT_E_INVALID_ARGUMENT, "null packet buffer/descriptors");
     const WaitFor lk(c);
@@ -1353,6 +1383,7 @@ int bt_parse_filter(bt_ctx* c, const uint8_t* base, const bt_pkt_desc* desc, uin
 
 int bt_parse_filter_ptrs(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                          bt_rec* records, uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx, uint32_t* n_pass) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (n && (!frames || !lens)) return fail(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
     for (uint32_t i = 0; i < n; ++i)
@@ -1375,26 +1406,37 @@ int bt_host_stage_bytes(const bt_ctx* c, int with_records, uint32_t* bytes) {
 }
 
 int bt_host_register(bt_ctx* c, void* host, uint64_t bytes, void** dev_alias) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !host || !dev_alias || !bytes) return fail(BT_E_INVALID_ARGUMENT, "null argument / empty range");
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipHostRegister(host, bytes, hipHostRegisterMapped));
-    hipError_t e = hipHostGetDevicePointer(dev_alias, host, 0);
-    if (e != hipSuccess) {
-        (void)hipHostUnregister(host);
-        return fail(BT_E_INTERNAL, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        for (const auto& r : c->host_regs)
+            if (r.first == (uintptr_t)host)
+                return fail(BT_E_INVALID_ARGUMENT, "%p is already registered on this context", host);
     }
+    // whole pages, in the process's one table (bt_pin.h): a range inside pages another
+    // registration holds shares them, one that holds only some of them is refused
+    uint8_t* alias = nullptr;
+    if (int rc = bt::pin_acquire(host, bytes, &c->device, 1, &alias)) return rc;
+    *dev_alias = alias;
     std::lock_guard<std::mutex> lk(c->mu);
     c->host_regs.emplace_back((uintptr_t)host, bytes);
     return BT_OK;
 }
 
 int bt_host_unregister(bt_ctx* c, void* host) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !host) return fail(BT_E_INVALID_ARGUMENT, "null argument");
-    HIP_TRY(hipSetDevice(c->device));
-    // every queued kernel that may read or write the range (the context stream, the
-    // compaction stream, callers' streams) has finished before its mapping goes away
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipHostUnregister(host));
+    uint64_t bytes = 0;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        for (const auto& r : c->host_regs)
+            if (r.first == (uintptr_t)host) bytes = r.second;
+    }
+    if (!bytes) return fail(BT_E_INVALID_ARGUMENT, "%p is not registered on this context", host);
+    // the last reference waits for every device that holds an alias of the pages (queued
+    // kernels that read or write them) before they are unregistered
+    if (int rc = bt::pin_release(host, bytes)) return rc;
     std::lock_guard<std::mutex> lk(c->mu);   // host_resident's cache (read under mu): the
     c->last_base = nullptr;                   // address may come back as another kind
     auto& r = c->host_regs;
@@ -1403,6 +1445,7 @@ int bt_host_unregister(bt_ctx* c, void* host) {
 }
 
 int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !out) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     static const unsigned flags = [] {
@@ -1415,6 +1458,7 @@ int bt_dev_malloc(bt_ctx* c, uint64_t bytes, void** out) {
 }
 
 int bt_dev_free(bt_ctx* c, void* p) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (!p) return BT_OK;
     HIP_TRY(hipSetDevice(c->device));
@@ -1457,6 +1501,7 @@ extern "C" {
 // DMA of chunk k^1 runs), so no DMA touches the caller's (usually pageable) memory; they
 // are ordered after the context's streams (after_cstream) and complete before returning.
 int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (bytes && (!dst || !src)) return fail(BT_E_INVALID_ARGUMENT, "null pointer");
     std::lock_guard<std::mutex> lk(c->xfer_mu);
@@ -1478,6 +1523,7 @@ int bt_memcpy_h2d(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
 }
 
 int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (bytes && (!dst || !src)) return fail(BT_E_INVALID_ARGUMENT, "null pointer");
     std::lock_guard<std::mutex> lk(c->xfer_mu);
@@ -1503,6 +1549,7 @@ int bt_memcpy_d2h(bt_ctx* c, void* dst, const void* src, uint64_t bytes) {
 }
 
 int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = after_cstream(c)) return rc;
@@ -1514,6 +1561,7 @@ int bt_memset_d(bt_ctx* c, void* dst, int value, uint64_t bytes) {
 int bt_ring_walk_tpv3_gpu(bt_ctx* c, const bt_tpv3_ring* ring, const void* ring_dev, uint32_t first_block,
                           uint32_t max_blocks, bt_pkt_desc* desc_dev, uint32_t cap, uint32_t* n_desc,
                           uint32_t* n_blocks_taken, uint32_t* bad_dev, void* stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !ring || !ring->base || !ring_dev || !n_desc || !n_blocks_taken || (cap && !desc_dev))
         return fail(BT_E_INVALID_ARGUMENT, "bt_ring_walk_tpv3_gpu: null argument");
     if (!ring->n_blocks || ring->block_size < 48 || first_block >= ring->n_blocks)
@@ -1581,6 +1629,7 @@ int bt_host_parallel(bt_ctx* c, void (*fn)(void*, uint32_t, uint32_t), void* use
 }
 
 int bt_stream_create(bt_ctx* c, void** stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = nullptr;
@@ -1590,6 +1639,7 @@ int bt_stream_create(bt_ctx* c, void** stream) {
 }
 
 int bt_stream_synchronize(bt_ctx* c, void* stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
@@ -1597,6 +1647,7 @@ int bt_stream_synchronize(bt_ctx* c, void* stream) {
 }
 
 int bt_stream_destroy(bt_ctx* c, void* stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !stream) return fail(BT_E_INVALID_ARGUMENT, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
@@ -1605,6 +1656,7 @@ int bt_stream_destroy(bt_ctx* c, void* stream) {
 }
 
 int bt_synchronize(bt_ctx* c) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1703,6 +1755,7 @@ int bt_proto_span(const bt_field_def* fields, uint32_t n_fields, uint64_t* span)
 
 int bt_extract_device(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
                       const bt_extract_out* out, void* stream) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     ExTable t;
     bool never = false;
@@ -1715,6 +1768,7 @@ int bt_extract_device(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, 
 
 int bt_time_extract2(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
                      const bt_extract_out* out, uint32_t iters, uint32_t mode, bt_timing* t) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c || !b || !out || !iters) return fail(BT_E_INVALID_ARGUMENT, "null argument / zero iterations");
     if (mode & ~(uint32_t)BT_TIME_KERNEL_EVENTS) return fail(BT_E_INVALID_ARGUMENT, "unknown mode");
     const bool kev = (mode & BT_TIME_KERNEL_EVENTS) != 0;
@@ -1738,6 +1792,7 @@ int bt_time_extract2(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, u
 
 int bt_time_extract_ex(bt_ctx* c, const bt_batch* b, const bt_field_def* fields, uint32_t n_fields,
                        const bt_extract_out* out, uint32_t iters, bt_timing* t) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     return bt_time_extract2(c, b, fields, n_fields, out, iters, BT_TIME_KERNEL_EVENTS, t);
 }
 
@@ -1800,6 +1855,7 @@ int bt_filter_dfa_pool(const bt_ctx* c, void* out, uint32_t cap, uint32_t* bytes
 
 int bt_extract(bt_ctx* c, const uint8_t* const* frames, const uint32_t* lens, uint32_t n, const bt_field_def* fields,
                uint32_t n_fields, uint8_t* status, uint64_t* values, uint8_t* image) {
+    const bt::DeviceRestore keep_device;   // the caller's current device, restored on return
     if (!c) return fail(BT_E_INVALID_ARGUMENT, "null context");
     if (n && (!frames || !lens)) return fail(BT_E_INVALID_ARGUMENT, "null frame pointers/lengths");
     ExTable t;

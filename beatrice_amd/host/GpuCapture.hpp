@@ -17,7 +17,10 @@
 // against beatrice_core in the process that loads it, as for the plugin.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
+#include <cstdlib>
+#include <new>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -32,7 +35,32 @@
 #include "beatrice/ICaptureBackend.hpp"
 
 namespace beatrice {
+
 namespace gpu {
+
+// Page-aligned, page-padded storage for the buffers a stage registers with the devices:
+// registration is in whole pages (include/beatrice_gpu.h, bt_host_register), so two such
+// buffers must never share a page, as std::vector's heap blocks can.
+template <class T>
+struct PageAllocator {
+    using value_type = T;
+    PageAllocator() = default;
+    template <class U>
+    PageAllocator(const PageAllocator<U>&) {}
+    T* allocate(size_t n) {
+        const size_t bytes = std::max<size_t>((n * sizeof(T) + 4095) & ~size_t(4095), 4096);
+        void* p = nullptr;
+        if (posix_memalign(&p, 4096, bytes) != 0) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { free(p); }
+    template <class U>
+    bool operator==(const PageAllocator<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PageAllocator<U>&) const { return false; }
+};
+template <class T>
+using PageVector = std::vector<T, PageAllocator<T>>;
 
 class GpuAfPacketBackend : public ICaptureBackend {
 public:
@@ -154,13 +182,13 @@ private:
     Options opts_;
     uint8_t* ringBase_ = nullptr;
     // registered host buffers: descriptors in, decisions / verdicts / records out
-    std::vector<bt_pkt_desc> desc_;
-    std::vector<uint8_t> decide_;
-    std::vector<uint64_t> verdict_;
-    std::vector<uint8_t> records_;
+    PageVector<bt_pkt_desc> desc_;
+    PageVector<uint8_t> decide_;
+    PageVector<uint64_t> verdict_;
+    PageVector<uint8_t> records_;
     // header gather: packed prefixes and their descriptors (registered)
-    std::vector<uint8_t> slots_;
-    std::vector<bt_pkt_desc> slotDesc_;
+    PageVector<uint8_t> slots_;
+    PageVector<bt_pkt_desc> slotDesc_;
     std::vector<void*> registered_;   // with the filter's group
     uint64_t polls_ = 0;
     Batch batch_;

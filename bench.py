@@ -619,11 +619,15 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5, shared: bool =
             nodes = [grp.placement(k)["numa_node"] for k in range(n_dev)]
             spans = numa.member_byte_ranges(synth.desc_off(desc), synth.desc_len(desc), bounds)
             data = numa.place_ranges(raw, [(lo, hi, nd) for (lo, hi), nd in zip(spans, nodes)])
+            if data is raw:   # no NUMA information: pages of its own all the same
+                data = abi.host_copy(raw)
             del raw
             data_nodes = [numa.page_nodes(data[lo:hi]) if hi > lo else [] for lo, hi in spans]
             tiles = (packets + 63) // 64
-            dec = np.zeros(tiles * 64, np.uint8)
-            ver = np.zeros(tiles, np.uint64)
+            # registration is in whole pages: every registered buffer on pages of its own
+            desc = abi.host_copy(desc)
+            dec = abi.host_array(tiles * 64)
+            ver = abi.host_array(tiles, np.uint64)
             for a in (data, desc, dec, ver):
                 grp.register(a)
                 held.append(a)

@@ -433,7 +433,16 @@ int  bt_host_stage_bytes(const bt_ctx* ctx, int with_records, uint32_t* bytes);
 /* Zero-copy ingest: page-lock a host range (an AF_XDP UMEM, an RX descriptor ring,
  * an output array) and map it into the device; *dev_alias is the pointer kernels
  * use (it may be passed as bt_batch.base / .desc or as an output). The kernels then
- * read the header windows straight over PCIe: no host gather, no staging copy. */
+ * read the header windows straight over PCIe: no host gather, no staging copy.
+ * Registration is in whole pages, in one table for the process (contexts and groups
+ * alike): the pages that hold [host, host + bytes) are registered once; a range inside
+ * pages a live registration already holds shares them (a reference, no second lock); a
+ * range that shares only some of its pages with a live registration is refused
+ * (BT_E_INVALID_ARGUMENT: register page-aligned buffers, or one range covering both), so no
+ * page is ever locked twice and no unregister unlocks a page another registration still
+ * covers. A range is registered once per context. bt_host_unregister drops the context's
+ * reference; the last one waits for the devices that hold an alias, then unlocks. The pages
+ * must stay mapped (not freed or unmapped) while registered. */
 int  bt_host_register(bt_ctx* ctx, void* host, uint64_t bytes, void** dev_alias);
 int  bt_host_unregister(bt_ctx* ctx, void* host);
 
@@ -606,8 +615,10 @@ int      bt_group_host_parallel(bt_group* group, void (*fn)(void* user, uint32_t
 
 /* Zero-copy over the group (AF_XDP UMEM, TPACKET_V3 ring, output arrays): page-lock a host
  * range once (portable, mapped) and map it into every member's device; each member reads
- * it through its own alias over its own PCIe link. Ranges must not overlap. Unregister
- * waits for every member's device first. */
+ * it through its own alias over its own PCIe link. Whole pages, in the same process-wide
+ * table as bt_host_register (shared when another registration holds all of the range's
+ * pages, refused when it holds only some). A group's ranges must not overlap. The last
+ * reference on the pages waits for every device holding an alias, then unlocks. */
 int      bt_group_host_register(bt_group* group, void* host, uint64_t bytes);
 int      bt_group_host_unregister(bt_group* group, void* host);
 /* bt_parse_filter_device over group-registered host memory, split across the members:

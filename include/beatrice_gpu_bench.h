@@ -81,6 +81,13 @@ int  bt_time_extract_ex(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* 
 int  bt_time_extract2(bt_ctx* ctx, const bt_batch* batch, const bt_field_def* fields, uint32_t n_fields,
                       const bt_extract_out* out, uint32_t iters, uint32_t mode, bt_timing* timing);
 
+/* ---- registered host pages (diagnostics) ---------------------------------------
+ * bt_host_register and bt_group_host_register keep one process-wide table of the whole
+ * pages they registered (beatrice_amd/csrc/bt_pin.h): lo_hi_refs[3 i .. 3 i + 2] = span i's
+ * first byte, end (both page-aligned) and reference count, ascending, for up to cap spans;
+ * *n = the number of live spans. Host only (no device call). */
+int  bt_host_pins(uint64_t* lo_hi_refs, uint32_t cap, uint32_t* n);
+
 #ifdef __cplusplus
 }
 #endif

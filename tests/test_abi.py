@@ -153,3 +153,16 @@ def test_reused_host_outputs_are_checked_and_viewed_per_call():
             abi._host_outputs(100, True, True, bad)
     with pytest.raises(ValueError):   # records given to a filter-only call
         abi._host_outputs(10, False, True, o)
+
+
+def test_reused_host_outputs_may_leave_out_unused_keys():
+    """A caller-built `outs` may omit the arrays the call does not write (no 'records' for a
+    filter-only call): the views are taken with .get, so that is not a KeyError."""
+    import numpy as np
+    o = abi.host_outputs(64, records=False)
+    del o["records"]
+    rec, ver, dec, pidx, npass = abi._host_outputs(64, False, True, o)
+    assert rec is None and len(dec) == 64 and len(ver) == 1
+    o2 = {"records": np.zeros((64, abi.BT_REC_BYTES), np.uint8)}   # parse-only: no filter keys at all
+    rec, ver, dec, pidx, npass = abi._host_outputs(64, True, False, o2)
+    assert rec.shape == (64, abi.BT_REC_BYTES) and ver is None and dec is None and pidx is None and npass is None

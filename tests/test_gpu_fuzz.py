@@ -51,20 +51,19 @@ def _check(out, dec, n, npass, where):
 class Arena:
     """A group's registered host buffers, registered once for the whole sweep (as a
     deployment registers its UMEM or ring once) and refilled every round: the capture is copied
-    in, the outputs are poisoned (0xFF) so that a byte the device did not write shows up.
-    BT_FUZZ_REGISTER_EACH=1 instead registers and unregisters each round's own arrays (the
-    round-5 sweeps' form; see DESIGN.md §5 for the one difference it showed)."""
+    in, the outputs are poisoned (0xFF) so that a byte the device did not write shows up. Only
+    with BT_FUZZ_ARENA=1; the default registers every round's own buffers (below)."""
     DATA = 128 << 20
     N = 70000
 
     def __init__(self, grp):
         self.grp = grp
         tiles = (self.N + 63) // 64
-        self.data = np.zeros(self.DATA, np.uint8)
-        self.desc = np.zeros(self.N, np.uint64)
-        self.rec = np.zeros(tiles * 6144, np.uint8)
-        self.dec = np.zeros(tiles * 64, np.uint8)
-        self.ver = np.zeros(tiles, np.uint64)
+        self.data = abi.host_array(self.DATA)
+        self.desc = abi.host_array(self.N, np.uint64)
+        self.rec = abi.host_array(tiles * 6144)
+        self.dec = abi.host_array(tiles * 64)
+        self.ver = abi.host_array(tiles, np.uint64)
         self.held = [self.data, self.desc, self.rec, self.dec, self.ver]
         for a in self.held:
             grp.register(a)
@@ -75,23 +74,30 @@ class Arena:
 
 
 def _mapped(grp, data, desc, n, records, arena=None):
+    """One mapped round. By default every buffer is the round's own: the capture and its
+    descriptors copied to fresh pages, fresh output pages poisoned with 0xFF, all registered
+    before the call and unregistered after it — thousands of registrations come and go at
+    recycled addresses over a sweep, the form round 5's one difference showed up in
+    (DESIGN.md §5). Registration is in whole pages, so each buffer has pages of its own
+    (abi.host_array)."""
     tiles = max(1, (n + 63) // 64)
     pidx = np.zeros(max(n, 1), np.uint32)
     npass = np.zeros(1, np.uint32)
     if arena is not None and data.nbytes <= Arena.DATA and n <= Arena.N:
         arena.data[:data.nbytes] = data
         arena.desc[:n] = desc[:n]
-        arena.dec.fill(0xFF)
-        arena.ver.fill(0xFFFFFFFFFFFFFFFF)
         data, desc = arena.data[:data.nbytes], arena.desc
         h_rec = arena.rec[:tiles * 6144] if records else None
         h_dec, h_ver = arena.dec[:tiles * 64], arena.ver[:tiles]
         held = []
     else:
-        h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
-        h_dec = np.zeros(tiles * 64, np.uint8)
-        h_ver = np.zeros(tiles, np.uint64)
+        data, desc = abi.host_copy(data), abi.host_copy(desc)
+        h_rec = abi.host_array(tiles * 6144) if records else None
+        h_dec = abi.host_array(tiles * 64)
+        h_ver = abi.host_array(tiles, np.uint64)
         held = [a for a in (data, desc, h_rec, h_dec, h_ver) if a is not None]
+    h_dec.fill(0xFF)
+    h_ver.fill(0xFFFFFFFFFFFFFFFF)
     for a in held:
         grp.register(a)
     try:
@@ -106,7 +112,7 @@ def _mapped(grp, data, desc, n, records, arena=None):
 
 
 def _arena(arenas, key, grp):
-    if os.environ.get("BT_FUZZ_REGISTER_EACH", "0") not in ("", "0"):
+    if os.environ.get("BT_FUZZ_ARENA", "0") in ("", "0"):
         return None
     if key not in arenas:
         arenas[key] = Arena(grp)

@@ -104,9 +104,12 @@ def _run_mapped(grp, base, desc, n, fmt=abi.DESC_PACKED, stride=0, records=True,
     """Registers the batch and the device-written outputs with the group, runs the mapped call,
     unregisters. Returns the outputs (records still in the tiled device layout)."""
     tiles = max(1, (n + 63) // 64)
-    h_rec = np.zeros(tiles * 6144, np.uint8) if records else None
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64) if verdict else None
+    # every registered buffer on pages of its own (registration is in whole pages)
+    base = abi.host_copy(base)
+    desc = None if desc is None else abi.host_copy(desc)
+    h_rec = abi.host_array(tiles * 6144) if records else None
+    h_dec = abi.host_array(tiles * 64)
+    h_ver = abi.host_array(tiles, np.uint64) if verdict else None
     pidx = np.full(max(n, 1), 0xFFFFFFFF, np.uint32)
     npass = np.zeros(1, np.uint32)
     held = [a for a in (base, desc, h_rec, h_dec, h_ver) if a is not None]
@@ -129,10 +132,11 @@ def _single_zero_copy(ctx, base, desc, n, fmt, filters):
     """The same batch through one context's bt_parse_filter_device (round 3's zero-copy path)."""
     ctx.compile(filters)
     tiles = max(1, (n + 63) // 64)
-    h_rec = np.zeros(tiles * 6144, np.uint8)
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64)
-    held = [base, desc, h_rec, h_dec, h_ver]
+    h_rec = abi.host_array(tiles * 6144)
+    h_dec = abi.host_array(tiles * 64)
+    h_ver = abi.host_array(tiles, np.uint64)
+    held = [abi.host_copy(base), abi.host_copy(desc), h_rec, h_dec, h_ver]
+    base = held[0]
     dev = [ctx.register(a) for a in held]
     try:
         ctx.run_device(abi.Batch(dev[0], dev[1], 0, n, base.nbytes, fmt, 0),
@@ -269,9 +273,10 @@ def test_group_mapped_fixed_stride_and_edges():
 def test_group_mapped_refuses_unregistered_and_bad_layouts():
     grp = _group(2)
     data, desc = synth.capture(synth.C3, 1000, seed=3)
+    data, desc = abi.host_copy(data), abi.host_copy(desc)
     try:
         grp.compile(C3_SET)
-        dec = np.zeros(1024, np.uint8)
+        dec = abi.host_array(1024)
         grp.register(data)
         grp.register(dec)
         with pytest.raises(abi.BtError) as e:    # descriptors not registered

@@ -270,6 +270,7 @@ def test_zero_copy_umem_ingest(gpu_ctx):
                {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
                {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
     gpu_ctx.compile(filters)
+    xdp = abi.host_copy(xdp)   # the RX ring on pages of its own, as the kernel maps it
     d_umem = gpu_ctx.register(umem)
     d_xdp = gpu_ctx.register(xdp)
     try:
@@ -295,9 +296,11 @@ def test_zero_copy_outputs(gpu_ctx):
     data, desc = synth.capture(synth.C4, n, seed=77)
     filters = [{"type": abi.BPF, "expr": "tcp", "priority": 1}]
     gpu_ctx.compile(filters)
-    h_rec = np.zeros(((n + 63) // 64) * 6144, np.uint8)
-    h_dec = np.zeros(n, np.uint8)
-    h_ver = np.zeros((n + 63) // 64, np.uint64)
+    # every registered buffer on pages of its own (registration is in whole pages)
+    data, desc = abi.host_copy(data), abi.host_copy(desc)
+    h_rec = abi.host_array(((n + 63) // 64) * 6144)
+    h_dec = abi.host_array(n)
+    h_ver = abi.host_array((n + 63) // 64, np.uint64)
     d_data, d_desc = gpu_ctx.register(data), gpu_ctx.register(desc)
     aliases = [gpu_ctx.register(x) for x in (h_rec, h_dec, h_ver)]
     try:

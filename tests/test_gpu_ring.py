@@ -24,13 +24,16 @@ CAPTURE_BIN = os.path.join(os.path.dirname(GOLDEN), "cpp", "test_capture")
 
 def _run_ring(ctx, ring, bs, nb, filters, records=True):
     """Register -> walk -> device run with outputs in registered host memory."""
+    ring = abi.host_copy(ring)   # on pages of its own, as the kernel maps a ring
     desc, taken = abi.ring_walk_tpv3(ring, bs, nb, ctx=ctx)
     assert taken == nb
     n = len(desc)
     tiles = (n + 63) // 64
-    h_rec = np.zeros(tiles * 6144, np.uint8)
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64)
+    # every registered buffer on pages of its own (registration is in whole pages)
+    desc = abi.host_copy(desc)
+    h_rec = abi.host_array(tiles * 6144)
+    h_dec = abi.host_array(tiles * 64)
+    h_ver = abi.host_array(tiles, np.uint64)
     ctx.compile(filters)
     held = [ring, desc, h_dec, h_ver] + ([h_rec] if records else [])
     dev = [ctx.register(a) for a in held]
@@ -113,14 +116,15 @@ def _run_gathered(ctx, ring, bs, nb, filters, dense=False, lean=False):
     (BT_BATCH_PREFIXES), slots and outputs in registered host memory."""
     wdesc, _ = abi.ring_walk_tpv3(ring, bs, nb, ctx=ctx)
     n = len(wdesc)
-    slots = np.full(n * abi.PREFIX_SLOT, 0xA5, np.uint8)   # poison past each prefix
-    gd = np.zeros(n, np.uint64)
+    slots = abi.host_array(n * abi.PREFIX_SLOT)   # own pages: registered below
+    slots.fill(0xA5)                               # poison past each prefix
+    gd = abi.host_array(n, np.uint64)
     desc, taken = abi.ring_gather_tpv3(ring, bs, nb, slots, gd, ctx=ctx, dense=dense, lean=lean)
     assert taken == nb and len(desc) == n
     tiles = (n + 63) // 64
-    h_rec = np.zeros(tiles * 6144, np.uint8)
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64)
+    h_rec = abi.host_array(tiles * 6144)
+    h_dec = abi.host_array(tiles * 64)
+    h_ver = abi.host_array(tiles, np.uint64)
     ctx.compile(filters)
     held = [slots, gd, h_dec, h_ver, h_rec]
     dev = [ctx.register(a) for a in held]

@@ -73,7 +73,9 @@ from beatrice_amd.numa import page_nodes, place_on  # noqa: E402
 
 
 def place(arr, node):
-    return place_on(arr, node, hugepages=a.hugepages)
+    out = place_on(arr, node, hugepages=a.hugepages)
+    # registration is in whole pages: a capture that may be registered gets pages of its own
+    return abi.host_copy(arr) if out is arr else out
 
 
 def data_node_for(placement):
@@ -122,13 +124,14 @@ if a.group:
                           "host_cpu_s_per_mpkt": round(cpu / (n / 1e6), 4), "cost_model": grp.cost(False, rec, True),
                           **where}), flush=True)
     tiles = (n + 63) // 64
-    h_dec = np.zeros(tiles * 64, np.uint8)
-    h_ver = np.zeros(tiles, np.uint64)
+    h_dec = abi.host_array(tiles * 64, np.uint8)
+    h_ver = abi.host_array(tiles, np.uint64)
+    desc = abi.host_copy(desc)
     for arr in (data, desc, h_dec, h_ver):
         grp.register(arr)
     for mode in ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
-        h_rec = np.zeros(tiles * 6144, np.uint8) if rec else None
+        h_rec = abi.host_array(tiles * 6144, np.uint8) if rec else None
         if rec:
             grp.register(h_rec)
         batch = abi.Batch(data.ctypes.data, desc.ctypes.data, 0, n, data.nbytes, abi.DESC_PACKED, 0)
@@ -156,19 +159,19 @@ if a.tpacket:
     B = a.ring_batch_blocks
     nbat = (used + B - 1) // B
     d_ring = ctx.register(ring)
-    h_desc = np.zeros(n + 64, np.uint64)
+    h_desc = abi.host_array(n + 64, np.uint64)
     d_desc = ctx.register(h_desc)
     if a.gather:
-        slots = np.zeros((n + 64) * abi.PREFIX_SLOT, np.uint8)
+        slots = abi.host_array((n + 64) * abi.PREFIX_SLOT, np.uint8)
         d_slots = ctx.register(slots)
     if a.gpu_walk:
         g_desc = ctx.alloc(8 * (n + 64))
     for mode in ("verdicts",) if a.lean else ("verdicts", "records+verdicts"):
         rec = mode != "verdicts"
         tiles = (n + 63) // 64 + nbat + 1          # each batch starts its outputs on a fresh tile
-        h_dec = np.zeros(tiles * 64, np.uint8)
-        h_ver = np.zeros(tiles, np.uint64)
-        h_rec = np.zeros(tiles * 6144, np.uint8) if rec else None
+        h_dec = abi.host_array(tiles * 64, np.uint8)
+        h_ver = abi.host_array(tiles, np.uint64)
+        h_rec = abi.host_array(tiles * 6144, np.uint8) if rec else None
         h_recs = np.zeros(n * 96, np.uint8) if rec and a.host_gather else None   # bt_rec, AoS
         d_dec, d_ver = ctx.register(h_dec), ctx.register(h_ver)
         d_rec = ctx.register(h_rec) if rec else None
@@ -277,6 +280,7 @@ if a.tpacket:
 
 if a.zero_copy:
     import numpy as np
+    desc = abi.host_copy(desc)
     d_data = ctx.register(data)
     d_desc = ctx.register(desc)
     n = a.packets
@@ -285,9 +289,9 @@ if a.zero_copy:
         run = abi.DeviceRun(ctx, np.zeros(256, np.uint8), None, n, stride=1, records=rec)
         run.batch = abi.Batch(d_data, d_desc, 0, n, data.nbytes, abi.DESC_PACKED, 0)
         # outputs come back to host memory: decisions + verdict words (+ records)
-        h_dec = np.zeros(n, np.uint8)
-        h_ver = np.zeros((n + 63) // 64, np.uint64)
-        h_rec = np.zeros(((n + 63) // 64) * 6144, np.uint8) if rec else None
+        h_dec = abi.host_array(n, np.uint8)
+        h_ver = abi.host_array((n + 63) // 64, np.uint64)
+        h_rec = abi.host_array(((n + 63) // 64) * 6144, np.uint8) if rec else None
         best = 1e9
         for _ in range(a.reps + 1):
             t0 = time.perf_counter()
