@@ -8,7 +8,7 @@
 #include <functional>
 #include <vector>
 
-#include "beatrice_gpu.h"
+#include "beatrice_gpu_bench.h"   // the product header + the harness entry points
 
 namespace bt {
 

@@ -71,6 +71,14 @@ uint32_t pin_spans(uint64_t* lo_hi_refs, uint32_t cap) {
 
 }  // namespace bt
 
+extern "C" int bt_host_alias(const void* host, uint64_t bytes, int device, void** alias) {
+    if (!host || !alias) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
+    uint8_t* a = nullptr;
+    if (int rc = bt::pin_alias(host, bytes, device, &a)) return rc;
+    *alias = a;
+    return BT_OK;
+}
+
 extern "C" int bt_host_pins(uint64_t* lo_hi_refs, uint32_t cap, uint32_t* n) {
     if (!n || (cap && !lo_hi_refs)) return bt::set_error(BT_E_INVALID_ARGUMENT, "null argument");
     *n = bt::pin_spans(lo_hi_refs, cap);

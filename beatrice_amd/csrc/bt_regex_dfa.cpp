@@ -45,7 +45,7 @@
 #include <string>
 #include <vector>
 
-#include "beatrice_gpu.h"
+#include "beatrice_gpu_bench.h"
 
 namespace {
 

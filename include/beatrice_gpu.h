@@ -368,10 +368,7 @@ typedef struct bt_placement {
     uint32_t reserved[4];
 } bt_placement;
 int  bt_context_placement(bt_ctx* ctx, bt_placement* out);
-/* Host-only helpers: the CPUs of NUMA node `node` this process may use (*n = 0 if none or
- * unknown; at most cap written), and the CPUs it may use at all (affinity set bounded by
- * the cgroup v2 quota). */
-int  bt_node_cpus(int node, int32_t* cpus, uint32_t cap, uint32_t* n);
+/* Host-only: the CPUs this process may use (affinity set bounded by the cgroup v2 quota). */
 uint32_t bt_usable_cpus(void);
 
 /* Compile the enabled filters: stable sort by priority (descending), parse each
@@ -383,9 +380,6 @@ int  bt_filter_program(const bt_ctx* ctx, bt_filter_slot* out, uint32_t cap, uin
  * the pool, a blob for bt_payload_dfa_eval): *bytes = the pool's size, min(cap, size) bytes
  * copied to out. For hosts that evaluate small batches on the CPU with the same program. */
 int  bt_filter_dfa_pool(const bt_ctx* ctx, void* out, uint32_t cap, uint32_t* bytes);
-/* host-only helper: compile without a context (no device needed) */
-int  bt_filter_compile_host(const bt_filter_desc* filters, uint32_t n,
-                            bt_filter_slot* out, uint32_t cap, uint32_t* n_slots);
 
 /* Pre-size the device workspace for batches of up to n packets (so later launches
  * never allocate, e.g. under hipGraph capture). */
@@ -449,25 +443,12 @@ int  bt_host_unregister(bt_ctx* ctx, void* host);
 /* ---- PAYLOAD filters on the GPU ---------------------------------
  * Replaces the per-packet std::regex construction + regex_search of
  * PacketFilter::applyPayloadFilter (src/PacketFilter.cpp:288-321) for the regular
- * subset of libstdc++'s ECMAScript grammar: the expression is compiled once to a byte
- * DFA that the kernel runs over the same <= 100-byte window after the IPv4 header.
- * bt_filter_compile does this for every PAYLOAD filter it can (BT_K_PAYLOAD slots, up
- * to 16 KiB of tables per program); the rest stay BT_K_HOST. The helpers below expose
- * the compiler and a host executor of the same DFA (tests, other hosts).
- *   bt_payload_dfa_compile  BT_OK (+ blob; blob == NULL: size only),
- *                           BT_E_INVALID_ARGUMENT if std::regex rejects the expression
- *                           (the reference's filter is then always false),
- *                           BT_E_NOT_IMPLEMENTED outside the modelled subset / too big,
- *                           BT_E_RESOURCE if cap is too small.
- *   bt_payload_dfa_search   regex_search(string(s, n), regex(expr)) for a compiled expr
- *   bt_payload_dfa_eval     applyPayloadFilter(frame, len) for a non-empty expression */
-int  bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size);
-/* The same with options: BT_DFA_NO_PAIRS leaves out the optional two-byte table (the
- * compiler adds it when it is <= 4 KiB; the filter compiler drops it when a program's
- * tables would not fit the 16 KiB pool otherwise). */
-#define BT_DFA_NO_PAIRS 0x1u
-int  bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob, uint32_t cap, uint32_t* size);
-int  bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);
+ * subset of libstdc++'s ECMAScript grammar: bt_filter_compile compiles every PAYLOAD
+ * expression it can once (BT_K_PAYLOAD slots, up to 16 KiB of tables per program); the
+ * rest stay BT_K_HOST. The compiler itself is in include/beatrice_gpu_bench.h.
+ *   bt_payload_dfa_eval  applyPayloadFilter(frame, len) on the host with a compiled slot's
+ *                        blob (bt_filter_dfa_pool): the C++ filter's continuation of a
+ *                        chain the device handed over */
 int  bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len);
 
 /* ---- capture-ring ingest: AF_PACKET TPACKET_V3 ---------------
@@ -497,19 +478,11 @@ typedef struct bt_tpv3_ring {
 int  bt_ring_walk_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block,
                        uint32_t max_blocks, bt_pkt_desc* desc, uint32_t cap,
                        uint32_t* n_desc, uint32_t* n_blocks_taken);
-/* The same walk, and each frame's header prefix is also copied into slot i of `slots`
- * (BT_PREFIX_SLOT bytes per frame, slot i at i * BT_PREFIX_SLOT): the bytes the layer walk
- * and the built-in filters read, i.e. max(38, the walked header end) rounded up to 16, at
- * most the frame. desc[i] = BT_DESC(i * BT_PREFIX_SLOT, min(tp_snaplen, 65535)). A batch
- * over `slots` (registered, or copied to the device) with flags = BT_BATCH_PREFIXES then
- * reads one aligned 64-B host line per packet over PCIe for headers up to 64 B, instead
- * of a window straddling the ring's 2-mod-16 frame starts. The walker copies while its
- * chains are in flight, one frame behind each chain's header read. */
 #define BT_PREFIX_SLOT 128u
-int  bt_ring_gather_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
-                         uint8_t* slots, bt_pkt_desc* desc, uint32_t cap, uint32_t* n_desc,
-                         uint32_t* n_blocks_taken);
-/* The same gather with the prefixes packed: the frames of the k-th taken block (whose first
+/* Header-prefix gathers: BT_PREFIX_SLOT bytes of `slots` per taken frame (the slot form,
+ * bt_ring_gather_tpv3, is in include/beatrice_gpu_bench.h). A batch over `slots`
+ * (registered, or copied to the device) runs with flags = BT_BATCH_PREFIXES.
+ * The walk with each frame's header prefix packed: the frames of the k-th taken block (whose first
  * descriptor is j_k) go back to back, each 16-B aligned and taking its prefix length rounded
  * up to 16, from byte j_k * BT_PREFIX_SLOT of `slots` (16-B aligned, BT_PREFIX_SLOT * cap
  * bytes, as above); desc[i] = BT_DESC(offset of frame i's prefix, min(tp_snaplen, 65535)),
@@ -530,18 +503,6 @@ int  bt_ring_gather_dense_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t f
 int  bt_ring_gather_lean_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t max_blocks,
                               uint8_t* slots, bt_pkt_desc* desc, bt_pkt_desc* ring_desc, uint32_t cap,
                               uint32_t* n_desc, uint32_t* n_blocks_taken);
-/* The walk with the frame chains followed on the GPU. The host reads only the taken blocks'
- * headers (block_status, num_pkts, offset_to_first_pkt: one line per block) and a kernel on
- * `stream` walks every chain through ring_dev (the ring's device-visible alias, e.g. from
- * bt_host_register), one lane per block, writing the descriptors (as bt_ring_walk_tpv3
- * does) into desc_dev, device memory of cap entries. *n_desc and *n_blocks_taken are known
- * on return, the descriptors once the stream has run the kernel; batches on the same
- * stream that read desc_dev follow it in order. A chain that leaves its block makes that
- * block's remaining descriptors empty (length 0: nothing of them is read) and stores
- * block + 1 into *bad_dev (device memory, optional; the largest such block wins). */
-int  bt_ring_walk_tpv3_gpu(bt_ctx* ctx, const bt_tpv3_ring* ring, const void* ring_dev, uint32_t first_block,
-                           uint32_t max_blocks, bt_pkt_desc* desc_dev, uint32_t cap, uint32_t* n_desc,
-                           uint32_t* n_blocks_taken, uint32_t* bad_dev, void* stream);
 /* Hands `count` blocks starting at first_block back to the kernel (TP_STATUS_KERNEL,
  * release-ordered). Call it once the device has finished reading them. */
 int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);
@@ -567,45 +528,6 @@ int      bt_group_parse_filter(bt_group* group, const uint8_t* base, const bt_pk
 int      bt_group_parse_filter_ptrs(bt_group* group, const uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                                     bt_rec* records, uint64_t* verdict, uint8_t* decide, uint32_t* pass_idx,
                                     uint32_t* n_pass);
-/* The split (host only): bounds[0..parts] with bounds[0] = 0, bounds[parts] = n, every
- * inner bound a multiple of 64, member k taking [bounds[k], bounds[k+1]); balanced by the
- * cost min(len, 128) + 8 + 96 bytes per packet (beatrice_amd/shard.py:shard_bounds). */
-int      bt_group_split(const uint32_t* lens, uint32_t n, uint32_t parts, uint32_t* bounds);
-/* The same with a cost model: packet cost = round_up(min(len, window), align) + fixed.
- * The group's calls weigh packets by what each call moves (bt_group_cost). */
-typedef struct bt_split_cost {
-    uint32_t window;               /* bytes of each frame the call reads / stages         */
-    uint32_t align;                /* ... rounded up to this (1 = exact)                  */
-    uint32_t fixed;                /* per-packet bytes independent of the length          */
-    uint32_t reserved;
-} bt_split_cost;
-int      bt_group_split_cost(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
-                             uint32_t* bounds);
-/* The split the group's calls use: bt_group_split_cost up to 4096 tiles; above, the cost of
- * one tile in every S (~4096 samples) stands for its run of S tiles and the cuts interpolate
- * within a run (an exact pass over 16M descriptors took ~45 ms on one thread before any
- * member started). Same form of bounds. */
-int      bt_group_split_plan(const uint32_t* lens, uint32_t n, uint32_t parts, const bt_split_cost* cost,
-                             uint32_t* bounds);
-/* The cost model a group call uses (mapped: bt_group_parse_filter_mapped, else the host
- * batches), for a call that asks for records / filter outputs, with desc_bytes-byte
- * descriptors (8 packed, 16 xdp_desc, 0 fixed stride):
- *   host batches: window = the bytes staged per frame (32: a filter-only call stages frame
- *                 bytes 12..43; 112 with records; 176 with a GPU PAYLOAD slot), align 16,
- *                 fixed = desc_bytes + 96 (records, bt_rec D2H) + 1 (decision D2H)
- *   mapped:       window = 128 with records (the walk's wide window) else 48 (the lean
- *                 first round reads frame bytes 12..37: two or three 16-B chunks by the
- *                 frame's alignment, 32 B + one chunk of slack), align 16, fixed =
- *                 desc_bytes + 64 (records: packed slabs) + 1 (decision) — all of it PCIe
- *                 traffic of the member's link. */
-int      bt_group_cost(bt_group* group, int mapped, int records, int filters, uint32_t desc_bytes,
-                       bt_split_cost* out);
-/* Host threads per member: `requested` (opts.host_threads, else BT_HOST_THREADS; 0 = auto)
- * is the whole group's budget, split evenly (at least 1, at most 16 each); auto gives each
- * member usable / members, at least 1 and at most 16 (one context alone: min(16, usable), the
- * single-context default; a context's host pipeline takes at most 8 of them while other callers
- * wait for the context). Host only; bt_group_create applies it. */
-int      bt_group_thread_budget(uint32_t members, uint32_t usable, uint32_t requested, uint32_t* per_member);
 /* bt_host_parallel over the whole group's host threads: fn(user, w, workers) runs once for
  * every w in [0, workers), workers = the members' pool sizes summed (member k's pool, on its
  * NUMA node, takes a contiguous range of w); returns when all have. For host-side work on a
@@ -731,14 +653,11 @@ int  bt_format_records_to(bt_ctx* ctx, const bt_rec* recs, uint32_t n, uint32_t 
 
 /* host-side record gather from the device layout (after a D2H copy) */
 void bt_record_gather(const void* records, uint32_t n_cap, uint32_t i, bt_rec* out);
-void bt_record_gather_planes(const void* planes, uint32_t n_cap, uint32_t i, bt_rec* out);
 /* All n records at once (planes != 0: plane-major), on ctx's host threads (ctx may be
  * NULL); *slabs (optional) gets the total of slabs the device stored. out == NULL with
  * slabs != NULL only counts (reads slab 1 of each record). */
 int  bt_record_unpack(bt_ctx* ctx, const void* records, uint32_t n_cap, uint32_t n, uint32_t planes, bt_rec* out,
                       uint64_t* slabs);
-/* Slabs the packed device form of this record occupies (2..6). */
-uint32_t bt_record_slabs(const bt_rec* r);
 
 #ifdef __cplusplus
 }

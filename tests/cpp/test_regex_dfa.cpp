@@ -26,7 +26,7 @@
 #include <string>
 #include <vector>
 
-#include "beatrice_gpu.h"
+#include "beatrice_gpu_bench.h"
 
 extern "C" int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size);
 extern "C" int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);

@@ -39,7 +39,7 @@ def _seed():
 
 def _check(out, dec, n, npass, where):
     bad = np.nonzero(out["decide"][:n] != dec)[0]
-    assert len(bad) == 0, f"{where}: {len(bad)} decisions differ, first {bad[:5]}"
+    assert len(bad) == 0, f"{where}: {len(bad)} decisions differ, first {bad[:5]}; evidence {out.get('evidence')}"
     if out.get("verdict") is not None:
         bits = np.unpackbits(out["verdict"].view(np.uint8), bitorder="little")[:n].astype(bool)
         assert np.array_equal(bits, (dec >> 6) == 0), f"{where}: verdict words"
@@ -73,7 +73,46 @@ class Arena:
             self.grp.unregister(a)
 
 
-def _mapped(grp, data, desc, n, records, arena=None):
+def _ranges(mask):
+    idx = np.nonzero(mask)[0]
+    if not len(idx):
+        return []
+    cuts = np.nonzero(np.diff(idx) > 1)[0]
+    return [(int(s), int(e) + 1) for s, e in zip(np.concatenate([[idx[0]], idx[cuts + 1]]),
+                                               np.concatenate([idx[cuts], [idx[-1]]]))][:8]
+
+
+def _evidence(ctx, grp, batch, outs, data, desc, h_dec, h_ver, expect, n):
+    """A mapped round whose decisions differ, examined while its buffers are still registered:
+    the same call again, and the device's own copy (extract kernel, through the alias the mapped
+    kernels read) of the capture and of its descriptors, compared with the host bytes."""
+    import ctypes
+    ev = {"first_bad": np.nonzero(h_dec[:n] != expect)[0][:12].tolist(),
+          "got": h_dec[np.nonzero(h_dec[:n] != expect)[0][:12]].tolist()}
+    h_dec.fill(0xFF)
+    h_ver.fill(0xFFFFFFFFFFFFFFFF)
+    grp.run_mapped(batch, outs)
+    ev["rerun_bad"] = int(np.count_nonzero(h_dec[:n] != expect))
+    for name, arr in (("data", data), ("desc", desc.view(np.uint8))):
+        nb = arr.nbytes // 256 * 256
+        if not nb:
+            continue
+        al = ctypes.c_void_p(0)
+        if abi.lib().bt_host_alias(arr.ctypes.data, nb, 0, ctypes.byref(al)) != 0:
+            ev[name] = "no alias"
+            continue
+        ex = abi.DeviceExtract(ctx, None, None, nb // 256, [(0, 256, abi.FT_BYTES, 0)],
+                               batch=abi.Batch(al.value, None, 256, nb // 256, nb, 0, 0))
+        ex.run()
+        img = ex.fetch()[2].reshape(-1)
+        ex.free()
+        diff = img[:nb] != arr[:nb]
+        ev[name] = {"host": hex(arr.ctypes.data), "alias": hex(al.value), "bytes_differ": int(diff.sum()),
+                    "ranges": _ranges(diff), "device_zero_frac": float((img[:nb][diff] == 0).mean()) if diff.any() else None}
+    return ev
+
+
+def _mapped(grp, data, desc, n, records, arena=None, expect=None, ctx=None):
     """One mapped round. By default every buffer is the round's own: the capture and its
     descriptors copied to fresh pages, fresh output pages poisoned with 0xFF, all registered
     before the call and unregistered after it — thousands of registrations come and go at
@@ -100,15 +139,21 @@ def _mapped(grp, data, desc, n, records, arena=None):
     h_ver.fill(0xFFFFFFFFFFFFFFFF)
     for a in held:
         grp.register(a)
+    batch = abi.Batch(data.ctypes.data, desc.ctypes.data, 0, n, data.nbytes, abi.DESC_PACKED, 0)
+    outs = abi.Outputs(None if h_rec is None else h_rec.ctypes.data, n, h_ver.ctypes.data,
+                       h_dec.ctypes.data, pidx.ctypes.data, npass.ctypes.data)
+    evidence = None
     try:
-        grp.run_mapped(abi.Batch(data.ctypes.data, desc.ctypes.data, 0, n, data.nbytes, abi.DESC_PACKED, 0),
-                       abi.Outputs(None if h_rec is None else h_rec.ctypes.data, n, h_ver.ctypes.data,
-                                   h_dec.ctypes.data, pidx.ctypes.data, npass.ctypes.data))
+        grp.run_mapped(batch, outs)
+        out = {"decide": h_dec[:n].copy(), "verdict": h_ver.copy(), "pass_idx": pidx[:int(npass[0])].copy(),
+               "n_pass": int(npass[0]), "records": abi.untile_records(h_rec, n) if records else None}
+        if expect is not None and ctx is not None and not np.array_equal(out["decide"], expect):
+            evidence = _evidence(ctx, grp, batch, outs, data, desc, h_dec, h_ver, expect, n)
     finally:
         for a in held:
             grp.unregister(a)
-    return {"decide": h_dec[:n].copy(), "verdict": h_ver.copy(), "pass_idx": pidx[:int(npass[0])],
-            "n_pass": int(npass[0]), "records": abi.untile_records(h_rec, n) if records else None}
+    out["evidence"] = evidence
+    return out
 
 
 def _arena(arenas, key, grp):
@@ -167,7 +212,8 @@ def test_randomized_parity_sweep():
                     groups[m] = abi.Group([0] * m, flags=abi.OPT_GROUP_SHARED_DEVICE if m > 1 else 0)
                 grp = groups[m]
                 grp.compile(prog)
-                out = (_mapped(grp, data, desc, n, records, _arena(arenas, m, grp)) if form == "mapped"
+                out = (_mapped(grp, data, desc, n, records, _arena(arenas, m, grp), expect=dec, ctx=ctx)
+                       if form == "mapped"
                        else grp.run_host(data, desc, records=records))
             _check(out, dec, n, npass, where)
             if records:

@@ -11,7 +11,7 @@
 #include <vector>
 #include <string>
 
-#include "beatrice_gpu.h"
+#include "beatrice_gpu_bench.h"
 
 extern "C" uint64_t bt_synth_layout(int cfg, uint64_t n, uint64_t seed, uint64_t* desc);
 extern "C" int bt_synth_fill(int cfg, uint64_t n, uint64_t seed, const uint64_t* desc, uint8_t* data, int nthreads);
