@@ -78,6 +78,7 @@ OPT_GROUP_SHARED_DEVICE = 0x4000
 OPT_NO_LEAN_PCIE = 0x8000
 OPT_MAPPED_GATHER_SPARSE = 0x10000
 OPT_NO_LEAN_HOST = 0x20000
+OPT_PAYLOAD_DFA = 0x40000
 TIME_KERNEL_EVENTS = 0x1
 TIME_PIPELINED = 0x2
 

@@ -279,13 +279,127 @@ __device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s
 // is done): <= 8 16-B loads, 4 in flight at a time (all 8 would cost the variant a
 // wave of occupancy). The walk is one dependent LDS read per byte (C == 256) or two
 // (byte classes); the sinks K (match) / K+1 (none possible) end it early.
+
+__device__ uint4 g_zero16[8];                    // source of the loads that read nothing
+
+// A lane's payload window loaded ahead (bt_parse_filter_pipe issues the loads before the
+// tile's parse, so their latency hides behind it): the 16-B chunks from the window's aligned
+// start, and the window's offset in the first one. nch = 0: nothing was loaded (the lane does
+// not reach a PAYLOAD slot, or has no window).
+struct PayWin {
+    uint4 v[8];
+    uint32_t sh, nch;
+};
+
+// applyPayloadFilter's window of a frame (eval_payload's gates): its start offset in the
+// frame (po) and length L; L = 0 when the filter returns false without a search.
+__device__ __forceinline__ uint32_t payload_window(uint32_t len, const uint32_t* w0, uint32_t& po) {
+    po = 14u + (byte_of(w0, 14) & 15u) * 4u;
+    if (!(len >= 34u && be16_of(w0, 12) == 0x0800u) || len <= po) return 0u;
+    return min(len - po, 100u);
+}
+
+__device__ __forceinline__ void issue_payload_loads(const MainArgs& a, uint64_t frame_off, uint32_t len,
+                                                    const uint32_t* w0, bool want, PayWin& pw) {
+    uint32_t po = 0;
+    const uint32_t L = want ? payload_window(len, w0, po) : 0u;
+    const uint64_t start = frame_off + po;
+    const uint64_t al = start & ~15ull;
+    pw.sh = (uint32_t)(start & 15ull);
+    pw.nch = L ? (pw.sh + L + 15u) >> 4 : 0u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
+#pragma unroll
+    for (uint32_t h = 0; h < 8u; h += 4u) {
+        if (__ballot(pw.nch > h) != 0ull) {   // wave-uniform: a group only when some lane needs it
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) {
+                const uint64_t g = al + 16ull * (h + k);
+                const bool ok = (h + k < pw.nch) & (g + 16ull <= a.bytes);
+                pw.v[h + k] = ld16(ok ? a.base + g : zero, a.nt & 2u);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) pw.v[h + k] = make_uint4(0, 0, 0, 0);
+        }
+    }
+}
+
+// The bit-parallel form (bt_regex_dfa.cpp "AST -> bit-parallel form"; blob layout there): an
+// extended Shift-And over the position set D. The loop takes four window bytes per turn
+// from the lane's LDS row (where eval_payload put the window) and runs until every lane of
+// the wave has matched or passed its window (wave-uniform exit, no divergence inside); the
+// row dwords two turns ahead and the table entries of the next four bytes are read before
+// this turn's state steps, which are then only shift / or / and on registers. Entries are 1,
+// 2, 4 or 8 bytes (the positions rounded up), so a small pattern's 256-entry table spans
+// few distinct dwords per LDS bank (1-byte entries: at most 2 per bank, 4-byte: 8). A byte
+// past the window (pos >= L) gets an empty mask: the partial matches of a SIMPLE pattern end
+// there, and the others hold D ($ reads D at the window's end). Returns regex_search's answer
+// over the L bytes.
+template <typename E, bool SIMPLE>
+__device__ __forceinline__ uint32_t bitpar_walk(const uint8_t* blob, const uint32_t* row, uint32_t staged_sh,
+                                                uint32_t L) {
+    using T = typename std::conditional<sizeof(E) == 8, uint64_t, uint32_t>::type;
+    const uint64_t* mk = reinterpret_cast<const uint64_t*>(blob + 16);
+    const T Iall = (T)mk[0], F = (T)mk[5];
+    const E* B = reinterpret_cast<const E*>(blob + 80);
+    const uint32_t* r = row + (staged_sh >> 2);
+    const uint32_t sh = staged_sh & 3u, rmax = 31u - (staged_sh >> 2);   // r[] stays inside the 33-dword row
+    // the general form's masks (SIMPLE: none of them is used)
+    const T I0 = SIMPLE ? (T)0 : (T)mk[1], S = SIMPLE ? (T)0 : (T)mk[2], A = SIMPLE ? (T)0 : (T)mk[3];
+    const T NF = SIMPLE ? ~(T)0 : (T)mk[4], Fe = SIMPLE ? (T)0 : (T)mk[6];
+    const uint32_t R = SIMPLE ? 0u : blob[7];
+    const bool anchored_all = !SIMPLE && (*reinterpret_cast<const uint32_t*>(blob + 8) & 4u) != 0u;
+    T D = 0, hit = 0, inj = Iall | I0;
+    auto step = [&](T b, uint32_t pos) {
+        if constexpr (SIMPLE) {
+            D = ((D << 1) | Iall) & (pos < L ? b : (T)0);
+            hit |= D & F;
+        } else {
+            T n = (((D << 1) & NF) | inj | (D & S)) & b;
+            inj = Iall;
+            for (uint32_t k = 0; k < R; ++k) n |= (n << 1) & A;
+            D = pos < L ? n : D;
+            hit |= D & F;
+        }
+    };
+    uint32_t t0 = r[0], t1 = r[1];
+    uint32_t w = __builtin_amdgcn_alignbyte(t1, t0, sh);
+    t0 = t1;
+    t1 = r[2];
+    T b0 = B[w & 0xFFu], b1 = B[(w >> 8) & 0xFFu], b2 = B[(w >> 16) & 0xFFu], b3 = B[w >> 24];
+    for (uint32_t i = 0;; i += 4u) {
+        // the next turn's bytes and entries, ahead of this turn's steps
+        const uint32_t wn = __builtin_amdgcn_alignbyte(t1, t0, sh);
+        t0 = t1;
+        t1 = r[min((i >> 2) + 3u, rmax)];
+        const T n0 = B[wn & 0xFFu], n1 = B[(wn >> 8) & 0xFFu], n2 = B[(wn >> 16) & 0xFFu], n3 = B[wn >> 24];
+        step(b0, i);
+        step(b1, i + 1u);
+        step(b2, i + 2u);
+        step(b3, i + 3u);
+        if (__ballot(!hit && i + 4u < L && (SIMPLE || D || !anchored_all)) == 0ull) break;
+        b0 = n0; b1 = n1; b2 = n2; b3 = n3;
+    }
+    return (hit || (D & Fe)) ? 1u : 0u;
+}
+
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
-                                                 uint32_t& staged_sh) {
-    if (!(len >= 34u && be16_of(w0, 12) == 0x0800u)) return 0u;
-    const uint32_t po = 14u + (byte_of(w0, 14) & 15u) * 4u;
-    if (len <= po) return 0u;
-    const uint32_t L = min(len - po, 100u);
+                                                 uint32_t& staged_sh, const PayWin* pre) {
+    uint32_t po;
+    const uint32_t L = payload_window(len, w0, po);
+    if (!L) return 0u;
+    const uint32_t K = *reinterpret_cast<const uint16_t*>(blob);
+    if (K == 0xFFFFu && blob[6] != 1u) return blob[6] == 2u ? 1u : 0u;   // bit-parallel: always / never
+    if (staged_sh == ~0u && pre) {   // loaded ahead: into the row (free once PARSE is done)
+        staged_sh = pre->sh;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k)
+            if (k < pre->nch) {
+                uint32_t* d = row + 4u * k;
+                d[0] = pre->v[k].x; d[1] = pre->v[k].y; d[2] = pre->v[k].z; d[3] = pre->v[k].w;
+            }
+    }
     if (staged_sh == ~0u) {
         const uint64_t start = frame_off + po;
         const uint64_t al = start & ~15ull;
@@ -308,7 +422,19 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
             }
         }
     }
-    const uint32_t K = *reinterpret_cast<const uint16_t*>(blob);
+    if (K == 0xFFFFu) {   // the bit-parallel form (wave-uniform: the slot's blob)
+        const uint32_t W = *reinterpret_cast<const uint16_t*>(blob + 2);
+        const bool simple = *reinterpret_cast<const uint32_t*>(blob + 8) == 0u && blob[7] == 0u;
+        switch (W) {
+        case 8: return simple ? bitpar_walk<uint8_t, true>(blob, row, staged_sh, L)
+                              : bitpar_walk<uint8_t, false>(blob, row, staged_sh, L);
+        case 16: return simple ? bitpar_walk<uint16_t, true>(blob, row, staged_sh, L)
+                               : bitpar_walk<uint16_t, false>(blob, row, staged_sh, L);
+        case 32: return simple ? bitpar_walk<uint32_t, true>(blob, row, staged_sh, L)
+                               : bitpar_walk<uint32_t, false>(blob, row, staged_sh, L);
+        default: return bitpar_walk<uint64_t, false>(blob, row, staged_sh, L);
+        }
+    }
     const uint32_t C = *reinterpret_cast<const uint16_t*>(blob + 2);
     uint32_t q = blob[4];
     if (q >= K) return q == K ? 1u : 0u;
@@ -397,7 +523,8 @@ __device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
 template <int F>
 __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const HotProgram& hot,
                                                   const uint8_t* dfa_lds, uint32_t* lrow, uint64_t my_off,
-                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot) {
+                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot,
+                                                  const PayWin* pre = nullptr) {
     const FilterIn x = filter_in([w0](uint32_t i) { return byte_of(w0, (int)i); }, len);
     uint32_t code = BT_DECIDE_PASS;
     slot = prog.n ? prog.n - 1u : 0u;
@@ -448,7 +575,7 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
         uint32_t r;
         if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
             r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
-              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh) : 0u;
+              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh, pre) : 0u;
         else
             r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
         if (open && r != 1u) {
@@ -460,7 +587,6 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
     return code;
 }
 
-__device__ uint4 g_zero16[8];                    // source of the loads that read nothing
 
 // Header windows of one 64-packet tile in flight in registers (LOAD stage).
 //  fixed stride: the tile is one contiguous span, cpp 16-B chunks per packet;
@@ -1048,6 +1174,16 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
     const HotProgram hot = hot_program(prog);
     bool wide = false;
+    // the first PAYLOAD slot: the lanes that reach it get their payload windows loaded ahead
+    uint32_t pay_first = ~0u;
+    if constexpr (FILTER == 2) {
+        if (!a.prefixes)
+            for (uint32_t f = 0; f < prog.n; ++f)
+                if (prog.f[f].kind == BT_K_PAYLOAD) {
+                    pay_first = f;
+                    break;
+                }
+    }
 
     // prologue: descriptors of t and t + step, round A of t (waited), then stand-ins for
     // a tile's stores so the first iteration's waits count like every later one's
@@ -1071,6 +1207,21 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         window<10>(row, s, w0);
         if (REC != kRecNone)   // round B, before the next tile's loads
             wide = round_b(a, t, lane, st.qa0, img, row, s, my_off, my_len, live, st.wide, need_max, w0);
+
+        // The payload windows of the lanes whose chain reaches the first PAYLOAD slot (the
+        // slots before it pass), loaded now: they arrive while this tile parses and its
+        // record stores issue (issued after the filter, each window cost a full memory round
+        // trip per tile: C3 with /GET|POST/ first 1.35 against 0.49 ms without the slot).
+        PayWin pw;
+        if constexpr (FILTER == 2) {
+            bool want = live && pay_first != ~0u;
+            if (__ballot(want) != 0ull) {
+                const FilterIn x = filter_in([&w0](uint32_t i) { return byte_of(w0, (int)i); }, my_len);
+                for (uint32_t f = 0; f < pay_first; ++f)
+                    want = want && eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x) == 1u;
+            }
+            issue_payload_loads(a, my_off, live ? my_len : 0u, w0, want, pw);
+        }
 
         // next tile: round A from the descriptors loaded one tile ago, then the
         // descriptors of the tile after it
@@ -1104,7 +1255,8 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live,
+                                                        slot, FILTER == 2 ? &pw : nullptr);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);

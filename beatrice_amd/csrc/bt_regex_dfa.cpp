@@ -622,6 +622,264 @@ uint32_t blob_size(const Packed& p) {
     return n;
 }
 
+// ------------------------------------------------------------------ AST -> bit-parallel form
+//
+// Most payload patterns are a union of linear sequences: byte classes one after another,
+// each maybe optional (?) and/or repeatable (+ *), the union maybe anchored at either end —
+// "GET|POST", "(?:GET|HEAD) /[^ ]* HTTP" (two sequences once the group is distributed),
+// "Host: [a-z0-9.-]+\.com", "^.{0,5}$". Such a union is searched with an extended
+// Shift-And over <= 64 positions, one bit per class occurrence (Navarro & Raffinot,
+// "Flexible Pattern Matching in Strings", ch. 4): per byte c
+//     D = (((D << 1) & NF) | inject | (D & S)) & B[c]      then  D |= (D << 1) & A, R times
+// where B[c] marks the positions whose class holds c, S the repeatable ones, A the optional
+// ones (the closure skips runs of up to R of them), inject the start of every sequence (at
+// every byte; at byte 0 only for ^-anchored ones) and NF clears the first bit of anchored
+// sequences so the previous sequence's last bit cannot leak into it. A match ends where a
+// sequence's last bit is set (a $-anchored one only after the last byte). The masks B[c]
+// depend on the byte alone, so the kernel fetches them ahead and the state chain is a few
+// ALU operations per byte instead of a dependent table read.
+//
+// Blob (16-B aligned like every pool blob; little endian):
+//   u16 0xFFFF (no DFA has that many states), u16 W (8 / 16 / 32 / 64: the positions rounded
+//   up; the width of a table entry, so small patterns read 1- or 2-byte entries, whose
+//   256-entry table spans fewer LDS banks' worth of distinct dwords)
+//   u8 0, u8 empty (match on the empty input), u8 form (1 search, 2 always true, 3 never),
+//   u8 R (closure steps)
+//   u32 flags: 1 S != 0, 2 some sequence ^-anchored, 4 every sequence ^-anchored, 8 Fe != 0
+//   u32 0
+//   u64 Iall, I0, S, A, NF, F, Fe      (I0 = the extra starts at byte 0)
+//   u64 pad
+//   B[256]: W-bit entries at byte 80
+constexpr uint16_t kBitparMagic = 0xFFFF;
+constexpr uint32_t kBitparHeader = 80;
+constexpr int kBitparMaxSeqs = 64;
+constexpr int kBitparMaxR = 8;
+
+struct Item {
+    enum K : uint8_t { SET, BOL, EOL } k = SET;
+    int set = -1;   // index into Bitpar::sets
+    bool opt = false, rep = false;
+};
+using Seqs = std::vector<std::vector<Item>>;
+
+struct Bitpar {
+    const std::vector<Node>& ast;
+    std::vector<Set> sets;
+    explicit Bitpar(const std::vector<Node>& a) : ast(a) {}
+
+    static Seqs product(const Seqs& a, const Seqs& b) {
+        if (a.size() * b.size() > (size_t)kBitparMaxSeqs) throw Unsupported{};
+        Seqs r;
+        for (const auto& x : a)
+            for (const auto& y : b) {
+                r.push_back(x);
+                r.back().insert(r.back().end(), y.begin(), y.end());
+                if (r.back().size() > 64) throw Unsupported{};
+            }
+        return r;
+    }
+
+    Seqs expand(int id) {
+        const Node& n = ast[id];
+        switch (n.t) {
+        case Node::SET: {
+            Item it;
+            it.set = (int)sets.size();
+            sets.push_back(n.set);
+            return {{it}};
+        }
+        case Node::EMPTY: return {{}};
+        case Node::BOL: case Node::EOL: {
+            Item it;
+            it.k = n.t == Node::BOL ? Item::BOL : Item::EOL;
+            return {{it}};
+        }
+        case Node::CAT: {
+            Seqs r{{}};
+            for (int k : n.kids) r = product(r, expand(k));
+            return r;
+        }
+        case Node::ALT: {
+            Seqs r;
+            for (int k : n.kids) {
+                Seqs e = expand(k);
+                r.insert(r.end(), e.begin(), e.end());
+                if (r.size() > (size_t)kBitparMaxSeqs) throw Unsupported{};
+            }
+            return r;
+        }
+        case Node::REP: {
+            const Seqs k = expand(n.kids[0]);
+            for (const auto& s : k)
+                for (const Item& it : s)
+                    if (it.k != Item::SET) throw Unsupported{};   // a repeated assertion
+            if (k.size() == 1 && k[0].size() == 1) {   // one class occurrence: copies of it
+                const Item x = k[0][0];
+                std::vector<Item> s;
+                if (n.hi < 0) {
+                    for (int c = 0; c + 1 < std::max(n.lo, 1); ++c) s.push_back(x);
+                    Item last = x;
+                    last.rep = true;
+                    if (n.lo == 0) last.opt = true;
+                    s.push_back(last);
+                } else {
+                    for (int c = 0; c < n.hi; ++c) {
+                        Item y = x;
+                        if (c >= n.lo) y.opt = true;
+                        s.push_back(y);
+                    }
+                }
+                if (s.size() > 64) throw Unsupported{};
+                return {s};
+            }
+            if (n.hi < 0) throw Unsupported{};   // (ab)* and the like: the DFA's
+            Seqs r;
+            for (int cnt = n.lo; cnt <= n.hi; ++cnt) {
+                Seqs c{{}};
+                for (int j = 0; j < cnt; ++j) c = product(c, k);
+                r.insert(r.end(), c.begin(), c.end());
+                if (r.size() > (size_t)kBitparMaxSeqs) throw Unsupported{};
+            }
+            return r;
+        }
+        }
+        throw Unsupported{};
+    }
+};
+
+struct BitparBlob {
+    int W = 32, form = 1, R = 0, empty = 0;
+    uint32_t flags = 0;
+    uint64_t Iall = 0, I0 = 0, S = 0, A = 0, NF = ~0ull, F = 0, Fe = 0;
+    uint64_t B[256] = {};
+};
+
+BitparBlob build_bitpar(const std::string& pattern) {
+    Parser ps(pattern);
+    const int root = ps.parse();
+    Bitpar bp(ps.nodes);
+    const Seqs all = bp.expand(root);
+    struct Lin {
+        std::vector<Item> e;   // classes only
+        bool bol = false, eol = false;
+    };
+    std::vector<Lin> keep;
+    BitparBlob o;
+    for (const auto& s : all) {
+        // where the assertions stand: ^ must come before every class, $ after every one
+        Lin l;
+        bool impossible = false;
+        for (int i = 0; i < (int)s.size(); ++i) {
+            if (s[i].k == Item::SET) continue;
+            bool mand_before = false, mand_after = false, any_before = false, any_after = false;
+            for (int j = 0; j < i; ++j)
+                if (s[j].k == Item::SET) { any_before = true; mand_before |= !s[j].opt; }
+            for (int j = i + 1; j < (int)s.size(); ++j)
+                if (s[j].k == Item::SET) { any_after = true; mand_after |= !s[j].opt; }
+            if (s[i].k == Item::BOL) {
+                if (mand_before) impossible = true;     // ^ after a consumed byte never holds
+                else if (any_before) throw Unsupported{};
+                else l.bol = true;
+            } else {
+                if (mand_after) impossible = true;      // $ before a byte to consume
+                else if (any_after) throw Unsupported{};
+                else l.eol = true;
+            }
+        }
+        if (impossible) continue;
+        for (const Item& it : s)
+            if (it.k == Item::SET) l.e.push_back(it);
+        bool nullable = true;
+        for (const Item& it : l.e) nullable &= it.opt;
+        if (nullable) {
+            o.empty = 1;
+            if (!(l.bol && l.eol)) {   // matches the empty string somewhere in any input
+                o.form = 2;
+                return o;
+            }
+            if (l.e.empty()) continue;   // ^$: only the empty input
+        }
+        keep.push_back(std::move(l));
+    }
+    if (keep.empty()) {
+        o.form = 3;
+        return o;
+    }
+    int bit = 0;
+    for (const Lin& l : keep) {
+        const int m = (int)l.e.size();
+        if (bit + m > 64) throw Unsupported{};
+        // starts: the first class and every class reachable by skipping optional ones
+        uint64_t starts = 0;
+        for (int j = 0; j < m; ++j) {
+            starts |= 1ull << (bit + j);
+            if (!l.e[j].opt) break;
+        }
+        (l.bol ? o.I0 : o.Iall) |= starts;
+        if (l.bol) o.NF &= ~(1ull << bit);
+        int run = 0;
+        for (int j = 0; j < m; ++j) {
+            const Item& it = l.e[j];
+            const uint64_t b = 1ull << (bit + j);
+            if (it.rep) o.S |= b;
+            if (it.opt && j > 0) o.A |= b;   // a sequence's first class is skipped by `starts`
+            run = it.opt && j > 0 ? run + 1 : 0;
+            o.R = std::max(o.R, run);
+            for (int c = 0; c < 256; ++c)
+                if (bp.sets[it.set].test(c)) o.B[c] |= b;
+        }
+        (l.eol ? o.Fe : o.F) |= 1ull << (bit + m - 1);
+        bit += m;
+    }
+    if (o.R > kBitparMaxR) throw Unsupported{};
+    o.A &= o.NF;
+    o.W = bit <= 8 ? 8 : bit <= 16 ? 16 : bit <= 32 ? 32 : 64;
+    o.flags = (o.S ? 1u : 0u) | (o.I0 ? 2u : 0u) | (!o.Iall ? 4u : 0u) | (o.Fe ? 8u : 0u);
+    return o;
+}
+
+uint32_t bitpar_size(const BitparBlob& o) {
+    return o.form != 1 ? kBitparHeader : kBitparHeader + 256u * (uint32_t)(o.W / 8);
+}
+
+void bitpar_write(const BitparBlob& o, uint8_t* p) {
+    std::memset(p, 0, bitpar_size(o));
+    const uint16_t magic = kBitparMagic, w = (uint16_t)o.W;
+    std::memcpy(p, &magic, 2);
+    std::memcpy(p + 2, &w, 2);
+    p[5] = (uint8_t)o.empty;
+    p[6] = (uint8_t)o.form;
+    p[7] = (uint8_t)o.R;
+    std::memcpy(p + 8, &o.flags, 4);
+    const uint64_t m[7] = {o.Iall, o.I0, o.S, o.A, o.NF, o.F, o.Fe};
+    std::memcpy(p + 16, m, sizeof(m));
+    if (o.form != 1) return;
+    const int e = o.W / 8;   // table entry bytes: the state width rounded up to 8/16/32/64 bits
+    for (int c = 0; c < 256; ++c) std::memcpy(p + kBitparHeader + e * c, &o.B[c], e);   // little endian
+}
+
+// The host executor of a bit-parallel blob: the kernel's loop, byte by byte.
+int bitpar_search(const uint8_t* p, const uint8_t* s, uint32_t n) {
+    if (n == 0) return p[5];
+    if (p[6] != 1) return p[6] == 2;
+    uint16_t W;
+    std::memcpy(&W, p + 2, 2);
+    uint64_t m[7];
+    std::memcpy(m, p + 16, sizeof(m));
+    const uint64_t Iall = m[0], I0 = m[1], S = m[2], A = m[3], NF = m[4], F = m[5], Fe = m[6];
+    const uint32_t R = p[7];
+    uint64_t D = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint64_t b = 0;
+        std::memcpy(&b, p + kBitparHeader + (W / 8) * s[i], W / 8);
+        D = (((D << 1) & NF) | Iall | (i == 0 ? I0 : 0) | (D & S)) & b;
+        for (uint32_t r = 0; r < R; ++r) D |= (D << 1) & A;
+        if (D & F) return 1;
+        if (!D && !Iall) return 0;
+    }
+    return (D & Fe) != 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -637,6 +895,17 @@ int bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob
         std::regex probe(e);   // the reference's own acceptance (src/PacketFilter.cpp:311-316)
     } catch (const std::regex_error&) {
         return BT_E_INVALID_ARGUMENT;
+    }
+    if (!(flags & BT_DFA_NO_BITPAR)) {   // the bit-parallel form where the pattern fits it
+        try {
+            const BitparBlob o = build_bitpar(e);
+            *size = bitpar_size(o);
+            if (!blob) return BT_OK;
+            if (cap < *size) return BT_E_RESOURCE;
+            bitpar_write(o, static_cast<uint8_t*>(blob));
+            return BT_OK;
+        } catch (const Unsupported&) {
+        }
     }
     Packed pk;
     try {
@@ -677,6 +946,7 @@ int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n) {
     const uint8_t* p = static_cast<const uint8_t*>(blob);
     uint16_t K, C;
     std::memcpy(&K, p, 2);
+    if (K == kBitparMagic) return bitpar_search(p, s, n);
     std::memcpy(&C, p + 2, 2);
     const uint8_t* endacc = p + 8;
     const uint8_t* cls = endacc + ((K + 3) & ~3);

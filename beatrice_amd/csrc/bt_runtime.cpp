@@ -895,14 +895,19 @@ int compile_program(const bt_filter_desc* f, uint32_t n, uint32_t ctx_flags, Com
         for (auto& s : slots) {
             const bt_filter_desc& d = f[s.source_index];
             if (s.kind != BT_K_HOST || d.type != BT_FILTER_PAYLOAD || !d.expression) continue;
-            uint32_t size = 0, fl = 0;
-            if (bt_payload_dfa_compile_ex(d.expression, fl, nullptr, 0, &size) != BT_OK) continue;
+            // the compiler's preferred form (bit-parallel where it fits, else the DFA with its
+            // two-byte table); when that does not fit the pool, the DFA, then the DFA without
+            // the optional table
+            const uint32_t base = (ctx_flags & BT_OPT_PAYLOAD_DFA) ? BT_DFA_NO_BITPAR : 0u;
+            const uint32_t forms[3] = {base, BT_DFA_NO_BITPAR, BT_DFA_NO_BITPAR | BT_DFA_NO_PAIRS};
             const size_t at = (pool.size() + 15) & ~(size_t)15;
-            if (at + size > kDfaPoolMax) {   // retry without the optional two-byte table
-                fl = BT_DFA_NO_PAIRS;
-                if (bt_payload_dfa_compile_ex(d.expression, fl, nullptr, 0, &size) != BT_OK || at + size > kDfaPoolMax)
-                    continue;
+            uint32_t size = 0, fl = 0;
+            bool fits = false;
+            for (uint32_t k = base ? 1u : 0u; k < 3 && !fits; ++k) {
+                fl = forms[k];
+                fits = bt_payload_dfa_compile_ex(d.expression, fl, nullptr, 0, &size) == BT_OK && at + size <= kDfaPoolMax;
             }
+            if (!fits) continue;
             pool.resize(at + size);
             if (bt_payload_dfa_compile_ex(d.expression, fl, pool.data() + at, size, &size) != BT_OK) {
                 pool.resize(at);

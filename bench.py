@@ -88,6 +88,14 @@ WORKLOADS = {
                name="C4: 16M QinQ/IPv6/IHL+TCP options, 2-mod-4 offsets, parse + PacketFilter "
                     "(BASELINE configs[3])"),
 }
+# C3 with a GPU PAYLOAD slot first: applyPayloadFilter's regex_search over every
+# IPv4 packet's <= 100-byte payload window (src/PacketFilter.cpp:288-321) before the 5-tuple set;
+# random payloads never match, so every window is searched to its end (the worst case)
+PAYLOAD_EXPR = "GET|POST"
+WORKLOADS["c3_payload"] = dict(cfg=synth.C3, fixed=False, parse=True, payload=PAYLOAD_EXPR, traffic_key="c3_payload",
+                               filters=[{"type": abi.PAYLOAD, "expr": PAYLOAD_EXPR, "priority": 9}] + C3_FILTERS,
+                               name="C3 + PAYLOAD /GET|POST/ first: 16M IMIX, parse + PacketFilter (payload regex on "
+                                    "every IPv4 packet's window, then udp, 10.0.0.0/8, 1000-2000) + ordered compaction")
 # configs[0]'s protocol: examples/parser_example.cpp:18-43's CUSTOM_PROTO (header u32 @0,
 # version u8 @4, length u16 @5, data BYTES[10] @7; all NETWORK byte order = 2), a user
 # table for ProtocolParser::parsePacket(frame, ProtocolDefinition)
@@ -417,7 +425,7 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     kms_max = max(r["main_ms"] for r in ranks)
     value = n_job / step_max / 1e6
     achieved = algo / (main_ms * 1e-3) / 1e9
-    key = name if not wl.get("payload") else None
+    key = wl.get("traffic_key", name if not wl.get("payload") else None)
     traffic_rec, traffic_src = load_traffic(args.traffic_json, key, n) if key else (None, "PAYLOAD variant")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -782,7 +790,7 @@ def main():
     ap.add_argument("--config", default="c2f", choices=sorted(WORKLOADS), help="the headline workload")
     ap.add_argument("--configs", default="auto",
                     help="comma list of extra workloads for the `configs` object (suffix _strong: strong "
-                         "scaling), 'none', or 'auto' (N=1: c2,c3,c4,c1; N>1: c3,c3_strong)")
+                         "scaling), 'none', or 'auto' (N=1: c2,c3,c4,c1,c3_payload; N>1: c3,c3_strong)")
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 18)
@@ -850,7 +858,7 @@ def main():
         head.update(filters=[{"type": abi.PAYLOAD, "expr": args.payload, "priority": 9}] + head["filters"],
                     name=head["name"] + f" + PAYLOAD /{args.payload}/ first", payload=args.payload)
     if args.configs == "auto":
-        extra = ["c2", "c3", "c4", "c1"] if world == 1 else ["c3", "c3_strong"]
+        extra = ["c2", "c3", "c4", "c1", "c3_payload"] if world == 1 else ["c3", "c3_strong"]
     elif args.configs == "none":
         extra = []
     else:

@@ -312,6 +312,8 @@ typedef struct bt_opts {
                                       reading each frame's window over PCIe */
 #define BT_OPT_NO_LEAN_HOST 0x20000u /* host batches, filter-only: stage each frame's first 48 B
                                       instead of bytes 12..43 (A/B only) */
+#define BT_OPT_PAYLOAD_DFA 0x40000u /* PAYLOAD slots as byte DFAs even where the bit-parallel
+                                      form fits (A/B only) */
 
 /* descriptor formats (bt_batch.desc_format) */
 #define BT_DESC_PACKED 0u          /* bt_pkt_desc: u64 offset:48 | length:16            */

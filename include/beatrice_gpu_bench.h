@@ -110,6 +110,9 @@ int  bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, ui
  * compiler adds it when it is <= 4 KiB; the filter compiler drops it when a program's
  * tables would not fit the 16 KiB pool otherwise). */
 #define BT_DFA_NO_PAIRS 0x1u
+/* BT_DFA_NO_BITPAR: always the DFA, never the bit-parallel form the compiler prefers for
+ * unions of linear class sequences (A/B and tests; blob layouts in bt_regex_dfa.cpp). */
+#define BT_DFA_NO_BITPAR 0x2u
 int  bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob, uint32_t cap, uint32_t* size);
 int  bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);
 /* The same walk, and each frame's header prefix is also copied into slot i of `slots`

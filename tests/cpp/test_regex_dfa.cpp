@@ -8,8 +8,10 @@
 // 2. Random patterns from a grammar over the modelled subset (literals incl. \n \r NUL
 //    and bytes >= 0x80, ., classes with ranges / negation / escapes, \d\w\s, groups,
 //    alternation, all quantifiers incl. stacked and lazy, ^ $ anywhere).
-// Every pattern std::regex accepts is compiled; where the compiler takes it (not
-// BT_E_NOT_IMPLEMENTED) the DFA must agree with regex_search on every test string:
+// Every pattern std::regex accepts is compiled twice, in the form the compiler prefers (the
+// bit-parallel Shift-And form where the pattern is a union of linear class sequences, else
+// the DFA) and as a DFA (BT_DFA_NO_BITPAR); where the compiler takes it (not
+// BT_E_NOT_IMPLEMENTED) each blob must agree with regex_search on every test string:
 // random strings over an alphabet that hits every class boundary, lengths 0..40,
 // plus the full applyPayloadFilter window path on synthetic frames.
 // libstdc++'s regex_search backtracks (exponential on nested quantifiers), so each
@@ -29,6 +31,8 @@
 #include "beatrice_gpu_bench.h"
 
 extern "C" int bt_payload_dfa_compile(const char* expression, void* blob, uint32_t cap, uint32_t* size);
+extern "C" int bt_payload_dfa_compile_ex(const char* expression, uint32_t flags, void* blob, uint32_t cap,
+                                         uint32_t* size);
 extern "C" int bt_payload_dfa_search(const void* blob, const uint8_t* s, uint32_t n);
 extern "C" int bt_payload_dfa_eval(const void* blob, const uint8_t* frame, uint32_t len);
 
@@ -92,7 +96,9 @@ struct Gen {
     }
 };
 
-static int g_bad = 0, g_checked = 0, g_unsupported = 0, g_rejected = 0, g_slow = 0;
+static int g_bad = 0, g_checked = 0, g_unsupported = 0, g_rejected = 0, g_slow = 0, g_bitpar = 0;
+
+static bool check_form(const std::string& pat, const std::regex& re, Gen& g, int nstr, uint32_t flags);
 
 static bool check(const std::string& pat, Gen& g, int nstr) {
     std::regex re;
@@ -119,9 +125,29 @@ static bool check(const std::string& pat, Gen& g, int nstr) {
         ++g_bad;
         return false;
     }
-    std::vector<uint8_t> blob(sz);
-    bt_payload_dfa_compile(pat.c_str(), blob.data(), sz, &sz);
     ++g_checked;
+    // the preferred form, then the DFA of the same pattern (the same strings: a copy of g)
+    Gen g2 = g;
+    if (!check_form(pat, re, g, nstr, 0)) return false;
+    if (bt_payload_dfa_compile(pat.c_str(), nullptr, 0, &sz) == BT_OK) {
+        std::vector<uint8_t> b(sz);
+        bt_payload_dfa_compile(pat.c_str(), b.data(), sz, &sz);
+        if (b[0] == 0xFF && b[1] == 0xFF) {
+            ++g_bitpar;
+            uint32_t s2 = 0;
+            if (bt_payload_dfa_compile_ex(pat.c_str(), BT_DFA_NO_BITPAR, nullptr, 0, &s2) == BT_OK)
+                return check_form(pat, re, g2, nstr, BT_DFA_NO_BITPAR);
+        }
+    }
+    return true;
+}
+
+static bool check_form(const std::string& pat, const std::regex& re, Gen& g, int nstr, uint32_t flags) {
+    uint32_t sz = 0;
+    bt_payload_dfa_compile_ex(pat.c_str(), flags, nullptr, 0, &sz);
+    std::vector<uint8_t> blob(sz);
+    bt_payload_dfa_compile_ex(pat.c_str(), flags, blob.data(), sz, &sz);
+    const char* form = blob.size() >= 2 && blob[0] == 0xFF && blob[1] == 0xFF ? "bitpar" : "dfa";
     for (int k = 0; k < nstr; ++k) {
         const std::string s = k == 0 ? std::string() : g.str();
         bool want;
@@ -138,7 +164,8 @@ static bool check(const std::string& pat, Gen& g, int nstr) {
                 std::snprintf(b, sizeof(b), "%02x", c);
                 hex += b;
             }
-            std::printf("FAIL /%s/ on [%s] (len %zu): std::regex %d dfa %d\n", pat.c_str(), hex.c_str(), s.size(), want, got);
+            std::printf("FAIL /%s/ on [%s] (len %zu): std::regex %d %s %d\n", pat.c_str(), hex.c_str(), s.size(), want,
+                        form, got);
             ++g_bad;
             return false;
         }
@@ -164,7 +191,7 @@ static bool check(const std::string& pat, Gen& g, int nstr) {
             }
         }
         if (bt_payload_dfa_eval(blob.data(), f.data(), len) != (int)want) {
-            std::printf("FAIL /%s/ frame eval (ihl %d len %u)\n", pat.c_str(), ihl, len);
+            std::printf("FAIL /%s/ %s frame eval (ihl %d len %u)\n", pat.c_str(), form, ihl, len);
             ++g_bad;
             return false;
         }
@@ -190,10 +217,10 @@ int main(int argc, char** argv) {
         if (pid == 0) {
             alarm(2);
             Gen gc(seed);
-            g_bad = g_checked = g_unsupported = g_rejected = 0;
+            g_bad = g_checked = g_unsupported = g_rejected = g_bitpar = 0;
             check(pat, gc, nstr);
             fflush(stdout);
-            _exit(g_bad ? 1 : g_checked ? 4 : g_unsupported ? 2 : 3);
+            _exit(g_bad ? 1 : g_bitpar ? 5 : g_checked ? 4 : g_unsupported ? 2 : 3);
         }
         int st = 0;
         waitpid(pid, &st, 0);
@@ -205,12 +232,14 @@ int main(int argc, char** argv) {
         case 1: ++g_bad; break;
         case 2: ++g_unsupported; break;
         case 3: ++g_rejected; break;
+        case 5: ++g_checked; ++g_bitpar; break;
         default: ++g_checked; break;
         }
     }
-    std::printf("patterns: %d compiled to DFA and checked, %d left on the host (outside the subset), "
-                "%d rejected by std::regex, %d skipped (std::regex_search > 2 s); %d disagreements\n",
-                g_checked, g_unsupported, g_rejected, g_slow, g_bad);
+    std::printf("patterns: %d compiled and checked (%d of them in the bit-parallel form, checked as a DFA too), "
+                "%d left on the host (outside the subset), %d rejected by std::regex, %d skipped "
+                "(std::regex_search > 2 s); %d disagreements\n",
+                g_checked, g_bitpar, g_unsupported, g_rejected, g_slow, g_bad);
     if (g_bad) {
         std::printf("%d FAILED\n", g_bad);
         return 1;

@@ -1,6 +1,10 @@
-"""GPU: PAYLOAD filters evaluated by the kernel's byte DFA (BT_K_PAYLOAD)
-instead of being resumed on the host, checked against the compiled reference
-(goldens; oracle/_ref on a live sample) and the DFA's host executor (full size)."""
+"""GPU: PAYLOAD filters evaluated by the kernel (BT_K_PAYLOAD) — the
+bit-parallel Shift-And form where the pattern is a union of linear class sequences, the byte
+DFA otherwise — instead of being resumed on the host, checked against the compiled reference
+(goldens; oracle/_ref on a live sample), the blobs' host executor (full size) and each other
+(the same program compiled both ways, BT_OPT_PAYLOAD_DFA)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -91,7 +95,9 @@ def test_payload_host_option_and_pool_limit():
         fs = [{"type": abi.PAYLOAD, "expr": big + "x" * k, "priority": -k} for k in range(40)]
         kinds = [abi.KINDS[p.kind] for p in ctx.compile(fs)]
         assert kinds[0] == "PAYLOAD" and "HOST" in kinds   # the 16 KiB pool fills, the rest stay on the host
-        assert kinds.index("HOST") == kinds.count("PAYLOAD")
+        pool = ctypes.c_uint32(0)
+        abi._check(abi.lib().bt_filter_dfa_pool(ctx.h, None, 0, ctypes.byref(pool)))
+        assert 0 < pool.value <= 16384
     finally:
         ctx.close()
 
@@ -132,3 +138,43 @@ def test_host_batch_payload_past_staged_headers():
     compare_decisions(out["decide"], code, src, filters, where="host-batch payload")
     late = [i for i, f in enumerate(frames) if f.find(b"MAGIC") >= 112]
     assert len(late) > 100 and (code[late] == 0).sum() > 50
+
+
+FORM_PATTERNS = ["GET|POST", "User-Agent: .*(bot|curl)", "^.{0,5}$", "\\s+$", "[\\x80-\\xff]{4,}", "passw(or)?d=",
+                 "^\\x16\\x03[\\x00-\\x03]", "(?:GET|HEAD) /[^ ]* HTTP", "a.?b*c", "[0-9a-f]{2}[^a-z]?z+$"]
+
+
+@pytest.mark.parametrize("cfg", [synth.C3, synth.FUZZ])
+def test_bitpar_and_dfa_forms_agree(cfg):
+    """Every FORM_PATTERNS regex takes the bit-parallel form by default (32- and 64-bit states,
+    anchors, optional and repeated classes) and decides every packet of a 1M-packet capture
+    exactly as the same slot compiled as a byte DFA; a 64k sample against the reference."""
+    n = 1 << 20
+    data, desc = synth.capture(cfg, n, seed=41)
+    # plant some matches: payload bytes of every 7th frame rewritten with pattern-shaped text
+    off, ln = synth.desc_off(desc), synth.desc_len(desc)
+    words = [b"GET /", b"POST", b"User-Agent: x bot", b"passwd=", b"\x16\x03\x01", b"HEAD /a HTTP", b"abbbc"]
+    for i in range(0, n, 7):
+        o, m = int(off[i]), int(ln[i])
+        if m > 60:
+            w = words[(i // 7) % len(words)]
+            at = o + 14 + 20 + (i % 13)
+            if at + len(w) <= o + m:
+                data[at:at + len(w)] = np.frombuffer(w, np.uint8)
+    bp, dfa = abi.Context(0), abi.Context(0, flags=abi.OPT_PAYLOAD_DFA)
+    try:
+        for expr in FORM_PATTERNS:
+            f = [{"type": abi.PAYLOAD, "expr": expr, "priority": 1}]
+            assert abi.KINDS[bp.compile(f)[0].kind] == "PAYLOAD" and abi.KINDS[dfa.compile(f)[0].kind] == "PAYLOAD"
+            blob = abi.payload_dfa(expr)
+            assert blob[:2] == b"\xff\xff", f"/{expr}/ did not take the bit-parallel form"
+            a, b = _run(bp, data, desc), _run(dfa, data, desc)
+            bad = np.nonzero(a["decide"] != b["decide"])[0]
+            assert len(bad) == 0, f"/{expr}/: {len(bad)} decisions differ between the forms, first {bad[:5]}"
+            if ol.ref_available():
+                k = 1 << 16
+                code, src = ol.ref_filter(data, desc, k, f)
+                compare_decisions(a["decide"][:k], code, src, f, where=f"{cfg}/bitpar /{expr}/")
+    finally:
+        dfa.close()
+        bp.close()

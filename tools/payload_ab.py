@@ -5,7 +5,10 @@ that differ only in their PAYLOAD slot, alternating variants round by round in o
   base        C3's 5-tuple set, no PAYLOAD slot (the uniform-predicate path, F = 1)
   last        + PAYLOAD /GET|POST/ last: the per-kind path, the regex only for packets that pass
   first       PAYLOAD /GET|POST/ first (every IPv4 packet runs it; random payloads never match:
-              the whole <= 100-byte window is walked) — the configuration the verdict quotes
+              the whole <= 100-byte window is walked) — the configuration the verdict quotes;
+              the bit-parallel (Shift-And) form the compiler picks for it
+  first_dfa   the same program with the slot compiled as a byte DFA (BT_OPT_PAYLOAD_DFA context)
+  ua, ua_dfa  PAYLOAD /User-Agent: .*(bot|curl)/ first: 33 positions (the 64-bit state)
   dot         PAYLOAD /./ first: staged, then decided on the first byte
   caret       PAYLOAD /^/ first: staged, the start state already accepts (staging alone)
 each with records (parse + filter) and without (filter only).
@@ -38,7 +41,9 @@ def prog(kind, expr=None):
 
 
 VARIANTS = {"base": prog("base"), "last": prog("last", "GET|POST"), "first": prog("first", "GET|POST"),
-            "dot": prog("first", "."), "caret": prog("first", "^")}
+            "first_dfa": prog("first", "GET|POST"), "ua": prog("first", "User-Agent: .*(bot|curl)"),
+            "ua_dfa": prog("first", "User-Agent: .*(bot|curl)"), "dot": prog("first", "."),
+            "caret": prog("first", "^")}
 
 
 def main():
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--records", default="1,0")
     a = ap.parse_args()
     ctx = abi.Context(0)
+    ctx_dfa = abi.Context(0, flags=abi.OPT_PAYLOAD_DFA)
     wl = dict(bench.WORKLOADS["c3"], payload="GET|POST")
     cap = bench.Capture(ctx, wl, a.packets, synth.SEEDS[synth.C3], 0, a.packets)
     run = cap.run
@@ -57,12 +63,17 @@ def main():
     names = a.variants.split(",")
     for rnd in range(a.rounds):
         for v in names:
-            p = ctx.compile(VARIANTS[v])
+            c = ctx_dfa if v.endswith("_dfa") else ctx
+            p = c.compile(VARIANTS[v])
             for rec in (int(x) for x in a.records.split(",")):
                 o = abi.Outputs(run.outs.records if rec else None, run.n, run.outs.verdict, run.outs.decide,
                                 run.outs.pass_idx, run.outs.n_pass)
-                ctx.time_device2(run.batch, [o], 2, abi.TIME_KERNEL_EVENTS)   # warm
-                t = ctx.time_device2(run.batch, [o], a.steps, abi.TIME_KERNEL_EVENTS)
+                c.time_device2(run.batch, [o], 2, abi.TIME_KERNEL_EVENTS)   # warm
+                t = c.time_device2(run.batch, [o], a.steps, abi.TIME_KERNEL_EVENTS)
+                if rnd == 0:   # every form decides the same as the first variant with a PAYLOAD slot
+                    dec = np.empty(run.n, np.uint8)
+                    abi.lib().bt_memcpy_d2h(c.h, dec.ctypes.data, run.outs.decide, run.n)
+                    res[(v, rec, "dec")] = dec
                 res.setdefault((v, rec), []).append(t.main_ms)
                 if rnd == 0:
                     res[(v, rec, "kinds")] = [abi.KINDS[s.kind] for s in p]
@@ -72,10 +83,15 @@ def main():
             ms = sorted(res[(v, rec)])
             print(json.dumps({"variant": v, "records": bool(rec), "packets": run.n, "kernel_ms_median": round(ms[len(ms) // 2], 4),
                               "kernel_ms_all": [round(x, 4) for x in ms], "kinds": res[(v, rec, "kinds")],
+                              "decisions_equal_to_dfa_form": (bool(np.array_equal(res[(v, rec, "dec")],
+                                                                                  res[(v + "_dfa", rec, "dec")]))
+                                                              if (v + "_dfa", rec, "dec") in res else None),
+                              "n_pass": int(np.count_nonzero((res[(v, rec, "dec")] >> 6) == 0)),
                               "mpps": round(run.n / (ms[len(ms) // 2] * 1e-3) / 1e6, 1),
                               "payload_extra_bytes_per_packet": round(cap.payload_extra / run.n, 2),
                               "header_window_bytes_per_packet": round(cap.win_bytes / run.n, 2)}), flush=True)
     run.free()
+    ctx_dfa.close()
     ctx.close()
 
 
