@@ -164,6 +164,12 @@ class Tpv3Ring(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class RingStageOpts(ctypes.Structure):
+    """bt_ring_stage_opts (include/beatrice_gpu.h)."""
+    _fields_ = [("batch_blocks", ctypes.c_uint32), ("gather", ctypes.c_uint32), ("in_place_every", ctypes.c_uint32),
+                ("in_place_blocks", ctypes.c_uint32)]
+
+
 EXPORTS = [
     "bt_abi_version", "bt_last_error", "bt_create", "bt_destroy", "bt_device_count", "bt_context_device",
     "bt_filter_compile",
@@ -175,7 +181,7 @@ EXPORTS = [
     "bt_payload_dfa_compile", "bt_payload_dfa_compile_ex", "bt_payload_dfa_search", "bt_payload_dfa_eval",
     "bt_format_records", "bt_format_records_to",
     "bt_record_unpack", "bt_record_slabs", "bt_ring_gather_tpv3", "bt_ring_gather_dense_tpv3",
-    "bt_ring_gather_lean_tpv3",
+    "bt_ring_gather_lean_tpv3", "bt_ring_stage_tpv3",
     "bt_group_create", "bt_group_destroy", "bt_group_size", "bt_group_member", "bt_group_filter_compile",
     "bt_group_parse_filter", "bt_group_parse_filter_ptrs", "bt_group_split",
     "bt_group_split_cost", "bt_group_cost", "bt_group_thread_budget", "bt_group_host_register",
@@ -254,6 +260,8 @@ def lib() -> ctypes.CDLL:
                                                      ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_ring_gather_lean_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, vp, vp, vp, u32,
                                                      ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+        "bt_ring_stage_tpv3": (ctypes.c_int, [vp, ctypes.POINTER(Tpv3Ring), u32, u32, ctypes.POINTER(RingStageOpts),
+                                              vp, vp, vp, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "bt_payload_dfa_compile": (ctypes.c_int, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
         "bt_payload_dfa_search": (ctypes.c_int, [vp, vp, u32]),
         "bt_payload_dfa_eval": (ctypes.c_int, [vp, vp, u32]),
@@ -787,6 +795,29 @@ def ring_gather_tpv3(ring: np.ndarray, block_size: int, n_blocks: int, slots: np
     else:
         _check(lib().bt_ring_gather_tpv3(*args, *tail))
     return out[slot_base:slot_base + nd.value], nb.value
+
+
+def ring_stage_tpv3(ctx: "Context", ring: np.ndarray, block_size: int, n_blocks: int, desc: np.ndarray,
+                    decide: np.ndarray, verdict: np.ndarray | None = None, slots: np.ndarray | None = None,
+                    first: int = 0, count: int | None = None, batch_blocks: int = 0, gather: bool = False,
+                    in_place_every: int = 0, in_place_blocks: int = 0):
+    """bt_ring_stage_tpv3: blocks [first, first + count) of a registered ring through the
+    context's filter, walk of each batch overlapping the kernels of the one before. desc /
+    decide (/ verdict, slots) are host arrays registered with ctx (abi.host_array + register).
+    Returns (frames, passed)."""
+    cap = min(len(desc), len(decide))
+    if verdict is not None and len(verdict) * 64 < cap:
+        raise ValueError("verdict: need ceil(cap / 64) words")
+    if slots is not None and slots.nbytes < cap * PREFIX_SLOT:
+        raise ValueError("slots: need cap * PREFIX_SLOT bytes")
+    r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
+    o = RingStageOpts(batch_blocks, int(gather), in_place_every, in_place_blocks)
+    nd, npass = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().bt_ring_stage_tpv3(ctx.h, ctypes.byref(r), first, n_blocks if count is None else count, ctypes.byref(o),
+                                    desc.ctypes.data, None if slots is None else slots.ctypes.data,
+                                    decide.ctypes.data, None if verdict is None else verdict.ctypes.data, cap,
+                                    ctypes.byref(nd), ctypes.byref(npass)))
+    return nd.value, npass.value
 
 
 def ring_walk_tpv3_gpu(ctx: "Context", ring: np.ndarray, ring_dev: int, block_size: int, n_blocks: int,

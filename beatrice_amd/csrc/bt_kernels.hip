@@ -383,6 +383,44 @@ __device__ __forceinline__ uint32_t bitpar_walk(const uint8_t* blob, const uint3
     return (hit || (D & Fe)) ? 1u : 0u;
 }
 
+// A SIMPLE pattern with a byte z that no class holds (the compiler records it): the window's
+// bytes past its end are overwritten with z in the row, so every byte the wave's walk reads
+// past a lane's window empties that lane's D and no position needs a bound check. The steps
+// are then ((D << 1) | I) & B[c] and an OR of the states (H; a match ended where H & F is
+// set): about 4 VALU per byte against 8 with the bound checks, which made the walk VALU-bound
+// (C3 /GET|POST/ first: 123 k VALU per wave of the 129 k the walk added, SQ counters).
+template <typename E>
+__device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint32_t* row, uint32_t staged_sh,
+                                                uint32_t L) {
+    const uint64_t* mk = reinterpret_cast<const uint64_t*>(blob + 16);
+    const uint32_t Iall = (uint32_t)mk[0], F = (uint32_t)mk[5];
+    const E* B = reinterpret_cast<const E*>(blob + 80);
+    const uint32_t* r = row + (staged_sh >> 2);
+    const uint32_t sh = staged_sh & 3u, rmax = 31u - (staged_sh >> 2);
+    uint32_t D = 0, H = 0;
+    uint32_t t0 = r[0], t1 = r[1], t2 = r[2];
+    for (uint32_t i = 0;; i += 8u) {
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(t1, t0, sh), w1 = __builtin_amdgcn_alignbyte(t2, t1, sh);
+        t0 = t2;
+        t1 = r[min((i >> 2) + 3u, rmax)];
+        t2 = r[min((i >> 2) + 4u, rmax)];
+        uint32_t b[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            b[k] = B[(w0 >> (8 * k)) & 0xFFu];
+            b[4 + k] = B[(w1 >> (8 * k)) & 0xFFu];
+        }
+        const uint32_t d0 = ((D << 1) | Iall) & b[0], d1 = ((d0 << 1) | Iall) & b[1];
+        const uint32_t d2 = ((d1 << 1) | Iall) & b[2], d3 = ((d2 << 1) | Iall) & b[3];
+        const uint32_t d4 = ((d3 << 1) | Iall) & b[4], d5 = ((d4 << 1) | Iall) & b[5];
+        const uint32_t d6 = ((d5 << 1) | Iall) & b[6];
+        D = ((d6 << 1) | Iall) & b[7];
+        H |= d0 | d1 | d2 | d3 | d4 | d5 | d6 | D;
+        if (__ballot(!(H & F) && i + 8u < L) == 0ull) break;
+    }
+    return (H & F) ? 1u : 0u;
+}
+
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
                                                  uint32_t& staged_sh, const PayWin* pre) {
@@ -391,7 +429,7 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
     if (!L) return 0u;
     const uint32_t K = *reinterpret_cast<const uint16_t*>(blob);
     if (K == 0xFFFFu && blob[6] != 1u) return blob[6] == 2u ? 1u : 0u;   // bit-parallel: always / never
-    if (staged_sh == ~0u && pre) {   // loaded ahead: into the row (free once PARSE is done)
+    if (staged_sh == ~0u && pre && pre->nch) {   // loaded ahead: into the row (free once PARSE is done)
         staged_sh = pre->sh;
 #pragma unroll
         for (uint32_t k = 0; k < 8u; ++k)
@@ -425,6 +463,18 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
     if (K == 0xFFFFu) {   // the bit-parallel form (wave-uniform: the slot's blob)
         const uint32_t W = *reinterpret_cast<const uint16_t*>(blob + 2);
         const bool simple = *reinterpret_cast<const uint32_t*>(blob + 8) == 0u && blob[7] == 0u;
+        const uint32_t z = blob[12];   // 1 + a byte no class holds, 0: none
+        if (simple && z && W <= 32u) {
+            // the row past the window: z in every byte (the dword the window ends in keeps
+            // the window's bytes below the end)
+            const uint32_t end = staged_sh + L, q = end >> 2, zz = (z - 1u) * 0x01010101u;
+            const uint32_t keep = (end & 3u) ? (1u << (8u * (end & 3u))) - 1u : 0u;
+            row[q] = (row[q] & keep) | (zz & ~keep);
+            for (uint32_t k = q + 1u; k < 33u; ++k) row[k] = zz;
+            return W == 8 ? bitpar_fast<uint8_t>(blob, row, staged_sh, L)
+                 : W == 16 ? bitpar_fast<uint16_t>(blob, row, staged_sh, L)
+                           : bitpar_fast<uint32_t>(blob, row, staged_sh, L);
+        }
         switch (W) {
         case 8: return simple ? bitpar_walk<uint8_t, true>(blob, row, staged_sh, L)
                               : bitpar_walk<uint8_t, false>(blob, row, staged_sh, L);
@@ -1177,7 +1227,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     // the first PAYLOAD slot: the lanes that reach it get their payload windows loaded ahead
     uint32_t pay_first = ~0u;
     if constexpr (FILTER == 2) {
-        if (!a.prefixes)
+        if (!a.prefixes && !(a.nt & 16u))
             for (uint32_t f = 0; f < prog.n; ++f)
                 if (prog.f[f].kind == BT_K_PAYLOAD) {
                     pay_first = f;
@@ -1256,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         if (FILTER) {
             uint32_t slot;
             const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live,
-                                                        slot, FILTER == 2 ? &pw : nullptr);
+                                                        slot, FILTER == 2 ? &pw : nullptr);   // pw.nch = 0: not loaded
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);

@@ -643,10 +643,11 @@ uint32_t blob_size(const Packed& p) {
 //   u16 0xFFFF (no DFA has that many states), u16 W (8 / 16 / 32 / 64: the positions rounded
 //   up; the width of a table entry, so small patterns read 1- or 2-byte entries, whose
 //   256-entry table spans fewer LDS banks' worth of distinct dwords)
-//   u8 0, u8 empty (match on the empty input), u8 form (1 search, 2 always true, 3 never),
+//   u8 m (the longest match in bytes when no class is optional or repeated, else 0),
+//   u8 empty (match on the empty input), u8 form (1 search, 2 always true, 3 never),
 //   u8 R (closure steps)
 //   u32 flags: 1 S != 0, 2 some sequence ^-anchored, 4 every sequence ^-anchored, 8 Fe != 0
-//   u32 0
+//   u8 1 + a byte no class holds (0: none, or it is 0xFF), u8 0 x3
 //   u64 Iall, I0, S, A, NF, F, Fe      (I0 = the extra starts at byte 0)
 //   u64 pad
 //   B[256]: W-bit entries at byte 80
@@ -748,7 +749,7 @@ struct Bitpar {
 };
 
 struct BitparBlob {
-    int W = 32, form = 1, R = 0, empty = 0;
+    int W = 32, form = 1, R = 0, empty = 0, longest = 0;
     uint32_t flags = 0;
     uint64_t Iall = 0, I0 = 0, S = 0, A = 0, NF = ~0ull, F = 0, Fe = 0;
     uint64_t B[256] = {};
@@ -829,6 +830,7 @@ BitparBlob build_bitpar(const std::string& pattern) {
                 if (bp.sets[it.set].test(c)) o.B[c] |= b;
         }
         (l.eol ? o.Fe : o.F) |= 1ull << (bit + m - 1);
+        o.longest = std::max(o.longest, m);
         bit += m;
     }
     if (o.R > kBitparMaxR) throw Unsupported{};
@@ -847,6 +849,16 @@ void bitpar_write(const BitparBlob& o, uint8_t* p) {
     const uint16_t magic = kBitparMagic, w = (uint16_t)o.W;
     std::memcpy(p, &magic, 2);
     std::memcpy(p + 2, &w, 2);
+    // the longest match in bytes when every class occurs exactly once (no ?, *, +): the
+    // kernel may then search pieces of the window independently (bitpar_chains)
+    p[4] = (o.S || o.A || o.longest > 255) ? 0 : (uint8_t)o.longest;
+    // 1 + the smallest byte no position's class holds (B[z] == 0), 0 if every byte is in some
+    // class: the kernel pads the window with it (bitpar_fast)
+    for (int c = 0; c < 256 && o.form == 1; ++c)
+        if (!o.B[c]) {
+            p[12] = (uint8_t)(c + 1 <= 255 ? c + 1 : 0);
+            break;
+        }
     p[5] = (uint8_t)o.empty;
     p[6] = (uint8_t)o.form;
     p[7] = (uint8_t)o.R;

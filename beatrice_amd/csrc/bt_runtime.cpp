@@ -513,6 +513,13 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
     if (c->opts.flags & BT_OPT_WIDE_ALWAYS) a.nt |= 8u;
+    // PAYLOAD windows are loaded ahead of the tile's parse (bt_parse_filter_pipe);
+    // BT_PAYLOAD_LATE=1 (A/B) loads them at the slot (eval_payload) instead.
+    static const bool late_payload = [] {
+        const char* e = getenv("BT_PAYLOAD_LATE");
+        return e && *e && *e != '0';
+    }();
+    if (late_payload) a.nt |= 16u;
     a.lean_lo = 0;
     if (lean && !(a.nt & 8u)) {   // frames over PCIe: lean round A, never the wide 128-B mode
         static const uint32_t lean_end = [] {   // A/B knobs: BT_LEAN_END, BT_LEAN_LO

@@ -678,7 +678,72 @@ def measure_group_ingest(n_dev: int, packets: int, reps: int = 5, shared: bool =
             for a in held:
                 grp.unregister(a)
             grp.close()
+        if n_dev == 1 and not shared:   # the ring stage of these frames (one device)
+            try:
+                out.setdefault("ring", {})[name] = measure_ring_stage(data, desc, nodes[0])
+            except Exception as e:   # reported, never fatal to the line
+                out.setdefault("ring", {})[name] = {"error": str(e)[:300]}
         del data, desc
+    return out
+
+
+def measure_ring_stage(data: np.ndarray, desc: np.ndarray, node: int, reps: int = 5) -> dict:
+    """The TPACKET_V3 ring stage on device 0 (bt_ring_stage_tpv3, the call GpuTpacketStage's
+    poll makes): the frames packed into a ring image laid out as the Linux kernel fills a
+    PACKET_RX_RING (synth.tpv3_ring), placed on the device's NUMA node and registered once; each
+    pass takes every block, the host walking (or lean-gathering) batch k+1 of 128 blocks while
+    the GPU filters batch k over PCIe, decisions and verdict words back in registered host
+    memory. PCIe-inclusive, never the line's `value`. Modes: in place (the stage's default), lean
+    gather on every other batch, lean gather on every batch, and every batch split (its last 40 or
+    56 of 128 blocks read in place, the rest gathered)."""
+    import time as _time
+    from beatrice_amd import numa
+    ring, rdesc, used = synth.tpv3_ring(data, desc)
+    n = len(rdesc)
+    placed = numa.place_ranges(ring, [(0, ring.nbytes, node)])   # pages of its own, as a ring mapping is
+    ring = placed if placed is not ring else abi.host_copy(ring)
+    del placed
+    ctx = abi.Context(0, flags=abi.OPT_SPIN_SYNC)
+    held = []
+    out = {"workload": "TPACKET_V3 ring image (kernel layout) of the same frames, registered once: per pass every "
+                       "block through bt_ring_stage_tpv3 (batches of 128 blocks, host walk of the next batch "
+                       "overlapping the kernels of this one), C3's 5-tuple filter, decisions + verdict words into "
+                       "registered host memory",
+           "frames": n, "ring_blocks": used, "block_bytes": synth.TPV3_BLOCK, "ring_bytes": int(ring.nbytes),
+           "unit": "Mpps", "pcie_inclusive": True}
+    try:
+        ctx.compile(C3_FILTERS)
+        rd = abi.host_array(n + 64, np.uint64)
+        dec = abi.host_array(n + 64)
+        ver = abi.host_array((n + 127) // 64, np.uint64)
+        slots = abi.host_array((n + 64) * abi.PREFIX_SLOT)
+        for a in (ring, rd, dec, ver, slots):
+            ctx.register(a)
+            held.append(a)
+        ref_dec = None
+        for mode, kw in (("in_place", {}), ("lean_every_other", dict(gather=True, in_place_every=2)),
+                         ("lean_all", dict(gather=True)), ("lean_split_40", dict(gather=True, in_place_blocks=40)),
+                         ("lean_split_56", dict(gather=True, in_place_blocks=56))):
+            abi.ring_stage_tpv3(ctx, ring, synth.TPV3_BLOCK, used, rd, dec, ver, slots, **kw)   # warm
+            times = []
+            for _ in range(reps):
+                t0 = _time.perf_counter()
+                got, npass = abi.ring_stage_tpv3(ctx, ring, synth.TPV3_BLOCK, used, rd, dec, ver, slots, **kw)
+                times.append(_time.perf_counter() - t0)
+            bits = np.unpackbits(ver.view(np.uint8), bitorder="little")[:got].astype(bool)
+            med = sorted(times)[len(times) // 2]
+            ent = {"value": round(got / med / 1e6, 1), "best": round(got / min(times) / 1e6, 1),
+                   "ms_per_pass": round(med * 1e3, 3), "frames": got, "pass_fraction": round(npass / max(got, 1), 4),
+                   "verdicts_match_decisions": bool(np.array_equal(bits, (dec[:got] >> 6) == 0))}
+            if ref_dec is None:
+                ref_dec = dec[:got].copy()
+            else:
+                ent["decisions_match_in_place"] = bool(np.array_equal(dec[:got], ref_dec))
+            out[mode] = ent
+    finally:
+        for a in held:
+            ctx.unregister(a)
+        ctx.close()
     return out
 
 

@@ -509,6 +509,30 @@ int  bt_ring_gather_lean_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t fi
  * release-ordered). Call it once the device has finished reading them. */
 int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32_t count);
 
+/* The ring stage in one call: up to n_blocks ready blocks from first_block through the
+ * context's filter program, in batches of batch_blocks (0 = 128). Each batch is walked on the
+ * host (bt_ring_walk_tpv3; with gather, its frames' bytes 12..43 packed into `slots`,
+ * bt_ring_gather_lean_tpv3) while the kernels of the batch before it run, so the host walk
+ * and the device's PCIe reads overlap. Writes one descriptor (ring-relative in place; slot-
+ * relative for gathered batches) and one decision byte per frame in ring order, and, if
+ * given, the verdict words and the pass count; stops early at a block the kernel still owns.
+ * The ring, desc (cap entries), decide (cap bytes) and, with gather, slots (cap *
+ * BT_PREFIX_SLOT bytes, 16-B aligned) must be registered with the context
+ * (bt_host_register). Filter-only: the decision bytes are the product (records: the
+ * descriptors + bt_parse_filter_device). Replaces the per-frame recv() loop feeding
+ * PacketFilter::applyFilters (reference src/AF_PacketBackend.cpp:318-363). */
+typedef struct bt_ring_stage_opts {
+    uint32_t batch_blocks;        /* blocks per kernel launch (0 = 128)                     */
+    uint32_t gather;              /* 1: pack bytes 12..43 of each frame (lean) before launch */
+    uint32_t in_place_every;      /* with gather: every k-th batch read in place (0 = none)  */
+    uint32_t in_place_blocks;     /* with gather: the last m blocks of every batch read in
+                                     place, the rest gathered (0 = whole batches; overrides
+                                     in_place_every)                                         */
+} bt_ring_stage_opts;
+int  bt_ring_stage_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_t first_block, uint32_t n_blocks,
+                        const bt_ring_stage_opts* opts, bt_pkt_desc* desc, uint8_t* slots, uint8_t* decide,
+                        uint64_t* verdict, uint32_t cap, uint32_t* n_desc, uint32_t* n_pass);
+
 /* ---- several devices in one process -------------------------------
  * The reference runs one daemon process whose capture threads feed one plugin set
  * (src/BeatriceContext.cpp:215-278, src/PluginManager.cpp:158-188). A group is one

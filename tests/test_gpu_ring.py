@@ -289,3 +289,79 @@ def test_gpu_walk_reports_a_malformed_block(gpu_ctx):
     assert np.array_equal(dev[:n0 + 6], host_ok[:n0 + 6])        # up to and including frame 5
     assert not dev[n0 + 6:n0 + n1].any()                         # the rest of block 1: empty
     assert np.array_equal(dev[n0 + n1:], host_ok[n0 + n1:])      # later blocks unaffected
+
+
+BUILTIN_C3 = [{"type": abi.PROTOCOL, "expr": "udp", "priority": 3},
+              {"type": abi.IP_RANGE, "expr": "10.0.0.0/8", "priority": 2},
+              {"type": abi.PORT_RANGE, "expr": "1000-2000", "priority": 1}]
+
+
+def _stage(ctx, ring, bs, used, n, **kw):
+    """bt_ring_stage_tpv3 over a ring image with every buffer registered on pages of its own."""
+    ring = abi.host_copy(ring)
+    desc = abi.host_array(n + 64, np.uint64)
+    dec = abi.host_array(n + 64)
+    ver = abi.host_array((n + 127) // 64, np.uint64)
+    slots = abi.host_array((n + 64) * abi.PREFIX_SLOT) if kw.get("gather") else None
+    held = [a for a in (ring, desc, dec, ver, slots) if a is not None]
+    for a in held:
+        ctx.register(a)
+    try:
+        got, npass = abi.ring_stage_tpv3(ctx, ring, bs, used, desc, dec, ver, slots, **kw)
+    finally:
+        for a in held:
+            ctx.unregister(a)
+    return ring, got, npass, desc[:got].copy(), dec[:got].copy(), ver.copy()
+
+
+@pytest.mark.parametrize("cfg", [synth.C2, synth.C3, synth.C4, synth.FUZZ])
+@pytest.mark.parametrize("mode", ["in_place", "lean_mix", "lean_all", "lean_split"])
+def test_ring_stage_decides_as_the_oracle(gpu_ctx, cfg, mode):
+    """The one-call ring stage (walk of batch k+1 overlapping the kernels of batch k; in place,
+    lean gather on every other batch, lean gather on all): every frame of a 200k-frame ring in
+    ring order, decisions against the oracle on the frames, verdict words and pass count from
+    them, batches of 7 blocks so that batches start mid-tile."""
+    n = 200_000
+    data, desc0 = synth.capture(cfg, n, seed=33)
+    ring, rdesc, used = synth.tpv3_ring(data, desc0)
+    gpu_ctx.compile(BUILTIN_C3)
+    kw = {"in_place": {}, "lean_mix": dict(gather=True, in_place_every=2), "lean_all": dict(gather=True),
+          "lean_split": dict(gather=True, in_place_blocks=3)}[mode]
+    ring, got, npass, desc, dec, ver = _stage(gpu_ctx, ring, synth.TPV3_BLOCK, used, n, batch_blocks=7, **kw)
+    assert got == len(rdesc) == n
+    _, odec, onp = ol.oracle_run(ring, rdesc, n, BUILTIN_C3, parse=False)
+    bad = np.nonzero(dec != odec)[0]
+    assert len(bad) == 0, f"{len(bad)} decisions differ, first {bad[:5]}"
+    bits = np.unpackbits(ver.view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(bits, (odec >> 6) == 0) and npass == onp
+    if mode == "in_place":
+        assert np.array_equal(desc, rdesc)
+
+
+def test_ring_stage_stops_at_a_kernel_owned_block(gpu_ctx):
+    """A block still owned by the kernel (TP_STATUS_KERNEL) ends the run there: the frames of
+    the blocks before it are decided, nothing after it is read."""
+    import ring_util as ru
+    n = 20_000
+    data, desc0 = synth.capture(synth.C3, n, seed=5)
+    ring, rdesc, used = synth.tpv3_ring(data, desc0)
+    stop = used // 2
+    at = stop * synth.TPV3_BLOCK + ru.BLOCK_STATUS
+    ring[at:at + 4] = np.frombuffer(np.uint32(ru.TP_STATUS_KERNEL).tobytes(), np.uint8)
+    gpu_ctx.compile(BUILTIN_C3)
+    ring, got, npass, desc, dec, ver = _stage(gpu_ctx, ring, synth.TPV3_BLOCK, used, n, batch_blocks=3)
+    expect = len(abi.ring_walk_tpv3(ring, synth.TPV3_BLOCK, used, max_blocks=stop)[0])
+    assert 0 < got == expect < n
+    _, odec, _ = ol.oracle_run(ring, rdesc[:got], got, BUILTIN_C3, parse=False)
+    assert np.array_equal(dec, odec)
+
+
+def test_ring_stage_refuses_unregistered_buffers(gpu_ctx):
+    n = 1000
+    data, desc0 = synth.capture(synth.C2, n, seed=1)
+    ring, _, used = synth.tpv3_ring(data, desc0)
+    ring = abi.host_copy(ring)
+    desc, dec = abi.host_array(n, np.uint64), abi.host_array(n)
+    gpu_ctx.compile(BUILTIN_C3)
+    with pytest.raises(abi.BtError, match="registered"):
+        abi.ring_stage_tpv3(gpu_ctx, ring, synth.TPV3_BLOCK, used, desc, dec)

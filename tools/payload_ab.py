@@ -10,7 +10,8 @@ that differ only in their PAYLOAD slot, alternating variants round by round in o
   first_dfa   the same program with the slot compiled as a byte DFA (BT_OPT_PAYLOAD_DFA context)
   ua, ua_dfa  PAYLOAD /User-Agent: .*(bot|curl)/ first: 33 positions (the 64-bit state)
   dot         PAYLOAD /./ first: staged, then decided on the first byte
-  caret       PAYLOAD /^/ first: staged, the start state already accepts (staging alone)
+  caret       PAYLOAD /^/ first: the bit-parallel compiler folds it to "always" (no window read)
+  caret_x     PAYLOAD /^x/ first: every window loaded and staged, the search over after one turn
 each with records (parse + filter) and without (filter only).
 
 Usage: python tools/payload_ab.py [--packets N] [--steps K] [--rounds R] [--variants a,b]
@@ -43,7 +44,7 @@ def prog(kind, expr=None):
 VARIANTS = {"base": prog("base"), "last": prog("last", "GET|POST"), "first": prog("first", "GET|POST"),
             "first_dfa": prog("first", "GET|POST"), "ua": prog("first", "User-Agent: .*(bot|curl)"),
             "ua_dfa": prog("first", "User-Agent: .*(bot|curl)"), "dot": prog("first", "."),
-            "caret": prog("first", "^")}
+            "caret": prog("first", "^"), "caret_x": prog("first", "^x"), "caret_x_dfa": prog("first", "^x")}
 
 
 def main():
