@@ -48,8 +48,7 @@ struct MainArgs {
     uint64_t* verdict;         // per-tile pass words (also the compaction's input)
     uint32_t blocked;          // tile order: 0 cyclic, 1 one contiguous range per wavefront
     uint32_t nt;               // bit0 non-temporal record stores, bit1 non-temporal header loads,
-                               // bit2 / bit3 force two-round / wide loads (A/B),
-                               // bit4 PAYLOAD windows loaded at the slot, not ahead (A/B)
+                               // bit2 / bit3 force two-round / wide loads (A/B)
     const uint8_t* dfa;        // PAYLOAD DFA pool (device), copied to dynamic LDS per block
     uint32_t dfa_bytes;        // 0: the program has no BT_K_PAYLOAD slot
     uint32_t prefixes;         // BT_BATCH_PREFIXES: base holds header prefixes only

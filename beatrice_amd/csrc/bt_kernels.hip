@@ -282,46 +282,12 @@ __device__ __forceinline__ uint32_t parse_packet(const uint32_t* row, uint32_t s
 
 __device__ uint4 g_zero16[8];                    // source of the loads that read nothing
 
-// A lane's payload window loaded ahead (bt_parse_filter_pipe issues the loads before the
-// tile's parse, so their latency hides behind it): the 16-B chunks from the window's aligned
-// start, and the window's offset in the first one. nch = 0: nothing was loaded (the lane does
-// not reach a PAYLOAD slot, or has no window).
-struct PayWin {
-    uint4 v[8];
-    uint32_t sh, nch;
-};
-
 // applyPayloadFilter's window of a frame (eval_payload's gates): its start offset in the
 // frame (po) and length L; L = 0 when the filter returns false without a search.
 __device__ __forceinline__ uint32_t payload_window(uint32_t len, const uint32_t* w0, uint32_t& po) {
     po = 14u + (byte_of(w0, 14) & 15u) * 4u;
     if (!(len >= 34u && be16_of(w0, 12) == 0x0800u) || len <= po) return 0u;
     return min(len - po, 100u);
-}
-
-__device__ __forceinline__ void issue_payload_loads(const MainArgs& a, uint64_t frame_off, uint32_t len,
-                                                    const uint32_t* w0, bool want, PayWin& pw) {
-    uint32_t po = 0;
-    const uint32_t L = want ? payload_window(len, w0, po) : 0u;
-    const uint64_t start = frame_off + po;
-    const uint64_t al = start & ~15ull;
-    pw.sh = (uint32_t)(start & 15ull);
-    pw.nch = L ? (pw.sh + L + 15u) >> 4 : 0u;
-    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
-#pragma unroll
-    for (uint32_t h = 0; h < 8u; h += 4u) {
-        if (__ballot(pw.nch > h) != 0ull) {   // wave-uniform: a group only when some lane needs it
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k) {
-                const uint64_t g = al + 16ull * (h + k);
-                const bool ok = (h + k < pw.nch) & (g + 16ull <= a.bytes);
-                pw.v[h + k] = ld16(ok ? a.base + g : zero, a.nt & 2u);
-            }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k) pw.v[h + k] = make_uint4(0, 0, 0, 0);
-        }
-    }
 }
 
 // The bit-parallel form (bt_regex_dfa.cpp "AST -> bit-parallel form"; blob layout there): an
@@ -423,21 +389,12 @@ __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint3
 
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
-                                                 uint32_t& staged_sh, const PayWin* pre) {
+                                                 uint32_t& staged_sh) {
     uint32_t po;
     const uint32_t L = payload_window(len, w0, po);
     if (!L) return 0u;
     const uint32_t K = *reinterpret_cast<const uint16_t*>(blob);
     if (K == 0xFFFFu && blob[6] != 1u) return blob[6] == 2u ? 1u : 0u;   // bit-parallel: always / never
-    if (staged_sh == ~0u && pre && pre->nch) {   // loaded ahead: into the row (free once PARSE is done)
-        staged_sh = pre->sh;
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k)
-            if (k < pre->nch) {
-                uint32_t* d = row + 4u * k;
-                d[0] = pre->v[k].x; d[1] = pre->v[k].y; d[2] = pre->v[k].z; d[3] = pre->v[k].w;
-            }
-    }
     if (staged_sh == ~0u) {
         const uint64_t start = frame_off + po;
         const uint64_t al = start & ~15ull;
@@ -573,8 +530,7 @@ __device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
 template <int F>
 __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const HotProgram& hot,
                                                   const uint8_t* dfa_lds, uint32_t* lrow, uint64_t my_off,
-                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot,
-                                                  const PayWin* pre = nullptr) {
+                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot) {
     const FilterIn x = filter_in([w0](uint32_t i) { return byte_of(w0, (int)i); }, len);
     uint32_t code = BT_DECIDE_PASS;
     slot = prog.n ? prog.n - 1u : 0u;
@@ -625,7 +581,7 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
         uint32_t r;
         if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
             r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
-              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh, pre) : 0u;
+              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh) : 0u;
         else
             r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
         if (open && r != 1u) {
@@ -1224,16 +1180,6 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
     const uint32_t need_max = REC != kRecNone ? kNeedParse : kNeedFilter;
     const HotProgram hot = hot_program(prog);
     bool wide = false;
-    // the first PAYLOAD slot: the lanes that reach it get their payload windows loaded ahead
-    uint32_t pay_first = ~0u;
-    if constexpr (FILTER == 2) {
-        if (!a.prefixes && !(a.nt & 16u))
-            for (uint32_t f = 0; f < prog.n; ++f)
-                if (prog.f[f].kind == BT_K_PAYLOAD) {
-                    pay_first = f;
-                    break;
-                }
-    }
 
     // prologue: descriptors of t and t + step, round A of t (waited), then stand-ins for
     // a tile's stores so the first iteration's waits count like every later one's
@@ -1257,21 +1203,6 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         window<10>(row, s, w0);
         if (REC != kRecNone)   // round B, before the next tile's loads
             wide = round_b(a, t, lane, st.qa0, img, row, s, my_off, my_len, live, st.wide, need_max, w0);
-
-        // The payload windows of the lanes whose chain reaches the first PAYLOAD slot (the
-        // slots before it pass), loaded now: they arrive while this tile parses and its
-        // record stores issue (issued after the filter, each window cost a full memory round
-        // trip per tile: C3 with /GET|POST/ first 1.35 against 0.49 ms without the slot).
-        PayWin pw;
-        if constexpr (FILTER == 2) {
-            bool want = live && pay_first != ~0u;
-            if (__ballot(want) != 0ull) {
-                const FilterIn x = filter_in([&w0](uint32_t i) { return byte_of(w0, (int)i); }, my_len);
-                for (uint32_t f = 0; f < pay_first; ++f)
-                    want = want && eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x) == 1u;
-            }
-            issue_payload_loads(a, my_off, live ? my_len : 0u, w0, want, pw);
-        }
 
         // next tile: round A from the descriptors loaded one tile ago, then the
         // descriptors of the tile after it
@@ -1305,8 +1236,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live,
-                                                        slot, FILTER == 2 ? &pw : nullptr);   // pw.nch = 0: not loaded
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);
@@ -1481,7 +1411,10 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
         else
             hipLaunchKernelGGL(kernel, dim3(g), dim3(kBlock), dyn, st, a, prog);
     };
-    if constexpr (FL < 0 && (REC == kRecTiled || REC == kRecNone)) {
+    // Not for PAYLOAD programs (F == 2): bt_parse_filter_main at its residency hides the window
+    // loads and the walk better than the pipe at 2 blocks/CU (C3 with /GET|POST/ first 0.885
+    // against 0.98 ms, filter-only 0.60 against 0.87; tools/payload_ab.py with BT_NO_PIPE).
+    if constexpr (FL < 0 && F != 2 && (REC == kRecTiled || REC == kRecNone)) {
         if (pf && a.desc && (a.nt & 1u) && use_pipe()) {
             // At most 2 blocks/CU (the residency is 3): with the filter slots evaluated side
             // by side, C3 0.491 against 0.498 ms and C4 0.915 against 0.948 at the residency

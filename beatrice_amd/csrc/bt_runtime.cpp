@@ -509,17 +509,15 @@ int run_device(bt_ctx* c, const bt_batch* b, const bt_outputs* o, hipStream_t st
     // BT_OPT_CACHE_DEFAULT turns both off, BT_OPT_NT_* force them on.
     if (c->opts.flags & BT_OPT_CACHE_DEFAULT) a.nt = 0;
     else a.nt = 3u;
+    // A program with a GPU PAYLOAD slot reads each frame's payload window right after its
+    // header window: header loads that keep their lines in L2 save those lines a second trip
+    // to HBM (C3 with /GET|POST/ first, filter-only: 0.60 against 0.92 ms; a slot that reads
+    // no window, 0.33 against 0.70; tools/payload_ab.py *_cache variants)
+    if (a.dfa_bytes && !(c->opts.flags & BT_OPT_NT_LOADS)) a.nt &= ~2u;
     if (c->opts.flags & BT_OPT_NT_STORES) a.nt |= 1u;
     if (c->opts.flags & BT_OPT_NT_LOADS) a.nt |= 2u;
     if (c->opts.flags & BT_OPT_WIDE_NEVER) a.nt |= 4u;
     if (c->opts.flags & BT_OPT_WIDE_ALWAYS) a.nt |= 8u;
-    // PAYLOAD windows are loaded ahead of the tile's parse (bt_parse_filter_pipe);
-    // BT_PAYLOAD_LATE=1 (A/B) loads them at the slot (eval_payload) instead.
-    static const bool late_payload = [] {
-        const char* e = getenv("BT_PAYLOAD_LATE");
-        return e && *e && *e != '0';
-    }();
-    if (late_payload) a.nt |= 16u;
     a.lean_lo = 0;
     if (lean && !(a.nt & 8u)) {   // frames over PCIe: lean round A, never the wide 128-B mode
         static const uint32_t lean_end = [] {   // A/B knobs: BT_LEAN_END, BT_LEAN_LO

@@ -44,7 +44,9 @@ def prog(kind, expr=None):
 VARIANTS = {"base": prog("base"), "last": prog("last", "GET|POST"), "first": prog("first", "GET|POST"),
             "first_dfa": prog("first", "GET|POST"), "ua": prog("first", "User-Agent: .*(bot|curl)"),
             "ua_dfa": prog("first", "User-Agent: .*(bot|curl)"), "dot": prog("first", "."),
-            "caret": prog("first", "^"), "caret_x": prog("first", "^x"), "caret_x_dfa": prog("first", "^x")}
+            "caret": prog("first", "^"), "caret_x": prog("first", "^x"), "caret_x_dfa": prog("first", "^x"),
+            "first_cache": prog("first", "GET|POST"), "caret_cache": prog("first", "^"),
+            "base_cache": prog("base")}
 
 
 def main():
@@ -57,6 +59,7 @@ def main():
     a = ap.parse_args()
     ctx = abi.Context(0)
     ctx_dfa = abi.Context(0, flags=abi.OPT_PAYLOAD_DFA)
+    ctx_cache = abi.Context(0, flags=abi.OPT_CACHE_DEFAULT)   # *_cache: default cache policy (no NT loads/stores)
     wl = dict(bench.WORKLOADS["c3"], payload="GET|POST")
     cap = bench.Capture(ctx, wl, a.packets, synth.SEEDS[synth.C3], 0, a.packets)
     run = cap.run
@@ -64,7 +67,7 @@ def main():
     names = a.variants.split(",")
     for rnd in range(a.rounds):
         for v in names:
-            c = ctx_dfa if v.endswith("_dfa") else ctx
+            c = ctx_dfa if v.endswith("_dfa") else ctx_cache if v.endswith("_cache") else ctx
             p = c.compile(VARIANTS[v])
             for rec in (int(x) for x in a.records.split(",")):
                 o = abi.Outputs(run.outs.records if rec else None, run.n, run.outs.verdict, run.outs.decide,
@@ -93,6 +96,7 @@ def main():
                               "header_window_bytes_per_packet": round(cap.win_bytes / run.n, 2)}), flush=True)
     run.free()
     ctx_dfa.close()
+    ctx_cache.close()
     ctx.close()
 
 
