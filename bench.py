@@ -401,9 +401,14 @@ def measure(name, wl, args, ctx, flags, dist, rank, world, strong):
     step_s = (t1 - t0) / args.steps
     # The main kernel's duration: the same K steps again, each main kernel between an
     # event pair recorded by its own dispatch. Those events cost the GPU ~9 us per step
-    # (tools/calib/boundary.hip), so they stay out of the timed region above.
-    tk = tm if args.kernel_events_in_timed else ctx.time_device2(run.batch, outs, args.steps,
-                                                                 mode | abi.TIME_KERNEL_EVENTS)
+    # (tools/calib/boundary.hip), so they stay out of the timed region above. A PAYLOAD
+    # program's main kernel fills every CU (bt_parse_filter_main at its residency), so in the
+    # pipelined form its dispatch events also span the previous step's compaction blocks it
+    # waits behind (1.35 ms between the events against 0.89 ms of kernel in the rocprofv3 trace
+    # of the same run): its kernel pass runs the compaction after each kernel instead.
+    kmode = 0 if wl.get("payload") else mode
+    tk = tm if args.kernel_events_in_timed else ctx.time_device2(run.batch, outs if kmode else outs[:1], args.steps,
+                                                                 kmode | abi.TIME_KERNEL_EVENTS)
 
     # algorithmic bytes of one main-kernel launch (SURVEY §8(d), R = the stored slabs):
     # min(len,128) header read + 8 B descriptor (0 for fixed stride) + R + 1 B decision
