@@ -135,9 +135,12 @@ public:
         // Header gather (bt_ring_gather_dense_tpv3): the walker packs each frame's header
         // prefix into registered slots and the kernels read those instead of the ring over
         // PCIe. inPlaceEvery = k > 0: every k-th batch is still read in
-        // place, sharing the work between the host's copy and the GPU's PCIe reads.
-        bool gather = false;
-        uint32_t inPlaceEvery = 0;
+        // place, sharing the work between the host's copy and the GPU's PCIe reads. The
+        // default since round 6 (gather, every other batch in place, lean prefixes for
+        // filter-only batches): bench.py's ring entry, C2 / C3 frames, 516 / 429 Mpps against
+        // 328 / 299 reading every batch in place (profiles/r06/bench_default_a.json).
+        bool gather = true;
+        uint32_t inPlaceEvery = 2;
         // Gathered batches that ask for no records pack only frame bytes 12..43
         // (bt_ring_gather_lean_tpv3, BT_BATCH_LEAN): the ring's e2e verdicts +17..45 % over the
         // full prefixes with inPlaceEvery = 2. false: the full prefixes.
