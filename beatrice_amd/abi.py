@@ -811,7 +811,7 @@ def ring_stage_tpv3(ctx: "Context", ring: np.ndarray, block_size: int, n_blocks:
     if slots is not None and slots.nbytes < cap * PREFIX_SLOT:
         raise ValueError("slots: need cap * PREFIX_SLOT bytes")
     r = Tpv3Ring(ring.ctypes.data, block_size, n_blocks, 0)
-    o = RingStageOpts(batch_blocks, int(gather), in_place_every, in_place_blocks)
+    o = RingStageOpts(batch_blocks, 2 if gather == "adaptive" else int(bool(gather)), in_place_every, in_place_blocks)
     nd, npass = ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib().bt_ring_stage_tpv3(ctx.h, ctypes.byref(r), first, n_blocks if count is None else count, ctypes.byref(o),
                                     desc.ctypes.data, None if slots is None else slots.ctypes.data,

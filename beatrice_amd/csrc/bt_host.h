@@ -23,6 +23,8 @@ int compile_program(const bt_filter_desc* f, uint32_t n, uint32_t ctx_flags, Com
 int install_program(bt_ctx* c, const CompiledProgram& p);
 uint32_t ctx_flags(const bt_ctx* c);
 int ctx_device(const bt_ctx* c);
+// Whether the context's stream still has queued work (hipStreamQuery: not ready).
+bool ctx_stream_busy(bt_ctx* c);
 // The CPUs the context's pool workers are pinned to (its device's NUMA node), or NULL.
 const cpu_set_t* ctx_pin(const bt_ctx* c);
 // Drops the context's cached "is this batch base host memory" answer (after an unregister).

@@ -387,9 +387,14 @@ __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint3
     return (H & F) ? 1u : 0u;
 }
 
+// `reuse`: the 16-B chunks of the frame's header window (from its 16-B-aligned start) that round
+// A left in the row (4 in descriptor mode with whole 64-B windows, else 0). The window's chunks
+// among them are moved down the row instead of read again: their lines were read a tile ago and
+// are often gone from L2 by now (C3 with /GET|POST/ first: 209 B read per packet against a
+// 131-B line floor).
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
-                                                 uint32_t& staged_sh) {
+                                                 uint32_t& staged_sh, uint32_t reuse) {
     uint32_t po;
     const uint32_t L = payload_window(len, w0, po);
     if (!L) return 0u;
@@ -400,20 +405,30 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
         const uint64_t al = start & ~15ull;
         staged_sh = (uint32_t)(start & 15ull);
         const uint32_t nch = (staged_sh + L + 15u) >> 4;   // <= 8: 128 B of the 132-B row
+        // window chunk k = header chunk d + k: those still in the row move down (d >= 2)
+        const uint32_t d = (uint32_t)((al - (frame_off & ~15ull)) >> 4);
+        const uint32_t kept = reuse > d ? min(reuse - d, nch) : 0u;
+        for (uint32_t k = 0; k < kept; ++k) {
+            uint32_t* dst = row + 4u * k;
+            const uint32_t* src = row + 4u * (k + d);
+            dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2]; dst[3] = src[3];
+        }
 #pragma unroll
         for (uint32_t h = 0; h < 8u; h += 4u) {
-            if (h < nch) {
+            if (h < nch && h + 4u > kept) {
                 uint4 v[4];
 #pragma unroll
                 for (uint32_t k = 0; k < 4u; ++k) {
                     const uint64_t g = al + 16ull * (h + k);
-                    v[k] = (h + k < nch && g + 16ull <= a.bytes) ? ld16(a.base + g, a.nt & 2u) : make_uint4(0, 0, 0, 0);
+                    v[k] = (h + k >= kept && h + k < nch && g + 16ull <= a.bytes) ? ld16(a.base + g, a.nt & 2u)
+                                                                                 : make_uint4(0, 0, 0, 0);
                 }
 #pragma unroll
-                for (uint32_t k = 0; k < 4u; ++k) {
-                    uint32_t* d = row + 4u * (h + k);
-                    d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
-                }
+                for (uint32_t k = 0; k < 4u; ++k)
+                    if (h + k >= kept) {
+                        uint32_t* q = row + 4u * (h + k);
+                        q[0] = v[k].x; q[1] = v[k].y; q[2] = v[k].z; q[3] = v[k].w;
+                    }
             }
         }
     }
@@ -530,7 +545,8 @@ __device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
 template <int F>
 __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const HotProgram& hot,
                                                   const uint8_t* dfa_lds, uint32_t* lrow, uint64_t my_off,
-                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot) {
+                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot,
+                                                  uint32_t reuse = 0u) {
     const FilterIn x = filter_in([w0](uint32_t i) { return byte_of(w0, (int)i); }, len);
     uint32_t code = BT_DECIDE_PASS;
     slot = prog.n ? prog.n - 1u : 0u;
@@ -581,7 +597,7 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
         uint32_t r;
         if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
             r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
-              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh) : 0u;
+              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh, reuse) : 0u;
         else
             r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
         if (open && r != 1u) {
@@ -966,7 +982,11 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevPr
         // ---- 3. FILTER ------------------------------------------------------
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            // round A's 64-B window (descriptor mode, whole windows, not a wide tile, whose
+            // line-bounded round A may stop short of it) is still in the row for PAYLOAD slots
+            const uint32_t reuse = FIXED_LOG2 < 0 && a.lean == 0xFFFFu && !this_wide ? 4u : 0u;
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live,
+                                                        slot, reuse);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             if (LATE) {   // unconditional buffer stores: a static count behind the next loads
                 const uint32_t cnt = min(64u, a.n - p0);

@@ -50,11 +50,16 @@ extern "C" int bt_ring_stage_tpv3(bt_ctx* ctx, const bt_tpv3_ring* ring, uint32_
     // with gather and in_place_blocks: each batch is two launches, its first blocks gathered and
     // its last in_place_blocks read in place, so the host's copies and the device's PCIe reads
     // share every batch instead of alternating between batches
-    const uint32_t split = o.gather && o.in_place_blocks ? std::min(o.in_place_blocks, per) : 0u;
+    const uint32_t split = o.gather == 1u && o.in_place_blocks ? std::min(o.in_place_blocks, per) : 0u;
+    // gather == 2 (adaptive): a batch is gathered when the device is still busy with the batches
+    // before it (the device is the bound: the host takes on the copies) and read in place when
+    // the device has caught up (the host is the bound: it only walks)
+    const bool adaptive = o.gather == 2u;
     uint32_t start = 0, done_blocks = 0, k = 0;
     while (done_blocks < n_blocks) {
         const uint32_t part = split ? (k & 1u) : 0u;   // split: even parts gathered, odd in place
-        const bool gathered = split ? part == 0u
+        const bool gathered = adaptive ? (k == 0u || bt::ctx_stream_busy(ctx))
+                            : split ? part == 0u
                                     : o.gather && !(o.in_place_every && k % o.in_place_every == o.in_place_every - 1);
         const uint32_t fb = (first_block + done_blocks) % ring->n_blocks;
         const uint32_t nb = std::min(split ? (part ? split : per - split) : per, n_blocks - done_blocks);

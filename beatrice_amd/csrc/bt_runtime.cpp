@@ -955,6 +955,12 @@ int install_program(bt_ctx* c, const CompiledProgram& p) {
 
 uint32_t ctx_flags(const bt_ctx* c) { return c->opts.flags; }
 int ctx_device(const bt_ctx* c) { return c->device; }
+
+bool ctx_stream_busy(bt_ctx* c) {
+    const bt::DeviceRestore keep_device;
+    if (hipSetDevice(c->device) != hipSuccess) return false;
+    return hipStreamQuery(c->stream) == hipErrorNotReady;
+}
 const cpu_set_t* ctx_pin(const bt_ctx* c) { return c->pinned ? &c->pin : nullptr; }
 void ctx_forget_base(bt_ctx* c) {
     std::lock_guard<std::mutex> lk(c->mu);

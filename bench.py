@@ -699,8 +699,9 @@ def measure_ring_stage(data: np.ndarray, desc: np.ndarray, node: int, reps: int 
     pass takes every block, the host walking (or lean-gathering) batch k+1 of 128 blocks while
     the GPU filters batch k over PCIe, decisions and verdict words back in registered host
     memory. PCIe-inclusive, never the line's `value`. Modes: in place (the stage's default), lean
-    gather on every other batch, lean gather on every batch, and every batch split (its last 40 or
-    56 of 128 blocks read in place, the rest gathered)."""
+    gather on every other batch, lean gather on every batch, every batch split (its last 40 of 128
+    blocks read in place, the rest gathered), and adaptive (a batch gathered while the device is
+    still busy, in place once it caught up; batches of 128 or 32 blocks)."""
     import time as _time
     from beatrice_amd import numa
     ring, rdesc, used = synth.tpv3_ring(data, desc)
@@ -728,7 +729,7 @@ def measure_ring_stage(data: np.ndarray, desc: np.ndarray, node: int, reps: int 
         ref_dec = None
         for mode, kw in (("in_place", {}), ("lean_every_other", dict(gather=True, in_place_every=2)),
                          ("lean_all", dict(gather=True)), ("lean_split_40", dict(gather=True, in_place_blocks=40)),
-                         ("lean_split_56", dict(gather=True, in_place_blocks=56))):
+                         ("adaptive", dict(gather="adaptive")), ("adaptive_32", dict(gather="adaptive", batch_blocks=32))):
             abi.ring_stage_tpv3(ctx, ring, synth.TPV3_BLOCK, used, rd, dec, ver, slots, **kw)   # warm
             times = []
             for _ in range(reps):

@@ -523,7 +523,9 @@ int  bt_ring_release_tpv3(const bt_tpv3_ring* ring, uint32_t first_block, uint32
  * PacketFilter::applyFilters (reference src/AF_PacketBackend.cpp:318-363). */
 typedef struct bt_ring_stage_opts {
     uint32_t batch_blocks;        /* blocks per kernel launch (0 = 128)                     */
-    uint32_t gather;              /* 1: pack bytes 12..43 of each frame (lean) before launch */
+    uint32_t gather;              /* 1: pack bytes 12..43 of each frame (lean) before launch;
+                                     2: adaptive: a batch is gathered while the device is still
+                                     busy with earlier batches, read in place once it caught up */
     uint32_t in_place_every;      /* with gather: every k-th batch read in place (0 = none)  */
     uint32_t in_place_blocks;     /* with gather: the last m blocks of every batch read in
                                      place, the rest gathered (0 = whole batches; overrides

@@ -315,7 +315,7 @@ def _stage(ctx, ring, bs, used, n, **kw):
 
 
 @pytest.mark.parametrize("cfg", [synth.C2, synth.C3, synth.C4, synth.FUZZ])
-@pytest.mark.parametrize("mode", ["in_place", "lean_mix", "lean_all", "lean_split"])
+@pytest.mark.parametrize("mode", ["in_place", "lean_mix", "lean_all", "lean_split", "adaptive"])
 def test_ring_stage_decides_as_the_oracle(gpu_ctx, cfg, mode):
     """The one-call ring stage (walk of batch k+1 overlapping the kernels of batch k; in place,
     lean gather on every other batch, lean gather on all): every frame of a 200k-frame ring in
@@ -326,7 +326,7 @@ def test_ring_stage_decides_as_the_oracle(gpu_ctx, cfg, mode):
     ring, rdesc, used = synth.tpv3_ring(data, desc0)
     gpu_ctx.compile(BUILTIN_C3)
     kw = {"in_place": {}, "lean_mix": dict(gather=True, in_place_every=2), "lean_all": dict(gather=True),
-          "lean_split": dict(gather=True, in_place_blocks=3)}[mode]
+          "lean_split": dict(gather=True, in_place_blocks=3), "adaptive": dict(gather="adaptive")}[mode]
     ring, got, npass, desc, dec, ver = _stage(gpu_ctx, ring, synth.TPV3_BLOCK, used, n, batch_blocks=7, **kw)
     assert got == len(rdesc) == n
     _, odec, onp = ol.oracle_run(ring, rdesc, n, BUILTIN_C3, parse=False)
