@@ -119,6 +119,18 @@ def kernel_source_sha() -> str:
     return h.hexdigest()[:16]
 
 
+_IMPORTED = time.time()
+
+
+def _process_start() -> float:
+    """This process's start (wall clock), from the OS; bench.py's import time without psutil."""
+    try:
+        import psutil
+        return psutil.Process().create_time()
+    except Exception:
+        return _IMPORTED
+
+
 def host_cpus() -> dict:
     """CPUs this process may run on: the affinity set, bounded by the cgroup v2/v1 CPU
     quota when one is set (threads past the quota only time-share it)."""
@@ -251,7 +263,10 @@ def main_kernel_name(wl, flags: int = 0) -> str:
     no_pipe = os.environ.get("BT_NO_PIPE", "") not in ("", "0")
     layout = flags & (abi.OPT_RECORDS_AOS | abi.OPT_RECORDS_PLANES)
     nt_stores = not (flags & abi.OPT_CACHE_DEFAULT) or (flags & abi.OPT_NT_STORES)
-    pipe = not (wl["fixed"] or no_pipe or layout or (flags & abi.OPT_NO_PREFETCH) or not nt_stores)
+    # a program with a GPU PAYLOAD slot runs the main kernel at its residency (launch_t's F == 2)
+    gpu_payload = any(f["type"] == abi.PAYLOAD for f in (wl.get("filters") or [])) and \
+        not (flags & abi.OPT_PAYLOAD_HOST)
+    pipe = not (wl["fixed"] or no_pipe or layout or (flags & abi.OPT_NO_PREFETCH) or not nt_stores or gpu_payload)
     return "bt_parse_filter_pipe" if pipe else "bt_parse_filter_main"
 
 
@@ -972,7 +987,11 @@ def main():
         dist.barrier()
 
     if rank == 0:
-        print(json.dumps(build_line(results, args, world, devices)), flush=True)
+        line = build_line(results, args, world, devices)
+        # rank 0's process age at the line (imports, every entry, the CPU baselines and the
+        # group entry): what to hold against the driver's per-run limit
+        line["job_wall_s"] = round(time.time() - _process_start(), 1)
+        print(json.dumps(line), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -78,6 +78,9 @@ def test_main_kernel_name(monkeypatch):
     assert bench.main_kernel_name(bench.WORKLOADS["c3"], abi.OPT_CACHE_DEFAULT) == "bt_parse_filter_main"
     assert bench.main_kernel_name(bench.WORKLOADS["c3"],
                                   abi.OPT_CACHE_DEFAULT | abi.OPT_NT_STORES) == "bt_parse_filter_pipe"
+    # a GPU PAYLOAD slot: the main kernel at its residency (launch_t's F == 2); host slots keep the pipe
+    assert bench.main_kernel_name(bench.WORKLOADS["c3_payload"]) == "bt_parse_filter_main"
+    assert bench.main_kernel_name(bench.WORKLOADS["c3_payload"], abi.OPT_PAYLOAD_HOST) == "bt_parse_filter_pipe"
     monkeypatch.setenv("BT_NO_PIPE", "1")
     assert bench.main_kernel_name(bench.WORKLOADS["c3"]) == "bt_parse_filter_main"
 
