@@ -355,6 +355,9 @@ __device__ __forceinline__ uint32_t bitpar_walk(const uint8_t* blob, const uint3
 // are then ((D << 1) | I) & B[c] and an OR of the states (H; a match ended where H & F is
 // set): about 4 VALU per byte against 8 with the bound checks, which made the walk VALU-bound
 // (C3 /GET|POST/ first: 123 k VALU per wave of the 129 k the walk added, SQ counters).
+// Reading the window one LDS byte per byte instead (no alignbyte / extraction; the compiler
+// merges the reads into unaligned 8-byte LDS reads and adds with byte selects) was slower
+// filter-only, 0.708-0.718 against 0.663-0.670 ms (profiles/r06/payload/libs_bytes_wpe4.log).
 template <typename E>
 __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint32_t* row, uint32_t staged_sh,
                                                 uint32_t L) {
@@ -363,14 +366,14 @@ __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint3
     const E* B = reinterpret_cast<const E*>(blob + 80);
     const uint32_t* r = row + (staged_sh >> 2);
     const uint32_t sh = staged_sh & 3u, rmax = 31u - (staged_sh >> 2);
-    uint32_t D = 0, H = 0;
     uint32_t t0 = r[0], t1 = r[1], t2 = r[2];
+    uint32_t D = 0, H = 0;
     for (uint32_t i = 0;; i += 8u) {
+        uint32_t b[8];
         const uint32_t w0 = __builtin_amdgcn_alignbyte(t1, t0, sh), w1 = __builtin_amdgcn_alignbyte(t2, t1, sh);
         t0 = t2;
         t1 = r[min((i >> 2) + 3u, rmax)];
         t2 = r[min((i >> 2) + 4u, rmax)];
-        uint32_t b[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             b[k] = B[(w0 >> (8 * k)) & 0xFFu];
@@ -837,8 +840,20 @@ constexpr bool late_issue(int fixed_log2, int rec, int filter, bool prefetch) {
     return fixed_log2 >= 0 && !prefetch && rec != kRecAoS && filter == 1;
 }
 
+// Waves per SIMD the compiler must fit bt_parse_filter_main into (1: no constraint). PAYLOAD
+// programs in descriptor mode: 4, the LDS residency (4 blocks/CU), so that the register budget
+// (128 VGPRs) does not hold the kernel at 3 and the window loads and the walk have a fourth
+// wave to hide behind (C3 with /GET|POST/ first, records: 0.818-0.836 against 0.908-0.917 ms,
+// with /GET|POST/ last 0.773-0.777 against 0.912-0.916; tools/gpu_payload_libs.sh,
+// profiles/r06/payload/libs_wpe4.log). launch_t runs those programs without the next-tile
+// prefetch, whose registers would spill at 128 (as would AoS records').
+constexpr int main_waves_per_eu(int fixed_log2, int rec, int filter, bool prefetch) {
+    return fixed_log2 < 0 && filter == 2 && !prefetch && rec != kRecAoS ? 4 : 1;
+}
+
 template <int FIXED_LOG2, int REC, int FILTER, bool PREFETCH>
-__global__ __launch_bounds__(kBlock) void bt_parse_filter_main(MainArgs a, DevProgram prog) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(main_waves_per_eu(FIXED_LOG2, REC, FILTER, PREFETCH))))
+void bt_parse_filter_main(MainArgs a, DevProgram prog) {
     // Per-wave LDS image: 64 rows x 33 dwords.
     constexpr uint32_t kRow = row_dw<FIXED_LOG2>();
     // a wave's image; with AoS records at least the tile's 6 KiB of bt_rec (staged below)
@@ -1454,7 +1469,24 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
         const char* e = getenv("BT_FIXED_PREFETCH");
         return e && *e && *e != '0';
     }();
+    // PAYLOAD programs in descriptor mode: no next-tile prefetch (main_waves_per_eu)
+    if (FL < 0 && F == 2) pf = false;
+    // PAYLOAD programs in descriptor mode run one block per kBlock / 64 tiles, not one residency
+    // wave of blocks: without the prefetch there is nothing for a persistent block to carry from
+    // tile to tile, and a residency grid that fills every CU leaves none for the previous step's
+    // compaction, so that some of its blocks start only when others end (C3 with /GET|POST/
+    // first, pipelined steps: 0.771-0.775 ms against 1.080-1.142 at the residency and 0.892-0.895
+    // at 3 blocks/CU; tools/gpu_payload_grid.sh, profiles/r06/payload/grid/).
+    // BT_PAYLOAD_GRID (A/B): blocks per CU instead, 0 = the residency.
+    static const int pay_grid = [] {
+        const char* e = getenv("BT_PAYLOAD_GRID");
+        return e && *e ? atoi(e) : -1;
+    }();
     if (pf && (FL < 0 || fixed_pf)) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
+    else if (FL < 0 && F == 2 && grid <= 0 && pay_grid)
+        go(bt_parse_filter_main<FL, REC, F, false>,
+           pay_grid < 0 ? (int)needed
+                        : std::min(pay_grid * cu_count(), resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn)));
     else go(bt_parse_filter_main<FL, REC, F, false>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn));
 }
 

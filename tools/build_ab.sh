@@ -11,6 +11,7 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Iinclud
 $H $FLAGS -c beatrice_amd/csrc/bt_kernels.hip -o $D/bt_kernels.o
 g++ -O2 -fPIC -std=c++17 -Wall -Iinclude -Ibeatrice_amd/csrc $RING_FLAGS -c beatrice_amd/csrc/bt_ring.cpp -o $D/bt_ring.o
 $H -shared -fPIC -o $D/libbeatrice_gpu.so $D/bt_kernels.o $D/bt_ring.o $O/bt_extract.o $O/bt_ring_walk.o \
-    $O/bt_runtime.o $O/bt_filter_compile.o $O/bt_regex_dfa.o $O/bt_format.o $O/bt_group.o
+    $O/bt_runtime.o $O/bt_filter_compile.o $O/bt_ring_stage.o $O/bt_regex_dfa.o $O/bt_format.o $O/bt_group.o \
+    $O/bt_pin.o
 rm -f $D/bt_kernels.o $D/bt_ring.o
 echo built $D
