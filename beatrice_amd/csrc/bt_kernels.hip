@@ -303,13 +303,13 @@ __device__ __forceinline__ uint32_t payload_window(uint32_t len, const uint32_t*
 // over the L bytes.
 template <typename E, bool SIMPLE>
 __device__ __forceinline__ uint32_t bitpar_walk(const uint8_t* blob, const uint32_t* row, uint32_t staged_sh,
-                                                uint32_t L) {
+                                                uint32_t L, uint32_t rdw) {
     using T = typename std::conditional<sizeof(E) == 8, uint64_t, uint32_t>::type;
     const uint64_t* mk = reinterpret_cast<const uint64_t*>(blob + 16);
     const T Iall = (T)mk[0], F = (T)mk[5];
     const E* B = reinterpret_cast<const E*>(blob + 80);
     const uint32_t* r = row + (staged_sh >> 2);
-    const uint32_t sh = staged_sh & 3u, rmax = 31u - (staged_sh >> 2);   // r[] stays inside the 33-dword row
+    const uint32_t sh = staged_sh & 3u, rmax = rdw - 2u - (staged_sh >> 2);   // r[] stays inside the row
     // the general form's masks (SIMPLE: none of them is used)
     const T I0 = SIMPLE ? (T)0 : (T)mk[1], S = SIMPLE ? (T)0 : (T)mk[2], A = SIMPLE ? (T)0 : (T)mk[3];
     const T NF = SIMPLE ? ~(T)0 : (T)mk[4], Fe = SIMPLE ? (T)0 : (T)mk[6];
@@ -360,12 +360,12 @@ __device__ __forceinline__ uint32_t bitpar_walk(const uint8_t* blob, const uint3
 // filter-only, 0.708-0.718 against 0.663-0.670 ms (profiles/r06/payload/libs_bytes_wpe4.log).
 template <typename E>
 __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint32_t* row, uint32_t staged_sh,
-                                                uint32_t L) {
+                                                uint32_t L, uint32_t rdw) {
     const uint64_t* mk = reinterpret_cast<const uint64_t*>(blob + 16);
     const uint32_t Iall = (uint32_t)mk[0], F = (uint32_t)mk[5];
     const E* B = reinterpret_cast<const E*>(blob + 80);
     const uint32_t* r = row + (staged_sh >> 2);
-    const uint32_t sh = staged_sh & 3u, rmax = 31u - (staged_sh >> 2);
+    const uint32_t sh = staged_sh & 3u, rmax = rdw - 2u - (staged_sh >> 2);   // the row's last padded dword
     uint32_t t0 = r[0], t1 = r[1], t2 = r[2];
     uint32_t D = 0, H = 0;
     for (uint32_t i = 0;; i += 8u) {
@@ -395,9 +395,14 @@ __device__ __forceinline__ uint32_t bitpar_fast(const uint8_t* blob, const uint3
 // among them are moved down the row instead of read again: their lines were read a tile ago and
 // are often gone from L2 by now (C3 with /GET|POST/ first: 209 B read per packet against a
 // 131-B line floor).
+//
+// `rdw`: the row's dwords (row_dw: 33 in descriptor mode, 17 for 64-B fixed strides). The window,
+// its padding and the walks' reads stay inside the lane's own row: the padding written past
+// a 17-dword row once overwrote the next lane's staged window (64-B fixed-stride batches,
+// tests/test_gpu_payload.py::test_fixed_stride_payload).
 __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_t* blob, uint32_t* row,
                                                  uint64_t frame_off, uint32_t len, const uint32_t* w0,
-                                                 uint32_t& staged_sh, uint32_t reuse) {
+                                                 uint32_t& staged_sh, uint32_t reuse, uint32_t rdw) {
     uint32_t po;
     const uint32_t L = payload_window(len, w0, po);
     if (!L) return 0u;
@@ -407,7 +412,8 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
         const uint64_t start = frame_off + po;
         const uint64_t al = start & ~15ull;
         staged_sh = (uint32_t)(start & 15ull);
-        const uint32_t nch = (staged_sh + L + 15u) >> 4;   // <= 8: 128 B of the 132-B row
+        // <= 8: 128 B of the 132-B row; a 64-B fixed-stride frame's window ends by row byte 32
+        const uint32_t nch = min((staged_sh + L + 15u) >> 4, (rdw - 1u) >> 2);
         // window chunk k = header chunk d + k: those still in the row move down (d >= 2)
         const uint32_t d = (uint32_t)((al - (frame_off & ~15ull)) >> 4);
         const uint32_t kept = reuse > d ? min(reuse - d, nch) : 0u;
@@ -445,19 +451,19 @@ __device__ __forceinline__ uint32_t eval_payload(const MainArgs& a, const uint8_
             const uint32_t end = staged_sh + L, q = end >> 2, zz = (z - 1u) * 0x01010101u;
             const uint32_t keep = (end & 3u) ? (1u << (8u * (end & 3u))) - 1u : 0u;
             row[q] = (row[q] & keep) | (zz & ~keep);
-            for (uint32_t k = q + 1u; k < 33u; ++k) row[k] = zz;
-            return W == 8 ? bitpar_fast<uint8_t>(blob, row, staged_sh, L)
-                 : W == 16 ? bitpar_fast<uint16_t>(blob, row, staged_sh, L)
-                           : bitpar_fast<uint32_t>(blob, row, staged_sh, L);
+            for (uint32_t k = q + 1u; k < rdw; ++k) row[k] = zz;
+            return W == 8 ? bitpar_fast<uint8_t>(blob, row, staged_sh, L, rdw)
+                 : W == 16 ? bitpar_fast<uint16_t>(blob, row, staged_sh, L, rdw)
+                           : bitpar_fast<uint32_t>(blob, row, staged_sh, L, rdw);
         }
         switch (W) {
-        case 8: return simple ? bitpar_walk<uint8_t, true>(blob, row, staged_sh, L)
-                              : bitpar_walk<uint8_t, false>(blob, row, staged_sh, L);
-        case 16: return simple ? bitpar_walk<uint16_t, true>(blob, row, staged_sh, L)
-                               : bitpar_walk<uint16_t, false>(blob, row, staged_sh, L);
-        case 32: return simple ? bitpar_walk<uint32_t, true>(blob, row, staged_sh, L)
-                               : bitpar_walk<uint32_t, false>(blob, row, staged_sh, L);
-        default: return bitpar_walk<uint64_t, false>(blob, row, staged_sh, L);
+        case 8: return simple ? bitpar_walk<uint8_t, true>(blob, row, staged_sh, L, rdw)
+                              : bitpar_walk<uint8_t, false>(blob, row, staged_sh, L, rdw);
+        case 16: return simple ? bitpar_walk<uint16_t, true>(blob, row, staged_sh, L, rdw)
+                               : bitpar_walk<uint16_t, false>(blob, row, staged_sh, L, rdw);
+        case 32: return simple ? bitpar_walk<uint32_t, true>(blob, row, staged_sh, L, rdw)
+                               : bitpar_walk<uint32_t, false>(blob, row, staged_sh, L, rdw);
+        default: return bitpar_walk<uint64_t, false>(blob, row, staged_sh, L, rdw);
         }
     }
     const uint32_t C = *reinterpret_cast<const uint16_t*>(blob + 2);
@@ -547,9 +553,9 @@ __device__ __forceinline__ HotProgram hot_program(const DevProgram& prog) {
 
 template <int F>
 __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevProgram& prog, const HotProgram& hot,
-                                                  const uint8_t* dfa_lds, uint32_t* lrow, uint64_t my_off,
-                                                  uint32_t len, const uint32_t* w0, bool live, uint32_t& slot,
-                                                  uint32_t reuse = 0u) {
+                                                  const uint8_t* dfa_lds, uint32_t* lrow, uint32_t rdw,
+                                                  uint64_t my_off, uint32_t len, const uint32_t* w0, bool live,
+                                                  uint32_t& slot, uint32_t reuse = 0u) {
     const FilterIn x = filter_in([w0](uint32_t i) { return byte_of(w0, (int)i); }, len);
     uint32_t code = BT_DECIDE_PASS;
     slot = prog.n ? prog.n - 1u : 0u;
@@ -600,7 +606,7 @@ __device__ __forceinline__ uint32_t filter_packet(const MainArgs& a, const DevPr
         uint32_t r;
         if (prog.f[f].kind == BT_K_PAYLOAD)   // wave-uniform
             r = a.prefixes ? 3u   // the payload is not in a prefix batch: host
-              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh, reuse) : 0u;
+              : open ? eval_payload(a, dfa_lds + prog.f[f].a, lrow, my_off, len, w0, staged_sh, reuse, rdw) : 0u;
         else
             r = eval_slot(prog.f[f].kind, prog.f[f].a, prog.f[f].b, x);
         if (open && r != 1u) {
@@ -1000,7 +1006,7 @@ void bt_parse_filter_main(MainArgs a, DevProgram prog) {
             // round A's 64-B window (descriptor mode, whole windows, not a wide tile, whose
             // line-bounded round A may stop short of it) is still in the row for PAYLOAD slots
             const uint32_t reuse = FIXED_LOG2 < 0 && a.lean == 0xFFFFu && !this_wide ? 4u : 0u;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live,
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, kRow, my_off, len, w0, live,
                                                         slot, reuse);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             if (LATE) {   // unconditional buffer stores: a static count behind the next loads
@@ -1271,7 +1277,7 @@ __global__ __launch_bounds__(kBlock) void bt_parse_filter_pipe(MainArgs a, DevPr
         // ---- FILTER ----
         if (FILTER) {
             uint32_t slot;
-            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, my_off, len, w0, live, slot);
+            const uint32_t code = filter_packet<FILTER>(a, prog, hot, dfa_lds, img + lane * kRow, kRow, my_off, len, w0, live, slot);
             const uint64_t pass = __ballot(live && code == BT_DECIDE_PASS);
             const uint32_t cnt = min(64u, a.n - p0);
             const auto rd = rsrc_of(a.decide ? a.decide + p0 : nullptr, a.decide ? cnt : 0u);

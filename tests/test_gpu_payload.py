@@ -178,3 +178,46 @@ def test_bitpar_and_dfa_forms_agree(cfg):
     finally:
         dfa.close()
         bp.close()
+
+
+@pytest.mark.parametrize("stride", [64, 128])
+def test_fixed_stride_payload(gpu_ctx, stride):
+    """Fixed-stride batches (no descriptors): 64-B frames use LDS rows of 17 dwords, not 33, so
+    the window staging, its padding and the walks must stay inside them; matches planted at
+    every offset of the window, frames with IP options and non-IPv4 frames, decided as the
+    descriptor path and the compiled reference decide them."""
+    rng = np.random.default_rng(stride)
+    n = 64 * 300 + 17
+    frames = []
+    for i in range(n):
+        f = bytearray(rng.integers(0, 256, stride, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00" if i % 11 else b"\x86\xdd"
+        ihl = 5 + (i % 7 == 0) * (i % 5)
+        f[14] = 0x40 | ihl
+        po = 14 + 4 * ihl
+        w = (b"GET", b"POST", b"GE", b"xPOSTx")[i % 4]
+        at = po + (i * 7) % max(1, stride - po - len(w) + 1)
+        if i % 3 and at + len(w) <= stride:
+            f[at:at + len(w)] = w
+        frames.append(bytes(f))
+    data, desc = synth.pack_frames(frames, align=stride)
+    assert np.all(synth.desc_off(desc) == np.arange(n) * stride)
+    for expr in ("GET|POST", "ST$|^x?G", "[\\x80-\\xff]{3}|\\d\\d"):
+        f = [{"type": abi.PAYLOAD, "expr": expr, "priority": 1}]
+        assert abi.KINDS[gpu_ctx.compile(f)[0].kind] == "PAYLOAD"
+        run = abi.DeviceRun(gpu_ctx, data[: n * stride], None, n, stride=stride, records=False)
+        run.run()
+        fixed = run.fetch()["decide"]
+        run.free()
+        by_desc = _run(gpu_ctx, data, desc)["decide"]
+        bad = np.nonzero(fixed != by_desc)[0]
+        assert len(bad) == 0, f"/{expr}/ stride {stride}: {len(bad)} fixed-stride decisions differ, first {bad[:5]}"
+        blob = abi.payload_dfa(expr)
+        want = np.array([abi.payload_dfa_eval(blob, data[i * stride:(i + 1) * stride]) for i in range(n)])
+        got = (fixed >> 6) == 0
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, f"/{expr}/ stride {stride}: {len(bad)} differ from the host executor, first {bad[:5]}"
+        assert 0 < want.sum() < n
+        if ol.ref_available():
+            code, src = ol.ref_filter(data, desc, n, f)
+            compare_decisions(fixed, code, src, f, where=f"fixed{stride}/{expr}")
