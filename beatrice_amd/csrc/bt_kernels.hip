@@ -1477,21 +1477,23 @@ void launch_t(const MainArgs& a, const DevProgram& prog, int grid, bool pf, hipS
     }();
     // PAYLOAD programs in descriptor mode: no next-tile prefetch (main_waves_per_eu)
     if (FL < 0 && F == 2) pf = false;
-    // PAYLOAD programs in descriptor mode run one block per kBlock / 64 tiles, not one residency
-    // wave of blocks: without the prefetch there is nothing for a persistent block to carry from
-    // tile to tile, and a residency grid that fills every CU leaves none for the previous step's
-    // compaction, so that some of its blocks start only when others end (C3 with /GET|POST/
-    // first, pipelined steps: 0.771-0.775 ms against 1.080-1.142 at the residency and 0.892-0.895
-    // at 3 blocks/CU; tools/gpu_payload_grid.sh, profiles/r06/payload/grid/).
-    // BT_PAYLOAD_GRID (A/B): blocks per CU instead, 0 = the residency.
+    // PAYLOAD programs in descriptor mode run one block per 12 tiles (three per wave), not one
+    // residency wave of blocks: without the prefetch there is nothing for a persistent block to
+    // carry from tile to tile, and a residency grid that fills every CU leaves none for the
+    // previous step's compaction, so that some of its blocks start only when others end (C3 with
+    // /GET|POST/ first, pipelined steps: 0.771-0.775 ms at one tile per wave against 1.080-1.142
+    // at the residency and 0.892-0.895 at 3 blocks/CU; two / three / four / eight / sixteen tiles
+    // per wave 0.775-0.778 / 0.753 / 0.756-0.759 / 0.764-0.767 / 0.803 ms; tools/gpu_payload_grid.sh,
+    // profiles/r06/payload/grid/).
+    // BT_PAYLOAD_GRID (A/B): blocks per CU instead, 0 = the residency, -k = one block per 4k tiles.
     static const int pay_grid = [] {
         const char* e = getenv("BT_PAYLOAD_GRID");
-        return e && *e ? atoi(e) : -1;
+        return e && *e ? atoi(e) : -3;
     }();
     if (pf && (FL < 0 || fixed_pf)) go(bt_parse_filter_main<FL, REC, F, true>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, true>>(dyn));
     else if (FL < 0 && F == 2 && grid <= 0 && pay_grid)
         go(bt_parse_filter_main<FL, REC, F, false>,
-           pay_grid < 0 ? (int)needed
+           pay_grid < 0 ? (int)((needed + (uint32_t)(-pay_grid) - 1u) / (uint32_t)(-pay_grid))
                         : std::min(pay_grid * cu_count(), resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn)));
     else go(bt_parse_filter_main<FL, REC, F, false>, grid > 0 ? 0 : resident_grid<bt_parse_filter_main<FL, REC, F, false>>(dyn));
 }
