@@ -238,7 +238,8 @@ REGEX_POOL = ["GET", "[\\x00-\\x1f][a-z]", "^..?\\d", "MAG+IC", "a|b", "\\d\\d",
 def test_randomized_payload_programs_vs_reference():
     """The same sweep with GPU PAYLOAD slots (regexes compiled to DFAs) between built-ins,
     checked against the compiled reference's own PacketFilter (std::regex per packet), on
-    host, device-resident and zero-copy mapped batches. Runs BT_FUZZ_SECONDS / 3."""
+    host, device-resident, zero-copy mapped and fixed-stride batches (C2's 64-B frames, whose
+    LDS rows are 17 dwords). Runs BT_FUZZ_SECONDS / 3."""
     from golden_util import compare_decisions
     seconds = float(os.environ.get("BT_FUZZ_SECONDS", "15")) / 3
     seed0 = _seed() ^ 0x9A
@@ -250,8 +251,9 @@ def test_randomized_payload_programs_vs_reference():
     t_end = time.time() + seconds
     rounds = 0
     try:
-        while time.time() < t_end or rounds < 3:
-            cfg = [synth.C3, synth.C4, synth.FUZZ][int(rng.integers(0, 3))]
+        while time.time() < t_end or rounds < 4:
+            form = ("host", "device", "mapped", "fixed")[rounds % 4]
+            cfg = [synth.C3, synth.C4, synth.FUZZ][int(rng.integers(0, 3))] if form != "fixed" else synth.C2
             n = int(rng.integers(1, 3000))
             data, desc = synth.capture(cfg, n, seed=int(rng.integers(1, 1 << 30)))
             if data.nbytes < 64:
@@ -261,7 +263,6 @@ def test_randomized_payload_programs_vs_reference():
                 prog.insert(int(rng.integers(0, len(prog) + 1)),
                             {"type": abi.PAYLOAD, "expr": REGEX_POOL[int(rng.integers(0, len(REGEX_POOL)))],
                              "priority": 40 + k})
-            form = ("host", "device", "mapped")[rounds % 3]
             where = f"payload round {rounds} form {form} cfg {cfg} n {n} program {prog}"
             if form == "mapped":
                 grp.compile(prog)
@@ -270,6 +271,11 @@ def test_randomized_payload_programs_vs_reference():
                 ctx.compile(prog)
                 if form == "host":
                     out = ctx.run_host(data, desc, records=False)
+                elif form == "fixed":   # no descriptors: frame i at i * 64
+                    r = abi.DeviceRun(ctx, data[: n * 64], None, n, stride=64, records=False)
+                    r.run()
+                    out = r.fetch()
+                    r.free()
                 else:
                     r = abi.DeviceRun(ctx, data, desc, n, records=False)
                     r.run()
