@@ -12,7 +12,8 @@ that differ only in their PAYLOAD slot, alternating variants round by round in o
   dot         PAYLOAD /./ first: staged, then decided on the first byte
   caret       PAYLOAD /^/ first: the bit-parallel compiler folds it to "always" (no window read)
   caret_x     PAYLOAD /^x/ first: every window loaded and staged, the search over after one turn
-  *_cache     the same under a BT_OPT_CACHE_DEFAULT context; *_nopf under BT_OPT_NO_PREFETCH
+  *_cache     the same under a BT_OPT_CACHE_DEFAULT context; *_nopf under BT_OPT_NO_PREFETCH;
+              *_wide under BT_OPT_WIDE_ALWAYS
 each with records (parse + filter) and without (filter only).
 
 Usage: python tools/payload_ab.py [--packets N] [--steps K] [--rounds R] [--variants a,b]
@@ -49,7 +50,8 @@ VARIANTS = {"base": prog("base"), "last": prog("last", "GET|POST"), "first": pro
             "first_cache": prog("first", "GET|POST"), "caret_cache": prog("first", "^"),
             "base_cache": prog("base"), "first_nopf": prog("first", "GET|POST"), "base_nopf": prog("base"),
             "caret_x_nopf": prog("first", "^x"), "last_nopf": prog("last", "GET|POST"),
-            "ua_nopf": prog("first", "User-Agent: .*(bot|curl)")}
+            "ua_nopf": prog("first", "User-Agent: .*(bot|curl)"), "first_wide": prog("first", "GET|POST"),
+            "last_wide": prog("last", "GET|POST"), "caret_x_wide": prog("first", "^x")}
 
 
 def main():
@@ -64,6 +66,7 @@ def main():
     ctx_dfa = abi.Context(0, flags=abi.OPT_PAYLOAD_DFA)
     ctx_cache = abi.Context(0, flags=abi.OPT_CACHE_DEFAULT)   # *_cache: default cache policy (no NT loads/stores)
     ctx_nopf = abi.Context(0, flags=abi.OPT_NO_PREFETCH)      # *_nopf: the main kernel without the next-tile prefetch
+    ctx_wide = abi.Context(0, flags=abi.OPT_WIDE_ALWAYS)      # *_wide: round A reads chunks 4..7 too
     wl = dict(bench.WORKLOADS["c3"], payload="GET|POST")
     cap = bench.Capture(ctx, wl, a.packets, synth.SEEDS[synth.C3], 0, a.packets)
     run = cap.run
@@ -72,7 +75,7 @@ def main():
     for rnd in range(a.rounds):
         for v in names:
             c = ctx_dfa if v.endswith("_dfa") else ctx_cache if v.endswith("_cache") else \
-                ctx_nopf if v.endswith("_nopf") else ctx
+                ctx_nopf if v.endswith("_nopf") else ctx_wide if v.endswith("_wide") else ctx
             p = c.compile(VARIANTS[v])
             for rec in (int(x) for x in a.records.split(",")):
                 o = abi.Outputs(run.outs.records if rec else None, run.n, run.outs.verdict, run.outs.decide,
